@@ -1,0 +1,211 @@
+#!/usr/bin/env python3
+"""bench.py -- device-resident index-build keys/s on MI355X (BASELINE.json metric).
+
+One step = the hot path over the whole synthetic key set that is resident in
+HBM: SpookyHash-short per key -> GOV bucket -> bucket-occupancy histogram
+(two-pass partitioned kernels) -> [N>1: RCCL all-reduce of the histogram over
+xGMI] -> edge offsets E[] (the low 56 bits of edgeOffsetAndSeed).
+
+Workload (default): BASELINE.json config 4, the README dataset shape,
+n = 13 193 787 549 keys x 13 bytes (171.5 GB), exact index, hash.checksum.bits=4,
+m = n/1500+1 = 8 795 859 buckets.  It fits one MI355X, so N=1 runs the whole
+set; with --gpus N the same key set is sharded N ways (strong scaling).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--n KEYS] [--no-cpu]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+README_N = 13_193_787_549     # README.md:50-60 record count
+KEY_LEN = 13
+HBM_PEAK_GBS = 8000.0         # MI355X_MICROARCH.md chip table: 8.0 TB/s HBM3E
+TILE = 8192                   # pass-1 tile: shard boundaries stay tile aligned
+
+
+def shard(n: int, rank: int, world: int):
+    """Contiguous key shard of rank r, tile aligned (by input order)."""
+    tiles = (n + TILE - 1) // TILE
+    lo = tiles * rank // world * TILE
+    hi = min(n, tiles * (rank + 1) // world * TILE)
+    return lo, hi
+
+
+def cpu_baseline(m: int, target_s: float, threads: int):
+    """The oracle's multi-threaded hash+bucket+histogram on resident 13-byte keys
+    (same key recipe, same m), timed on this box's host cores; bounded sample."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    calib_n = 4_000_000
+    keys = O.gen_keys13_mt(0, calib_n, threads)
+    _, dt = O.histogram_fixed_mt(keys, KEY_LEN, m, threads)
+    rate = calib_n / max(dt, 1e-6)
+    n = int(min(max(rate * target_s, calib_n), 400_000_000))
+    keys = O.gen_keys13_mt(0, n, threads)
+    total_keys, total_s = 0, 0.0
+    passes = 0
+    while total_s < target_s * 0.9 or passes == 0:
+        _, dt = O.histogram_fixed_mt(keys, KEY_LEN, m, threads)
+        total_keys += n
+        total_s += dt
+        passes += 1
+        if passes >= 8:
+            break
+    del keys
+    return {"value": total_keys / total_s, "unit": "keys/s", "cores": threads, "kind": "port",
+            "sample": f"{passes} pass(es) over {n} resident 13-byte keys (first {n} of the workload's key recipe), "
+                      f"m={m}, {total_s:.1f} s of CPU work, {threads} threads, "
+                      f"oracle bo_histogram_fixed_mt (C restatement pinned to the reference's spooky.c)"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--n", type=int, default=README_N, help="total keys (all ranks)")
+    ap.add_argument("--mode", type=int, default=0, help="0 auto/partitioned, 2 direct atomics")
+    ap.add_argument("--chunk", type=int, default=0, help="keys per partitioned chunk (0 = default)")
+    ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            raise SystemExit("--gpus N>1 must be launched with torch.distributed.run (one rank per GPU)")
+    torch.cuda.set_device(local_rank)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    from bsdb_amd import Context
+    ctx = Context(local_rank)
+    if args.mode:
+        ctx.set_histogram_mode(args.mode)
+    if args.chunk:
+        ctx.set_chunk_keys(args.chunk)
+
+    n = args.n
+    m = n // 1500 + 1
+    lo, hi = shard(n, rank, world)
+    nloc = hi - lo
+    keys = torch.empty(KEY_LEN * nloc + 16, dtype=torch.uint8, device="cuda")
+    ctx.gen_keys13(lo, nloc, out=keys)          # synthetic keys written in HBM (untimed)
+    counts = torch.zeros(m, dtype=torch.int32, device="cuda")
+    E = torch.empty(m + 1, dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()
+
+    def step():
+        counts.zero_()
+        ctx.histogram_fixed(keys, KEY_LEN, m, counts=counts, n=nloc)
+        if world > 1:
+            dist.all_reduce(counts)             # RCCL over xGMI: the global histogram
+        ctx.edge_offsets(counts, out=E)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    ctx.profile_read(ctx.PASS1); ctx.profile_read(ctx.PASS2); ctx.profile_read(ctx.SCAN)
+    ctx.set_profiling(True)
+
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    ctx.set_profiling(False)
+    p1_ms, p1_launches, p1_keys = ctx.profile_read(ctx.PASS1)
+    p2_ms, p2_launches, _ = ctx.profile_read(ctx.PASS2)
+    sc_ms, _, _ = ctx.profile_read(ctx.SCAN)
+
+    t = torch.tensor([dt, p1_ms, p2_ms], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dt, p1_ms_max, p2_ms_max = t.tolist()
+
+    # correctness guard on the measured output: every key counted exactly once
+    total = int(E[-1].item())
+    ok = total == n
+
+    if rank == 0:
+        value = n * args.steps / dt
+        p1_avg_s = p1_ms / 1e3 / max(p1_launches, 1)
+        keys_per_launch = p1_keys / max(p1_launches, 1)
+        achieved = KEY_LEN * keys_per_launch / p1_avg_s / 1e9        # GB/s, algorithmic bytes
+        traffic = None
+        prof = os.path.join(ROOT, "profiles", "pmc_pass1_latest.json")
+        if os.path.exists(prof):
+            try:
+                pj = json.load(open(prof))
+                if pj.get("keys_per_launch") == keys_per_launch:
+                    traffic = pj.get("hbm_bytes_per_launch")
+            except Exception:
+                traffic = None
+        cpu = None
+        if not args.no_cpu:
+            cpu = cpu_baseline(m, args.cpu_seconds, args.cpu_threads)
+        line = {
+            "metric": "index-build keys/s (device-resident), 13B x 13-byte keys; % HBM roofline",
+            "value": value,
+            "unit": "keys/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": dt * 1e3 / args.steps,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "u64",
+            "data": "synthetic (SURVEY.md §8(d) D2 13-byte keys, generated in HBM before timing)",
+            "config": {
+                "workload": "BASELINE config 4: README dataset shape, 13-byte keys, exact index, "
+                            "hash.checksum.bits=4; hash -> bucket -> histogram -> edge offsets",
+                "n_keys": n, "key_bytes": KEY_LEN, "num_buckets": m,
+                "keys_per_gpu": nloc if world == 1 else f"~{n // world}",
+                "parallelism": f"key-shard x{world}" + (" + RCCL all-reduce(histogram)" if world > 1 else ""),
+                "histogram_mode": "atomic" if args.mode == 2 else "partitioned-2pass",
+            },
+            "roofline": {
+                "bound": "hbm", "kernel": "k_pass1 (hash+bucket+partition)",
+                "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                "traffic": traffic,
+                "bytes_per_key": KEY_LEN, "keys_per_launch": keys_per_launch,
+                "avg_launch_ms": p1_avg_s * 1e3, "launches": p1_launches,
+            },
+            "path_roofline_frac": value * KEY_LEN / (HBM_PEAK_GBS * 1e9) / world,
+            "kernel_ms_per_step": {"pass1": p1_ms / args.steps, "pass2": p2_ms / args.steps,
+                                   "edge_offsets": sc_ms / args.steps},
+            "cpu_baseline": cpu,
+            "check": {"E[m]==n": ok},
+        }
+        print(json.dumps(line), flush=True)
+    del keys
+    ctx.close()
+    if world > 1:
+        dist.destroy_process_group()
+    if not ok:
+        raise SystemExit(f"histogram total {total} != n {n}")
+
+
+if __name__ == "__main__":
+    main()

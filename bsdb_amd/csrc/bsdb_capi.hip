@@ -1,0 +1,428 @@
+// bsdb_capi.hip -- C ABI (include/bsdb_mi355x.h) over the gfx950 kernels.
+//
+// One context per writer/device: stream, workspace (partition id regions,
+// cursors, scan scratch) and host staging, all owned here.  Launch functions
+// enqueue only (no hipMalloc/sync on the dev_ path once the workspace has
+// grown to the call's size), so a caller can capture them in a hipGraph.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <new>
+#include <vector>
+
+#include "../../include/bsdb_mi355x.h"
+#include "hash_kernels.hip"
+
+using namespace bsdb;
+
+struct bsdb_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    int hist_mode = 0;
+    uint64_t chunk_keys = 0;
+    std::mutex mu;
+    // workspace
+    void *ids = nullptr;
+    size_t ids_bytes = 0;
+    uint32_t *cursor = nullptr;   // NCOPY * MAX_PARTS
+    uint32_t *overflow = nullptr; // 1 word
+    uint64_t *scan_part = nullptr;
+    size_t scan_part_n = 0;
+    // host-API staging
+    uint8_t *d_keys = nullptr;
+    size_t d_keys_bytes = 0;
+    void *d_out = nullptr;
+    size_t d_out_bytes = 0;
+    // live profiling: event pairs per launch, per kind
+    bool profiling = false;
+    struct Rec { hipEvent_t a, b; int kind; uint64_t keys; };
+    std::vector<Rec> recs;
+    std::vector<hipEvent_t> pool;
+    hipEvent_t ev() {
+        if (!pool.empty()) { hipEvent_t e = pool.back(); pool.pop_back(); return e; }
+        hipEvent_t e = nullptr;
+        (void)hipEventCreate(&e);
+        return e;
+    }
+};
+
+// RAII bracket: records an event before and after the launches in its scope.
+struct ProfScope {
+    bsdb_ctx *c; hipStream_t s; int kind; uint64_t keys; hipEvent_t a = nullptr;
+    ProfScope(bsdb_ctx *c_, hipStream_t s_, int k, uint64_t n) : c(c_), s(s_), kind(k), keys(n) {
+        if (c->profiling) { a = c->ev(); (void)hipEventRecord(a, s); }
+    }
+    ~ProfScope() {
+        if (!a) return;
+        hipEvent_t b = c->ev();
+        (void)hipEventRecord(b, s);
+        c->recs.push_back({a, b, kind, keys});
+    }
+};
+
+namespace {
+
+constexpr uint64_t DEFAULT_CHUNK_KEYS = 1ULL << 31;
+
+#define HIP_OK(x)                                      \
+    do {                                               \
+        if ((x) != hipSuccess) return BSDB_EIO;        \
+    } while (0)
+
+int grow(void **p, size_t *have, size_t need) {
+    if (*have >= need) return BSDB_OK;
+    if (*p) (void)hipFree(*p);
+    *p = nullptr;
+    *have = 0;
+    if (hipMalloc(p, need) != hipSuccess) return BSDB_ENOMEM;
+    *have = need;
+    return BSDB_OK;
+}
+
+hipStream_t pick(bsdb_ctx *c, void *stream) { return stream ? (hipStream_t)stream : c->stream; }
+
+int launch_status() { return hipGetLastError() == hipSuccess ? BSDB_OK : BSDB_EIO; }
+
+// ---- pass-1 dispatch over (source layout, epilogue) ------------------------
+template <int EPI>
+void launch_pass1(const P1Args &a, bool var, uint32_t key_len, uint64_t tiles, hipStream_t s) {
+    const dim3 g((uint32_t)tiles), b(P1_THREADS);
+    if (var) {
+        k_pass1<SRC_VAR, EPI, 1, 0><<<g, b, 0, s>>>(a);
+    } else if (key_len == 13) {
+        k_pass1<SRC_STAGED13, EPI, 4, 13><<<g, b, 0, s>>>(a);
+    } else if (key_len >= 1 && key_len <= 13) {
+        k_pass1<SRC_STAGED, EPI, 4, 0><<<g, b, 0, s>>>(a);
+    } else if (key_len >= 14 && key_len <= 26) {
+        k_pass1<SRC_STAGED, EPI, 2, 0><<<g, b, 0, s>>>(a);
+    } else if (key_len >= 27 && key_len <= 52) {
+        k_pass1<SRC_STAGED, EPI, 1, 0><<<g, b, 0, s>>>(a);
+    } else {
+        k_pass1<SRC_FIXED_DIRECT, EPI, 1, 0><<<g, b, 0, s>>>(a);
+    }
+}
+
+struct PartPlan {
+    uint32_t nparts;
+    uint64_t cap;    // ids per (partition, copy) region, multiple of 8
+    uint32_t slice;  // ids per pass-2 workgroup, multiple of 8
+    uint32_t slices;
+};
+
+// Region capacity: the expected share of a full partition per copy plus
+// 8 sigma and one tile of slack (tiles go round-robin over the copies).
+PartPlan plan_partitions(uint64_t chunk, uint64_t m) {
+    PartPlan p{};
+    p.nparts = (uint32_t)((m + PART_BUCKETS - 1) / PART_BUCKETS);
+    const double frac = std::min(1.0, (double)PART_BUCKETS / (double)m);
+    const double e = (double)chunk * frac / NCOPY;
+    uint64_t cap = (uint64_t)(e * 1.02 + 8.0 * std::sqrt(e) + 2 * P1_TILE + 64);
+    cap = (cap + 7) & ~7ULL;
+    p.cap = cap;
+    // pass-2 workgroups: at least ~1024 in flight, each >= 64 Ki ids
+    const uint64_t regions = (uint64_t)p.nparts * NCOPY;
+    uint64_t slice = std::max<uint64_t>(65536, (uint64_t)std::ceil(e * regions / 1024.0));
+    slice = std::min<uint64_t>(slice, cap);
+    slice = (slice + 7) & ~7ULL;
+    p.slice = (uint32_t)slice;
+    p.slices = (uint32_t)((cap + slice - 1) / slice);
+    return p;
+}
+
+int histogram_impl(bsdb_ctx *c, const uint8_t *keys, const uint64_t *offsets, uint64_t blob_bytes,
+                   uint32_t key_len, uint64_t n, uint64_t seed, uint64_t m, uint32_t *counts,
+                   hipStream_t s) {
+    if (n == 0) return BSDB_OK;
+    const bool var = offsets != nullptr;
+    P1Args a{};
+    a.keys = keys;
+    a.offsets = offsets;
+    a.blob_bytes = blob_bytes;
+    a.key_len = key_len;
+    a.seed = seed;
+    a.multiplier = 2 * m;
+    a.counts = counts;
+    const uint32_t nparts = (uint32_t)((m + PART_BUCKETS - 1) / PART_BUCKETS);
+    const bool atomic_mode = c->hist_mode == 2 || nparts > (uint32_t)MAX_PARTS;
+    if (atomic_mode) {
+        a.n = n;
+        ProfScope ps(c, s, 0, n);
+        launch_pass1<EPI_ATOMIC>(a, var, key_len, (n + P1_TILE - 1) / P1_TILE, s);
+        return launch_status();
+    }
+    uint64_t chunk = c->chunk_keys ? c->chunk_keys : DEFAULT_CHUNK_KEYS;
+    chunk = std::max<uint64_t>(P1_TILE, chunk / P1_TILE * P1_TILE);
+    chunk = std::min<uint64_t>(chunk, (n + P1_TILE - 1) / P1_TILE * P1_TILE);
+    const PartPlan pp = plan_partitions(chunk, m);
+    int rc = grow(&c->ids, &c->ids_bytes, (size_t)pp.nparts * NCOPY * pp.cap * sizeof(uint16_t));
+    if (rc) return rc;
+    a.ids = (uint16_t *)c->ids;
+    a.cursor = c->cursor;
+    a.overflow = c->overflow;
+    a.cap = pp.cap;
+    a.nparts = pp.nparts;
+    for (uint64_t k0 = 0; k0 < n; k0 += chunk) {
+        const uint64_t nk = std::min(chunk, n - k0);
+        P1Args ac = a;
+        ac.n = nk;
+        if (var) {
+            ac.offsets = offsets + k0;
+        } else {
+            ac.keys = keys + k0 * key_len;
+            ac.blob_bytes = nk * key_len;
+        }
+        HIP_OK(hipMemsetAsync(c->cursor, 0, sizeof(uint32_t) * NCOPY * pp.nparts, s));
+        HIP_OK(hipMemsetAsync(c->overflow, 0, sizeof(uint32_t), s));
+        {
+            ProfScope ps(c, s, 0, nk);
+            launch_pass1<EPI_PARTITION>(ac, var, key_len, (nk + P1_TILE - 1) / P1_TILE, s);
+        }
+        {
+            ProfScope ps(c, s, 1, nk);
+            k_pass2<<<dim3(pp.slices, pp.nparts * NCOPY), P2_THREADS, 0, s>>>(
+                (const uint16_t *)c->ids, c->cursor, c->overflow, pp.cap, pp.nparts, pp.slice, m, counts);
+        }
+        if (var) {
+            k_overflow_fallback<SRC_VAR, 0><<<1024, P1_THREADS, 0, s>>>(ac);
+        } else {
+            k_overflow_fallback<SRC_FIXED_DIRECT, 0><<<1024, P1_THREADS, 0, s>>>(ac);
+        }
+        if ((rc = launch_status())) return rc;
+    }
+    return BSDB_OK;
+}
+
+int hash_impl(const uint8_t *keys, const uint64_t *offsets, uint64_t blob_bytes, uint32_t key_len,
+              uint64_t n, uint64_t seed, uint64_t *sig, hipStream_t s) {
+    if (n == 0) return BSDB_OK;
+    P1Args a{};
+    a.keys = keys;
+    a.offsets = offsets;
+    a.blob_bytes = blob_bytes;
+    a.key_len = key_len;
+    a.n = n;
+    a.seed = seed;
+    a.sig = sig;
+    launch_pass1<EPI_SIG>(a, offsets != nullptr, key_len, (n + P1_TILE - 1) / P1_TILE, s);
+    return launch_status();
+}
+
+bool aligned16(const void *p) { return ((uintptr_t)p & 15) == 0; }
+
+}  // namespace
+
+extern "C" {
+
+int bsdb_abi_version(void) { return BSDB_ABI_VERSION; }
+
+const char *bsdb_strerror(int code) {
+    switch (code) {
+        case BSDB_OK: return "ok";
+        case BSDB_EINVAL: return "invalid argument";
+        case BSDB_ENOMEM: return "device out of memory";
+        case BSDB_EIO: return "HIP runtime error";
+        case BSDB_ENODEV: return "no such HIP device";
+        case BSDB_EDUP: return "duplicate key signature";
+        case BSDB_ESEEDS: return "exhausted local seeds";
+        default: return "unknown error";
+    }
+}
+
+uint64_t bsdb_num_buckets(uint64_t n) { return n / BUCKET_SIZE + 1; }
+
+int bsdb_open(int device, bsdb_ctx **out) {
+    if (!out) return BSDB_EINVAL;
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return BSDB_ENODEV;
+    bsdb_ctx *c = new (std::nothrow) bsdb_ctx();
+    if (!c) return BSDB_ENOMEM;
+    c->device = device;
+    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return BSDB_EIO;
+    }
+    if (hipMalloc(&c->cursor, sizeof(uint32_t) * NCOPY * MAX_PARTS) != hipSuccess ||
+        hipMalloc(&c->overflow, sizeof(uint32_t) * 4) != hipSuccess) {
+        bsdb_close(c);
+        return BSDB_ENOMEM;
+    }
+    *out = c;
+    return BSDB_OK;
+}
+
+int bsdb_close(bsdb_ctx *c) {
+    if (!c) return BSDB_EINVAL;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    (void)hipFree(c->ids);
+    (void)hipFree(c->cursor);
+    (void)hipFree(c->overflow);
+    (void)hipFree(c->scan_part);
+    (void)hipFree(c->d_keys);
+    (void)hipFree(c->d_out);
+    for (auto &r : c->recs) { (void)hipEventDestroy(r.a); (void)hipEventDestroy(r.b); }
+    for (auto e : c->pool) (void)hipEventDestroy(e);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+    return BSDB_OK;
+}
+
+int bsdb_set_histogram_mode(bsdb_ctx *c, int mode) {
+    if (!c || mode < 0 || mode > 2) return BSDB_EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    c->hist_mode = mode;
+    return BSDB_OK;
+}
+
+int bsdb_set_chunk_keys(bsdb_ctx *c, uint64_t chunk_keys) {
+    if (!c) return BSDB_EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    c->chunk_keys = chunk_keys;
+    return BSDB_OK;
+}
+
+int bsdb_dev_hash_fixed(bsdb_ctx *c, const uint8_t *d_keys, uint32_t key_len, uint64_t n, uint64_t seed,
+                        uint64_t *d_sig, void *stream) {
+    if (!c || (n && (!d_keys || !d_sig)) || !aligned16(d_keys) || !aligned16(d_sig)) return BSDB_EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    HIP_OK(hipSetDevice(c->device));
+    return hash_impl(d_keys, nullptr, n * key_len, key_len, n, seed, d_sig, pick(c, stream));
+}
+
+int bsdb_dev_hash_var(bsdb_ctx *c, const uint8_t *d_blob, uint64_t blob_bytes, const uint64_t *d_off, uint64_t n,
+                      uint64_t seed, uint64_t *d_sig, void *stream) {
+    if (!c || (n && (!d_blob || !d_off || !d_sig)) || !aligned16(d_sig)) return BSDB_EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    HIP_OK(hipSetDevice(c->device));
+    return hash_impl(d_blob, d_off, blob_bytes, 0, n, seed, d_sig, pick(c, stream));
+}
+
+int bsdb_dev_histogram_fixed(bsdb_ctx *c, const uint8_t *d_keys, uint32_t key_len, uint64_t n, uint64_t seed,
+                             uint64_t m, uint32_t *d_counts, void *stream) {
+    if (!c || m == 0 || m > 0x7FFFFFFFULL || (n && (!d_keys || !d_counts)) || !aligned16(d_keys)) return BSDB_EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    HIP_OK(hipSetDevice(c->device));
+    return histogram_impl(c, d_keys, nullptr, n * key_len, key_len, n, seed, m, d_counts, pick(c, stream));
+}
+
+int bsdb_dev_histogram_var(bsdb_ctx *c, const uint8_t *d_blob, uint64_t blob_bytes, const uint64_t *d_off,
+                           uint64_t n, uint64_t seed, uint64_t m, uint32_t *d_counts, void *stream) {
+    if (!c || m == 0 || m > 0x7FFFFFFFULL || (n && (!d_blob || !d_off || !d_counts))) return BSDB_EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    HIP_OK(hipSetDevice(c->device));
+    return histogram_impl(c, d_blob, d_off, blob_bytes, 0, n, seed, m, d_counts, pick(c, stream));
+}
+
+int bsdb_dev_edge_offsets(bsdb_ctx *c, const uint32_t *d_counts, uint64_t m, uint64_t *d_E, void *stream) {
+    if (!c || m == 0 || !d_counts || !d_E) return BSDB_EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    HIP_OK(hipSetDevice(c->device));
+    const uint64_t nb = (m + SCAN_BLOCK - 1) / SCAN_BLOCK;
+    size_t have = c->scan_part_n * sizeof(uint64_t);
+    int rc = grow((void **)&c->scan_part, &have, nb * sizeof(uint64_t));
+    if (rc) return rc;
+    c->scan_part_n = have / sizeof(uint64_t);
+    hipStream_t s = pick(c, stream);
+    ProfScope ps(c, s, 2, m);
+    k_scan_partial<<<(uint32_t)nb, SCAN_THREADS, 0, s>>>(d_counts, m, c->scan_part);
+    k_scan_top<<<1, SCAN_THREADS, 0, s>>>(c->scan_part, nb);
+    k_scan_final<<<(uint32_t)nb, SCAN_THREADS, 0, s>>>(d_counts, m, c->scan_part, d_E);
+    return launch_status();
+}
+
+int bsdb_dev_gen_keys13(bsdb_ctx *c, uint64_t first, uint64_t n, uint8_t *d_keys, void *stream) {
+    if (!c || (n && !d_keys) || !aligned16(d_keys)) return BSDB_EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    HIP_OK(hipSetDevice(c->device));
+    if (n == 0) return BSDB_OK;
+    k_gen_keys13<<<(uint32_t)((n + 255) / 256), 256, 0, pick(c, stream)>>>(first, n, d_keys);
+    return launch_status();
+}
+
+int bsdb_set_profiling(bsdb_ctx *c, int enable) {
+    if (!c) return BSDB_EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    c->profiling = enable != 0;
+    return BSDB_OK;
+}
+
+int bsdb_profile_read(bsdb_ctx *c, int kind, double *total_ms, uint64_t *launches, uint64_t *keys) {
+    if (!c || !total_ms || !launches || !keys) return BSDB_EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    HIP_OK(hipSetDevice(c->device));
+    double t = 0;
+    uint64_t nl = 0, nk = 0;
+    std::vector<bsdb_ctx::Rec> keep;
+    for (auto &r : c->recs) {
+        if (r.kind != kind) { keep.push_back(r); continue; }
+        HIP_OK(hipEventSynchronize(r.b));
+        float ms = 0;
+        HIP_OK(hipEventElapsedTime(&ms, r.a, r.b));
+        t += ms;
+        nl += 1;
+        nk += r.keys;
+        c->pool.push_back(r.a);
+        c->pool.push_back(r.b);
+    }
+    c->recs.swap(keep);
+    *total_ms = t;
+    *launches = nl;
+    *keys = nk;
+    return BSDB_OK;
+}
+
+// ---- host-buffer entry points ---------------------------------------------
+int bsdb_histogram_fixed(bsdb_ctx *c, const uint8_t *h_keys, uint32_t key_len, uint64_t n, uint64_t seed,
+                         uint64_t m, uint32_t *h_counts) {
+    if (!c || m == 0 || m > 0x7FFFFFFFULL || (n && !h_keys) || !h_counts) return BSDB_EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    HIP_OK(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    const uint64_t batch = std::max<uint64_t>(P1_TILE, (256ULL << 20) / std::max<uint32_t>(key_len, 1) / P1_TILE * P1_TILE);
+    int rc = grow((void **)&c->d_keys, &c->d_keys_bytes, (size_t)std::min(batch, std::max<uint64_t>(n, 1)) * std::max<uint32_t>(key_len, 1) + 16);
+    if (rc) return rc;
+    rc = grow(&c->d_out, &c->d_out_bytes, m * sizeof(uint32_t));
+    if (rc) return rc;
+    uint32_t *d_counts = (uint32_t *)c->d_out;
+    HIP_OK(hipMemsetAsync(d_counts, 0, m * sizeof(uint32_t), s));
+    for (uint64_t k0 = 0; k0 < n; k0 += batch) {
+        const uint64_t nk = std::min(batch, n - k0);
+        HIP_OK(hipMemcpyAsync(c->d_keys, h_keys + k0 * key_len, nk * key_len, hipMemcpyHostToDevice, s));
+        if ((rc = histogram_impl(c, c->d_keys, nullptr, nk * key_len, key_len, nk, seed, m, d_counts, s))) return rc;
+    }
+    std::vector<uint32_t> tmp(m);
+    HIP_OK(hipMemcpyAsync(tmp.data(), d_counts, m * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    HIP_OK(hipStreamSynchronize(s));
+    for (uint64_t b = 0; b < m; ++b) h_counts[b] += tmp[b];
+    return BSDB_OK;
+}
+
+int bsdb_hash_fixed(bsdb_ctx *c, const uint8_t *h_keys, uint32_t key_len, uint64_t n, uint64_t seed,
+                    uint64_t *h_sig) {
+    if (!c || (n && (!h_keys || !h_sig))) return BSDB_EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    HIP_OK(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    const uint64_t batch = std::max<uint64_t>(P1_TILE, (64ULL << 20) / std::max<uint32_t>(key_len, 1) / P1_TILE * P1_TILE);
+    const uint64_t cap = std::min(batch, std::max<uint64_t>(n, 1));
+    int rc = grow((void **)&c->d_keys, &c->d_keys_bytes, (size_t)cap * std::max<uint32_t>(key_len, 1) + 16);
+    if (rc) return rc;
+    rc = grow(&c->d_out, &c->d_out_bytes, cap * 16);
+    if (rc) return rc;
+    for (uint64_t k0 = 0; k0 < n; k0 += batch) {
+        const uint64_t nk = std::min(batch, n - k0);
+        HIP_OK(hipMemcpyAsync(c->d_keys, h_keys + k0 * key_len, nk * key_len, hipMemcpyHostToDevice, s));
+        if ((rc = hash_impl(c->d_keys, nullptr, nk * key_len, key_len, nk, seed, (uint64_t *)c->d_out, s))) return rc;
+        HIP_OK(hipMemcpyAsync(h_sig + 2 * k0, c->d_out, nk * 16, hipMemcpyDeviceToHost, s));
+    }
+    HIP_OK(hipStreamSynchronize(s));
+    return BSDB_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,433 @@
+// hash_kernels.hip -- the index-build hot path on MI355X (gfx950).
+//
+// Per key: SpookyHash-short (A3) -> bucket = multiplyHigh(sig0>>>1, 2m) (A4)
+// -> bucket-occupancy histogram (A6).  Reference loop being replaced:
+// ConcurrentBucketedHashStore.add (CBHS:360-395) + the GOV producer that
+// accumulates edgeOffsetAndSeed (GOV:385-402).
+//
+// Why two passes: m = n/1500+1 buckets (8.8 M at 13 B keys) is a 35 MB
+// table, far beyond LDS, and per-key device-scope atomics into it run at the
+// memory-side atomic rate (~20 G random adds/s), 20x slower than the key
+// stream.  So pass 1 hashes a tile of 8192 keys, counting-sorts the tile's
+// bucket ids by partition (32768 buckets each) in LDS and writes 2-byte
+// partition-local ids in runs; pass 2 histograms one partition at a time in a
+// 128 KiB LDS table and flushes it with coalesced atomics.  Extra traffic is
+// 4 B/key on top of the key bytes.  See DESIGN.md.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "spooky_dev.hpp"
+
+namespace bsdb {
+
+constexpr int P1_THREADS = 512;
+constexpr int P1_KEYS_PER_THREAD = 16;
+constexpr int P1_TILE = P1_THREADS * P1_KEYS_PER_THREAD;  // 8192 keys per workgroup
+constexpr int STAGE_BYTES = 26624;                        // 2048 keys x 13 B
+constexpr int PART_SHIFT = 15;                            // 32768 buckets per partition
+constexpr int PART_BUCKETS = 1 << PART_SHIFT;
+constexpr int MAX_PARTS = 512;
+constexpr int NCOPY = 8;                                  // cursor/region copies (one per XCD)
+constexpr int P2_THREADS = 1024;
+
+enum Epi { EPI_PARTITION = 0, EPI_ATOMIC = 1, EPI_SIG = 2 };
+enum Src { SRC_STAGED13 = 0, SRC_STAGED = 1, SRC_FIXED_DIRECT = 2, SRC_VAR = 3 };
+
+struct P1Args {
+    const uint8_t *keys;      // fixed: n*key_len bytes; var: blob
+    const uint64_t *offsets;  // var only
+    uint64_t blob_bytes;      // bytes readable at keys
+    uint64_t n;               // keys in this launch
+    uint32_t key_len;         // fixed only
+    uint64_t seed;
+    uint64_t multiplier;      // 2 * num_buckets
+    // EPI_PARTITION
+    uint16_t *ids;            // [P][NCOPY][cap]
+    uint32_t *cursor;         // [NCOPY][P]
+    uint32_t *overflow;       // set when a region would overflow
+    uint64_t cap;             // capacity of one (partition, copy) region, multiple of 8
+    uint32_t nparts;
+    // EPI_ATOMIC
+    uint32_t *counts;
+    // EPI_SIG
+    uint64_t *sig;
+};
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+// Streaming 16-byte load, read-once data (keys, partition ids): nontemporal so
+// the stream does not evict the re-used tables from L2 / Infinity Cache.
+__device__ __forceinline__ uint4 ntload16(const void *p) {
+    const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(p));
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+// Bounds-checked little-endian u64 read from global memory.
+__device__ __forceinline__ uint64_t gload64(const uint8_t *base, uint64_t limit, uint64_t pos) {
+    const uint64_t a = pos & ~3ULL;
+    const uint32_t sh = (uint32_t)(pos & 3) * 8;
+    const uint32_t *q = reinterpret_cast<const uint32_t *>(base + a);
+    const uint32_t d0 = a + 4 <= limit ? q[0] : 0;
+    const uint32_t d1 = a + 8 <= limit ? q[1] : 0;
+    const uint32_t d2 = a + 12 <= limit ? q[2] : 0;
+    return funnel64(d0, d1, d2, sh);
+}
+
+// Copies bytes [src_lo, src_lo + nbytes) of global memory into LDS starting at
+// dword-aligned `stage`, with 16-byte loads where the source is aligned.  The
+// caller guarantees src_lo % 16 == 0 for the staged paths (tile starts are
+// multiples of 2048 keys: 2048*L bytes, and the key blob is 16-B aligned).
+struct StageRegs {
+    uint4 v[4];
+};
+
+__device__ __forceinline__ void stage_load(StageRegs &r, const uint8_t *src, uint64_t nbytes, int tid) {
+    const uint32_t nvec = (uint32_t)(nbytes >> 4);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const uint32_t i = tid + j * P1_THREADS;
+        if (i < nvec) {
+            r.v[j] = ntload16(src + (uint64_t)i * 16);
+        } else if (i == nvec && (nbytes & 15)) {
+            // ragged end of the chunk: byte loads, never past nbytes
+            uint8_t tmp[16];
+            for (int b = 0; b < 16; ++b) tmp[b] = (uint64_t)i * 16 + b < nbytes ? src[(uint64_t)i * 16 + b] : 0;
+            r.v[j] = *reinterpret_cast<uint4 *>(tmp);
+        }
+    }
+}
+
+__device__ __forceinline__ void stage_store(const StageRegs &r, uint32_t *stage, uint64_t nbytes, int tid) {
+    const uint32_t nvec = (uint32_t)((nbytes + 15) >> 4);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const uint32_t i = tid + j * P1_THREADS;
+        if (i < nvec) reinterpret_cast<uint4 *>(stage)[i] = r.v[j];
+    }
+}
+
+// Hash of key `k` of the staged sub-tile (byte offset k*L in LDS).
+template <int LFIX>
+__device__ __forceinline__ void hash_staged(const uint32_t *stage, uint32_t k, uint32_t key_len,
+                                            uint64_t seed, uint64_t &s0, uint64_t &s1) {
+    const uint32_t L = LFIX ? LFIX : key_len;
+    const uint32_t o = k * L;
+    if (LFIX == 13) {
+        const uint32_t *q = stage + (o >> 2);
+        const uint32_t sh = (o & 3) * 8;
+        const uint32_t d0 = q[0], d1 = q[1], d2 = q[2], d3 = q[3];
+        const uint64_t w0 = funnel64(d0, d1, d2, sh);
+        const uint32_t w1lo = __builtin_amdgcn_alignbit(d3, d2, sh);
+        const uint32_t b12 = (d3 >> sh) & 0xFF;
+        const uint64_t w1 = ((uint64_t)b12 << 32) | w1lo;
+        spooky_8_15(w0, w1, 13, seed, s0, s1);
+    } else {
+        auto rd = [&](uint32_t off) -> uint64_t {
+            const uint32_t p = o + off;
+            const uint32_t *q = stage + (p >> 2);
+            return funnel64(q[0], q[1], q[2], (p & 3) * 8);
+        };
+        spooky_short(rd, L, seed, s0, s1);
+    }
+}
+
+// Block-wide exclusive scan of one u32 per thread (512 threads).
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *wsum, int tid, uint32_t &total) {
+    const int lane = tid & 63, wid = tid >> 6;
+    uint32_t x = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d, 64);
+        if (lane >= d) x += y;
+    }
+    if (lane == 63) wsum[wid] = x;
+    __syncthreads();
+    uint32_t pre = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < P1_THREADS / 64; ++w) {
+        const uint32_t s = wsum[w];
+        pre += w < wid ? s : 0;
+        tot += s;
+    }
+    total = tot;
+    return pre + x - v;
+}
+
+// Pass 1: one workgroup = one tile of 8192 consecutive keys.
+template <int SRC, int EPI, int KPS, int LFIX>
+__global__ __launch_bounds__(P1_THREADS, 4) void k_pass1(P1Args a) {
+    // stage (key bytes of one sub-tile) and sorted (the tile's bucket ids in
+    // partition order) are never live together: one 32 KiB buffer serves both.
+    constexpr int UNION_WORDS = EPI == EPI_PARTITION ? P1_TILE : (STAGE_BYTES + 64) / 4;
+    __shared__ __align__(16) uint32_t stage[UNION_WORDS];
+    uint32_t *sorted = stage;
+    __shared__ uint32_t bkl[EPI == EPI_PARTITION ? P1_TILE : 1];  // bucket of key kt
+    __shared__ uint32_t hist[MAX_PARTS], start[MAX_PARTS], run[MAX_PARTS], base[MAX_PARTS];
+    __shared__ uint32_t wsum[P1_THREADS / 64];
+
+    const int tid = threadIdx.x;
+    const uint64_t tile0 = (uint64_t)blockIdx.x * P1_TILE;
+    if (tile0 >= a.n) return;
+    const uint32_t tile_n = (uint32_t)min((uint64_t)P1_TILE, a.n - tile0);
+    const uint32_t L = LFIX ? LFIX : a.key_len;
+
+    if (EPI == EPI_PARTITION) {
+        for (int i = tid; i < MAX_PARTS; i += P1_THREADS) hist[i] = 0;
+    }
+
+    auto emit = [&](uint32_t kt, uint64_t gk, uint64_t s0, uint64_t s1) {
+        if (EPI == EPI_SIG) {
+            reinterpret_cast<ulonglong2 *>(a.sig)[gk] = make_ulonglong2(s0, s1);
+        } else {
+            const uint32_t b = bucket_of(s0, a.multiplier);
+            if (EPI == EPI_ATOMIC) {
+                atomicAdd(a.counts + b, 1u);
+            } else {
+                bkl[kt] = b;
+                atomicAdd(&hist[b >> PART_SHIFT], 1u);
+            }
+        }
+    };
+
+    if (SRC == SRC_STAGED13 || SRC == SRC_STAGED) {
+        // sub-tile = P1_THREADS*KPS keys staged through LDS with 16-B loads,
+        // next sub-tile prefetched into registers while this one hashes.
+        constexpr int SUB = P1_THREADS * KPS;
+        constexpr int NSUB = P1_KEYS_PER_THREAD / KPS;
+        const uint64_t tile_bytes0 = tile0 * L;
+        StageRegs pre;
+        auto sub_bytes = [&](int s) -> uint64_t {
+            const uint64_t k0 = (uint64_t)s * SUB;
+            if (k0 >= tile_n) return 0;
+            return (uint64_t)min((uint32_t)SUB, tile_n - (uint32_t)k0) * L;
+        };
+        stage_load(pre, a.keys + tile_bytes0, sub_bytes(0), tid);
+        if (EPI == EPI_PARTITION) __syncthreads();  // hist zeroed
+#pragma unroll
+        for (int s = 0; s < NSUB; ++s) {
+            const uint64_t nb = sub_bytes(s);
+            if (s) __syncthreads();  // all reads of the previous sub-tile done
+            stage_store(pre, stage, nb, tid);
+            __syncthreads();
+            if (s + 1 < NSUB) stage_load(pre, a.keys + tile_bytes0 + (uint64_t)(s + 1) * SUB * L, sub_bytes(s + 1), tid);
+#pragma unroll
+            for (int q = 0; q < KPS; ++q) {
+                const uint32_t k = tid + q * P1_THREADS;  // key within sub-tile
+                const uint32_t kt = s * SUB + k;           // key within tile
+                if (kt < tile_n) {
+                    uint64_t s0, s1;
+                    hash_staged<LFIX>(stage, k, L, a.seed, s0, s1);
+                    emit(kt, tile0 + kt, s0, s1);
+                }
+            }
+        }
+    } else {
+        // direct global reads: long fixed keys (L > 52) and variable-length keys
+        if (EPI == EPI_PARTITION) __syncthreads();
+#pragma unroll
+        for (int j = 0; j < P1_KEYS_PER_THREAD; ++j) {
+            const uint32_t kt = tid + j * P1_THREADS;
+            if (kt < tile_n) {
+                const uint64_t gk = tile0 + kt;
+                uint64_t pos, len;
+                if (SRC == SRC_VAR) {
+                    pos = a.offsets[gk];
+                    len = a.offsets[gk + 1] - pos;
+                } else {
+                    pos = gk * L;
+                    len = L;
+                }
+                auto rd = [&](uint32_t off) -> uint64_t { return gload64(a.keys, a.blob_bytes, pos + off); };
+                uint64_t s0, s1;
+                spooky_short(rd, (uint32_t)len, a.seed, s0, s1);
+                emit(kt, gk, s0, s1);
+            }
+        }
+    }
+
+    if (EPI != EPI_PARTITION) return;
+
+    // ---- counting sort of the tile by partition, then run-wise write-out ----
+    __syncthreads();
+    const uint32_t P = a.nparts;
+    const int copy = blockIdx.x & (NCOPY - 1);
+    uint32_t cnt = tid < (int)P ? hist[tid] : 0, total;
+    const uint32_t excl = block_excl_scan(cnt, wsum, tid, total);
+    if (tid < (int)P) {
+        start[tid] = excl;
+        run[tid] = excl;
+        base[tid] = cnt ? atomicAdd(a.cursor + copy * P + tid, cnt) : 0;
+    }
+    __syncthreads();
+    for (uint32_t kt = tid; kt < tile_n; kt += P1_THREADS) {
+        const uint32_t b = bkl[kt];
+        const uint32_t pos = atomicAdd(&run[b >> PART_SHIFT], 1u);
+        sorted[pos] = b;
+    }
+    __syncthreads();
+    bool ovf = false;
+    for (uint32_t j = tid; j < tile_n; j += P1_THREADS) {
+        const uint32_t b = sorted[j];
+        const uint32_t p = b >> PART_SHIFT;
+        const uint64_t idx = (uint64_t)base[p] + (j - start[p]);
+        if (idx < a.cap) {
+            a.ids[((uint64_t)p * NCOPY + copy) * a.cap + idx] = (uint16_t)(b & (PART_BUCKETS - 1));
+        } else {
+            ovf = true;
+        }
+    }
+    if (ovf) atomicOr(a.overflow, 1u);
+}
+
+// Pass 2: LDS histogram of one slice of one (partition, copy) region.
+__global__ __launch_bounds__(P2_THREADS, 4) void k_pass2(const uint16_t *ids, const uint32_t *cursor,
+                                                         const uint32_t *overflow, uint64_t cap,
+                                                         uint32_t nparts, uint32_t slice,
+                                                         uint64_t num_buckets, uint32_t *counts) {
+    __shared__ uint32_t hist[PART_BUCKETS];
+    if (*overflow) return;
+    const int tid = threadIdx.x;
+    const uint32_t p = blockIdx.y / NCOPY, c = blockIdx.y % NCOPY;
+    const uint64_t cnt = min((uint64_t)cursor[c * nparts + p], cap);
+    const uint64_t lo = (uint64_t)blockIdx.x * slice;
+    if (lo >= cnt) return;
+    const uint64_t hi = min(cnt, lo + slice);
+    for (int i = tid; i < PART_BUCKETS; i += P2_THREADS) hist[i] = 0;
+    __syncthreads();
+    const uint16_t *src = ids + ((uint64_t)p * NCOPY + c) * cap;
+    // lo is a multiple of 8 (slice % 8 == 0, cap % 8 == 0): 16-B aligned vectors
+    const uint64_t nvec = (hi - lo) >> 3;
+    const uint4 *v = reinterpret_cast<const uint4 *>(src + lo);
+    for (uint64_t i = tid; i < nvec; i += P2_THREADS) {
+        const uint4 w = ntload16(v + i);
+        atomicAdd(&hist[w.x & 0xFFFF], 1u); atomicAdd(&hist[w.x >> 16], 1u);
+        atomicAdd(&hist[w.y & 0xFFFF], 1u); atomicAdd(&hist[w.y >> 16], 1u);
+        atomicAdd(&hist[w.z & 0xFFFF], 1u); atomicAdd(&hist[w.z >> 16], 1u);
+        atomicAdd(&hist[w.w & 0xFFFF], 1u); atomicAdd(&hist[w.w >> 16], 1u);
+    }
+    for (uint64_t i = lo + nvec * 8 + tid; i < hi; i += P2_THREADS) atomicAdd(&hist[src[i]], 1u);
+    __syncthreads();
+    const uint64_t b0 = (uint64_t)p << PART_SHIFT;
+    const uint32_t nb = (uint32_t)min((uint64_t)PART_BUCKETS, num_buckets - b0);
+    for (uint32_t i = tid; i < nb; i += P2_THREADS) {
+        const uint32_t h = hist[i];
+        if (h) atomicAdd(counts + b0 + i, h);
+    }
+}
+
+// Fallback when pass 1 overflowed a region (adversarial key sets): recount the
+// whole launch with direct atomics.  Exits immediately in the normal case.
+template <int SRC, int LFIX>
+__global__ __launch_bounds__(P1_THREADS) void k_overflow_fallback(P1Args a) {
+    if (*a.overflow == 0) return;
+    const uint64_t stride = (uint64_t)gridDim.x * P1_THREADS;
+    for (uint64_t gk = (uint64_t)blockIdx.x * P1_THREADS + threadIdx.x; gk < a.n; gk += stride) {
+        uint64_t pos, len;
+        if (SRC == SRC_VAR) {
+            pos = a.offsets[gk];
+            len = a.offsets[gk + 1] - pos;
+        } else {
+            pos = gk * a.key_len;
+            len = a.key_len;
+        }
+        auto rd = [&](uint32_t off) -> uint64_t { return gload64(a.keys, a.blob_bytes, pos + off); };
+        uint64_t s0, s1;
+        spooky_short(rd, (uint32_t)len, a.seed, s0, s1);
+        atomicAdd(a.counts + bucket_of(s0, a.multiplier), 1u);
+    }
+}
+
+// ---- A6: exclusive prefix sum counts[m] (u32) -> E[m+1] (u64) ------------
+constexpr int SCAN_THREADS = 1024;
+constexpr int SCAN_PER_THREAD = 8;
+constexpr int SCAN_BLOCK = SCAN_THREADS * SCAN_PER_THREAD;
+
+__device__ __forceinline__ uint64_t block_excl_scan64(uint64_t v, uint64_t *wsum, int tid, uint64_t &total) {
+    const int lane = tid & 63, wid = tid >> 6;
+    uint64_t x = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint64_t y = __shfl_up(x, d, 64);
+        if (lane >= d) x += y;
+    }
+    if (lane == 63) wsum[wid] = x;
+    __syncthreads();
+    uint64_t pre = 0, tot = 0;
+    for (int w = 0; w < SCAN_THREADS / 64; ++w) {
+        const uint64_t s = wsum[w];
+        pre += w < wid ? s : 0;
+        tot += s;
+    }
+    total = tot;
+    __syncthreads();
+    return pre + x - v;
+}
+
+__global__ __launch_bounds__(SCAN_THREADS) void k_scan_partial(const uint32_t *counts, uint64_t m, uint64_t *part) {
+    __shared__ uint64_t wsum[SCAN_THREADS / 64];
+    const uint64_t i0 = (uint64_t)blockIdx.x * SCAN_BLOCK + (uint64_t)threadIdx.x * SCAN_PER_THREAD;
+    uint64_t s = 0;
+#pragma unroll
+    for (int j = 0; j < SCAN_PER_THREAD; ++j) s += i0 + j < m ? counts[i0 + j] : 0;
+    uint64_t tot;
+    block_excl_scan64(s, wsum, threadIdx.x, tot);
+    if (threadIdx.x == 0) part[blockIdx.x] = tot;
+}
+
+__global__ __launch_bounds__(SCAN_THREADS) void k_scan_top(uint64_t *part, uint64_t nparts) {
+    __shared__ uint64_t wsum[SCAN_THREADS / 64];
+    uint64_t carry = 0;
+    for (uint64_t b = 0; b < nparts; b += SCAN_THREADS) {
+        const uint64_t i = b + threadIdx.x;
+        const uint64_t v = i < nparts ? part[i] : 0;
+        uint64_t tot;
+        const uint64_t e = block_excl_scan64(v, wsum, threadIdx.x, tot);
+        if (i < nparts) part[i] = carry + e;
+        carry += tot;
+    }
+}
+
+__global__ __launch_bounds__(SCAN_THREADS) void k_scan_final(const uint32_t *counts, uint64_t m,
+                                                             const uint64_t *part, uint64_t *E) {
+    __shared__ uint64_t wsum[SCAN_THREADS / 64];
+    const uint64_t i0 = (uint64_t)blockIdx.x * SCAN_BLOCK + (uint64_t)threadIdx.x * SCAN_PER_THREAD;
+    uint32_t c[SCAN_PER_THREAD];
+    uint64_t s = 0;
+#pragma unroll
+    for (int j = 0; j < SCAN_PER_THREAD; ++j) {
+        c[j] = i0 + j < m ? counts[i0 + j] : 0;
+        s += c[j];
+    }
+    uint64_t tot;
+    uint64_t run = part[blockIdx.x] + block_excl_scan64(s, wsum, threadIdx.x, tot);
+    if (i0 == 0) E[0] = 0;
+#pragma unroll
+    for (int j = 0; j < SCAN_PER_THREAD; ++j) {
+        run += c[j];
+        if (i0 + j < m) E[i0 + j + 1] = run;
+    }
+}
+
+// ---- synthetic 13-byte keys (bench input) ------------
+__global__ __launch_bounds__(256) void k_gen_keys13(uint64_t first, uint64_t n, uint8_t *out) {
+    __shared__ __align__(16) uint8_t buf[256 * 13];
+    const uint64_t k0 = (uint64_t)blockIdx.x * 256;
+    const uint64_t k = k0 + threadIdx.x;
+    if (k < n) {
+        const uint64_t i = first + k;
+        const uint64_t w0 = splitmix64(i ^ 0xB5DB0001ULL);
+        const uint64_t w1 = (i ^ (splitmix64(i + 1) >> 24)) & 0xFFFFFFFFFFULL;
+        uint8_t *d = buf + threadIdx.x * 13;
+        for (int b = 0; b < 8; ++b) d[b] = (uint8_t)(w0 >> (8 * b));
+        for (int b = 0; b < 5; ++b) d[8 + b] = (uint8_t)(w1 >> (8 * b));
+    }
+    __syncthreads();
+    // k0*13 = blockIdx*3328 is dword aligned: dword stores, byte tail
+    const uint32_t nbytes = (uint32_t)min((uint64_t)256, n - k0) * 13;
+    uint32_t *o32 = reinterpret_cast<uint32_t *>(out + k0 * 13);
+    const uint32_t *b32 = reinterpret_cast<const uint32_t *>(buf);
+    for (uint32_t w = threadIdx.x; w < nbytes / 4; w += 256) o32[w] = b32[w];
+    for (uint32_t b = (nbytes & ~3u) + threadIdx.x; b < nbytes; b += 256) out[k0 * 13 + b] = buf[b];
+}
+
+}  // namespace bsdb

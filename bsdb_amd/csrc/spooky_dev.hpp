@@ -1,0 +1,128 @@
+// spooky_dev.hpp -- SpookyHash-short, bucket map and GOV helpers as CDNA4
+// device functions.  Behaviour follows the reference's C spec
+// (src/main/c/spooky.c:55-175) and GOV's bucket map
+// (GOVMinimalPerfectHashFunctionModified.java:559, 315-317); the code is laid
+// out for 64-wide wavefronts: every 64-bit op lowers to a pair of 32-bit VALU
+// ops (rotates -> v_alignbit_b32 x2, adds -> v_lshl_add_u64 / add+addc).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace bsdb {
+
+constexpr uint64_t SC = 0x9e3779b97f4a7c13ULL;  // spooky.c:39
+constexpr uint64_t OFFSET_MASK = ~0ULL >> 8;    // GOV:157
+constexpr uint32_t BUCKET_SIZE = 1500;          // GOV:281
+
+__device__ __forceinline__ uint64_t rotl64(uint64_t x, int k) { return (x << k) | (x >> (64 - k)); }
+
+// spooky.c:55-68
+__device__ __forceinline__ void short_mix(uint64_t &h0, uint64_t &h1, uint64_t &h2, uint64_t &h3) {
+    h2 = rotl64(h2, 50); h2 += h3; h0 ^= h2;
+    h3 = rotl64(h3, 52); h3 += h0; h1 ^= h3;
+    h0 = rotl64(h0, 30); h0 += h1; h2 ^= h0;
+    h1 = rotl64(h1, 41); h1 += h2; h3 ^= h1;
+    h2 = rotl64(h2, 54); h2 += h3; h0 ^= h2;
+    h3 = rotl64(h3, 48); h3 += h0; h1 ^= h3;
+    h0 = rotl64(h0, 38); h0 += h1; h2 ^= h0;
+    h1 = rotl64(h1, 37); h1 += h2; h3 ^= h1;
+    h2 = rotl64(h2, 62); h2 += h3; h0 ^= h2;
+    h3 = rotl64(h3, 34); h3 += h0; h1 ^= h3;
+    h0 = rotl64(h0, 5);  h0 += h1; h2 ^= h0;
+    h1 = rotl64(h1, 36); h1 += h2; h3 ^= h1;
+}
+
+// spooky.c:72-84
+__device__ __forceinline__ void short_end(uint64_t &h0, uint64_t &h1, uint64_t &h2, uint64_t &h3) {
+    h3 ^= h2; h2 = rotl64(h2, 15); h3 += h2;
+    h0 ^= h3; h3 = rotl64(h3, 52); h0 += h3;
+    h1 ^= h0; h0 = rotl64(h0, 26); h1 += h0;
+    h2 ^= h1; h1 = rotl64(h1, 51); h2 += h1;
+    h3 ^= h2; h2 = rotl64(h2, 28); h3 += h2;
+    h0 ^= h3; h3 = rotl64(h3, 9);  h0 += h3;
+    h1 ^= h0; h0 = rotl64(h0, 47); h1 += h0;
+    h2 ^= h1; h1 = rotl64(h1, 54); h2 += h1;
+    h3 ^= h2; h2 = rotl64(h2, 32); h3 += h2;
+    h0 ^= h3; h3 = rotl64(h3, 25); h0 += h3;
+    h1 ^= h0; h0 = rotl64(h0, 63); h1 += h0;
+}
+
+// Keys of 8..15 bytes have no ShortMix: h2 = SC + bytes[0..8), h3 = SC + bytes[8..len)
+// (spooky.c:132-149), h0 = seed + 8*len (spooky.c:170).
+__device__ __forceinline__ void spooky_8_15(uint64_t w0, uint64_t w1, uint32_t len, uint64_t seed,
+                                            uint64_t &sig0, uint64_t &sig1) {
+    uint64_t h0 = seed + (uint64_t)len * 8, h1 = seed, h2 = SC + w0, h3 = SC + w1;
+    short_end(h0, h1, h2, h3);
+    sig0 = h0;
+    sig1 = h1;
+}
+
+__device__ __forceinline__ uint64_t low_bytes_mask(uint32_t k) {  // k in 0..8
+    return k >= 8 ? ~0ULL : ((1ULL << (8 * k)) - 1);
+}
+
+// Generic SpookyHash-short over a key read through `rd(off)`, which returns the
+// little-endian u64 at byte offset `off` of the key (bytes past the key end may
+// be garbage: they are masked here).  spooky.c:94-175.
+template <class Reader>
+__device__ __forceinline__ void spooky_short(const Reader &rd, uint32_t len, uint64_t seed,
+                                             uint64_t &sig0, uint64_t &sig1) {
+    uint64_t h0 = seed, h1 = seed, h2 = SC, h3 = SC;
+    uint32_t rem = len & 31, off = 0;
+    if (len > 15) {
+        const uint32_t nblk = len >> 5;
+        for (uint32_t b = 0; b < nblk; ++b, off += 32) {
+            h2 += rd(off);
+            h3 += rd(off + 8);
+            short_mix(h0, h1, h2, h3);
+            h0 += rd(off + 16);
+            h1 += rd(off + 24);
+        }
+        if (rem >= 16) {
+            h2 += rd(off);
+            h3 += rd(off + 8);
+            short_mix(h0, h1, h2, h3);
+            off += 16;
+            rem -= 16;
+        }
+    }
+    if (rem == 0) {
+        h2 += SC;
+        h3 += SC;
+    } else if (rem >= 8) {
+        h2 += rd(off);
+        h3 += rd(off + 8) & low_bytes_mask(rem - 8);
+    } else {
+        h2 += rd(off) & low_bytes_mask(rem);
+    }
+    h0 += (uint64_t)len * 8;
+    short_end(h0, h1, h2, h3);
+    sig0 = h0;
+    sig1 = h1;
+}
+
+// GOV:559 / CBHS:965 -- Math.multiplyHigh(sig0 >>> 1, 2m); sig0>>>1 < 2^63 so the
+// signed and unsigned high products agree.
+__device__ __forceinline__ uint32_t bucket_of(uint64_t sig0, uint64_t multiplier) {
+    return (uint32_t)__umul64hi(sig0 >> 1, multiplier);
+}
+
+// GOV:315-317 (C_TIMES_256 = 281)
+__device__ __forceinline__ uint64_t vertex_offset(uint64_t eos) { return ((eos & OFFSET_MASK) * 281) >> 8; }
+
+// Funnel read of 8 bytes at byte offset `o` of a dword-addressed buffer.
+__device__ __forceinline__ uint64_t funnel64(uint32_t d0, uint32_t d1, uint32_t d2, uint32_t sh) {
+    const uint32_t lo = __builtin_amdgcn_alignbit(d1, d0, sh);
+    const uint32_t hi = __builtin_amdgcn_alignbit(d2, d1, sh);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// SURVEY.md §8(d) D2 synthetic keys (bench input generator only).
+__host__ __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+    uint64_t z = x + 0x9e3779b97f4a7c15ULL;
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
+    return z ^ (z >> 31);
+}
+
+}  // namespace bsdb

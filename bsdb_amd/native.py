@@ -1,0 +1,215 @@
+"""ctypes binding of ``include/bsdb_mi355x.h`` (``libbsdb_mi355x.so``).
+
+This is the product path: every call lands in a hand-written gfx950 kernel.
+There is no CPU fallback -- if the library is missing or a call fails, a
+:class:`BsdbError` is raised (mirroring the reference's JNI convention of
+negative return codes turned into exceptions, ``src/main/c/native.c:29-34``).
+
+Device buffers are ``torch`` tensors (torch is plumbing here: HBM allocation,
+streams, ``torch.distributed``); the C ABI itself takes plain pointers.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from typing import Optional
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libbsdb_mi355x.so")
+HEADER = os.path.join(os.path.dirname(HERE), "include", "bsdb_mi355x.h")
+
+BSDB_OK = 0
+ERRORS = {-22: "EINVAL", -12: "ENOMEM", -5: "EIO", -19: "ENODEV", -17: "EDUP", -34: "ESEEDS"}
+
+# (name, restype, argtypes) -- kept in the order of include/bsdb_mi355x.h
+_vp, _u64, _u32, _i = C.c_void_p, C.c_uint64, C.c_uint32, C.c_int
+SIGNATURES = [
+    ("bsdb_abi_version", _i, []),
+    ("bsdb_strerror", C.c_char_p, [_i]),
+    ("bsdb_open", _i, [_i, C.POINTER(_vp)]),
+    ("bsdb_close", _i, [_vp]),
+    ("bsdb_num_buckets", _u64, [_u64]),
+    ("bsdb_dev_hash_fixed", _i, [_vp, _vp, _u32, _u64, _u64, _vp, _vp]),
+    ("bsdb_dev_hash_var", _i, [_vp, _vp, _u64, _vp, _u64, _u64, _vp, _vp]),
+    ("bsdb_dev_histogram_fixed", _i, [_vp, _vp, _u32, _u64, _u64, _u64, _vp, _vp]),
+    ("bsdb_dev_histogram_var", _i, [_vp, _vp, _u64, _vp, _u64, _u64, _u64, _vp, _vp]),
+    ("bsdb_dev_edge_offsets", _i, [_vp, _vp, _u64, _vp, _vp]),
+    ("bsdb_set_histogram_mode", _i, [_vp, _i]),
+    ("bsdb_set_chunk_keys", _i, [_vp, _u64]),
+    ("bsdb_set_profiling", _i, [_vp, _i]),
+    ("bsdb_profile_read", _i, [_vp, _i, C.POINTER(C.c_double), C.POINTER(_u64), C.POINTER(_u64)]),
+    ("bsdb_histogram_fixed", _i, [_vp, _vp, _u32, _u64, _u64, _u64, _vp]),
+    ("bsdb_hash_fixed", _i, [_vp, _vp, _u32, _u64, _u64, _vp]),
+    ("bsdb_dev_gen_keys13", _i, [_vp, _u64, _u64, _vp, _vp]),
+]
+
+HIST_AUTO, HIST_PARTITIONED, HIST_ATOMIC = 0, 1, 2
+
+
+class BsdbError(RuntimeError):
+    def __init__(self, fn: str, code: int):
+        super().__init__(f"{fn} failed: {code} ({ERRORS.get(code, '?')})")
+        self.code = code
+
+
+_lib: Optional[C.CDLL] = None
+
+
+def lib() -> C.CDLL:
+    """Loads the gfx950 library; raises if it was not built (no fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"{LIB_PATH} missing: run `python -c 'import __graft_entry__ as g; g.build()'` "
+                               "or `make -C bsdb_amd/csrc` (hipcc --offload-arch=gfx950)")
+        # torch's bundled HIP runtime shares the soname libamdhip64.so.7: import
+        # torch first so this library binds to the same runtime instance.
+        import torch  # noqa: F401
+        L = C.CDLL(LIB_PATH)
+        for name, res, args in SIGNATURES:
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def _check(fn: str, rc: int):
+    if rc != BSDB_OK:
+        raise BsdbError(fn, rc)
+
+
+def num_buckets(n: int) -> int:
+    return int(lib().bsdb_num_buckets(n))
+
+
+def _ptr(t) -> int:
+    return t.data_ptr()
+
+
+def _stream(stream) -> Optional[int]:
+    import torch
+    if stream is None:
+        return torch.cuda.current_stream().cuda_stream
+    return stream.cuda_stream if hasattr(stream, "cuda_stream") else int(stream)
+
+
+class Context:
+    """One ``bsdb_ctx`` on one HIP device.  All ``*_dev`` methods take torch
+    tensors resident on that device and enqueue on the current torch stream."""
+
+    def __init__(self, device: int = 0):
+        self._h = C.c_void_p()
+        _check("bsdb_open", lib().bsdb_open(device, C.byref(self._h)))
+        self.device = device
+
+    def close(self):
+        if self._h:
+            _check("bsdb_close", lib().bsdb_close(self._h))
+            self._h = C.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- configuration
+    def set_histogram_mode(self, mode: int):
+        _check("bsdb_set_histogram_mode", lib().bsdb_set_histogram_mode(self._h, mode))
+
+    def set_chunk_keys(self, n: int):
+        _check("bsdb_set_chunk_keys", lib().bsdb_set_chunk_keys(self._h, n))
+
+    # ---- live per-kernel timing (HIP events on the launch stream)
+    PASS1, PASS2, SCAN = 0, 1, 2
+
+    def set_profiling(self, on: bool):
+        _check("bsdb_set_profiling", lib().bsdb_set_profiling(self._h, 1 if on else 0))
+
+    def profile_read(self, kind: int):
+        t, nl, nk = C.c_double(), C.c_uint64(), C.c_uint64()
+        _check("bsdb_profile_read", lib().bsdb_profile_read(self._h, kind, C.byref(t), C.byref(nl), C.byref(nk)))
+        return t.value, nl.value, nk.value
+
+    # ---- A3: signatures
+    def hash_fixed(self, keys, key_len: int, seed: int = 0, out=None, stream=None):
+        import torch
+        n = keys.numel() // key_len if key_len else 0
+        if out is None:
+            out = torch.empty((n, 2), dtype=torch.int64, device=keys.device)
+        _check("bsdb_dev_hash_fixed", lib().bsdb_dev_hash_fixed(
+            self._h, _ptr(keys), key_len, n, seed & (2**64 - 1), _ptr(out), _stream(stream)))
+        return out
+
+    def hash_var(self, blob, offsets, seed: int = 0, out=None, stream=None):
+        import torch
+        n = offsets.numel() - 1
+        if out is None:
+            out = torch.empty((n, 2), dtype=torch.int64, device=offsets.device)
+        _check("bsdb_dev_hash_var", lib().bsdb_dev_hash_var(
+            self._h, _ptr(blob), blob.numel(), _ptr(offsets), n, seed & (2**64 - 1), _ptr(out), _stream(stream)))
+        return out
+
+    # ---- A3+A4+A6: bucket-occupancy histogram (accumulating)
+    def histogram_fixed(self, keys, key_len: int, m: int, counts=None, seed: int = 0, n: Optional[int] = None,
+                        stream=None):
+        import torch
+        if n is None:
+            n = keys.numel() // key_len
+        if counts is None:
+            counts = torch.zeros(m, dtype=torch.int32, device=keys.device)
+        _check("bsdb_dev_histogram_fixed", lib().bsdb_dev_histogram_fixed(
+            self._h, _ptr(keys), key_len, n, seed & (2**64 - 1), m, _ptr(counts), _stream(stream)))
+        return counts
+
+    def histogram_var(self, blob, offsets, m: int, counts=None, seed: int = 0, stream=None):
+        import torch
+        if counts is None:
+            counts = torch.zeros(m, dtype=torch.int32, device=offsets.device)
+        _check("bsdb_dev_histogram_var", lib().bsdb_dev_histogram_var(
+            self._h, _ptr(blob), blob.numel(), _ptr(offsets), offsets.numel() - 1, seed & (2**64 - 1), m,
+            _ptr(counts), _stream(stream)))
+        return counts
+
+    def edge_offsets(self, counts, out=None, stream=None):
+        import torch
+        m = counts.numel()
+        if out is None:
+            out = torch.empty(m + 1, dtype=torch.int64, device=counts.device)
+        _check("bsdb_dev_edge_offsets", lib().bsdb_dev_edge_offsets(
+            self._h, _ptr(counts), m, _ptr(out), _stream(stream)))
+        return out
+
+    def gen_keys13(self, first: int, n: int, out=None, stream=None):
+        import torch
+        if out is None:
+            out = torch.empty(13 * n + 16, dtype=torch.uint8, device=f"cuda:{self.device}")
+        _check("bsdb_dev_gen_keys13", lib().bsdb_dev_gen_keys13(self._h, first, n, _ptr(out), _stream(stream)))
+        return out
+
+    # ---- host-buffer API (numpy in, numpy out; includes H2D/D2H)
+    def histogram_fixed_host(self, keys_np, key_len: int, m: int, counts_np=None, seed: int = 0):
+        import numpy as np
+        keys_np = np.ascontiguousarray(keys_np, np.uint8)
+        if counts_np is None:
+            counts_np = np.zeros(m, np.uint32)
+        n = keys_np.size // key_len
+        _check("bsdb_histogram_fixed", lib().bsdb_histogram_fixed(
+            self._h, keys_np.ctypes.data, key_len, n, seed & (2**64 - 1), m, counts_np.ctypes.data))
+        return counts_np
+
+    def hash_fixed_host(self, keys_np, key_len: int, seed: int = 0):
+        import numpy as np
+        keys_np = np.ascontiguousarray(keys_np, np.uint8)
+        n = keys_np.size // key_len
+        out = np.zeros((max(n, 1), 2), np.uint64)
+        _check("bsdb_hash_fixed", lib().bsdb_hash_fixed(
+            self._h, keys_np.ctypes.data, key_len, n, seed & (2**64 - 1), out.ctypes.data))
+        return out[:n]

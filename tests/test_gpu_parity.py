@@ -1,0 +1,177 @@
+"""GPU parity: the gfx950 kernels, called through the C ABI, against the CPU
+oracle (itself pinned to the reference C by tests/test_oracle_golden.py).
+Integer/byte work: every comparison is bit-exact."""
+import numpy as np
+import pytest
+
+import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from bsdb_amd import Context
+    c = Context(0)
+    yield c
+    c.close()
+
+
+def dev(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+def u64(t):
+    return t.cpu().numpy().view(np.uint64)
+
+
+def rand_keys(n, L, seed=1):
+    return np.random.default_rng(seed).integers(0, 256, n * L, dtype=np.uint8)
+
+
+@pytest.mark.parametrize("L", [1, 2, 7, 8, 9, 12, 13, 14, 15, 16, 17, 26, 27, 31, 32, 33, 47, 52, 53, 64, 100, 255])
+def test_hash_fixed_lengths(ctx, L):
+    n = 20_001  # ragged: 2 full tiles + a partial one
+    keys = rand_keys(n, L, L)
+    got = u64(ctx.hash_fixed(dev(keys), L, seed=0))
+    np.testing.assert_array_equal(got, O.hash_fixed(keys, L))
+
+
+def test_hash_fixed_seed(ctx):
+    keys = rand_keys(10_000, 13)
+    for seed in (0x0123456789ABCDEF, 1 << 63):
+        np.testing.assert_array_equal(u64(ctx.hash_fixed(dev(keys), 13, seed=seed)), O.hash_fixed(keys, 13, seed))
+
+
+def test_hash_every_length_golden(ctx, golden):
+    msg = golden["len_msg"]
+    keys = [msg[:L].tobytes() for L in range(201)]
+    off = np.zeros(len(keys) + 1, np.uint64)
+    off[1:] = np.cumsum([len(k) for k in keys])
+    blob = np.frombuffer(b"".join(keys), np.uint8)
+    for si, seed in enumerate(golden["len_seeds"]):
+        got = u64(ctx.hash_var(dev(blob), dev(off.view(np.int64)), seed=int(seed)))
+        np.testing.assert_array_equal(got, golden["len_sig"][si, :, :2])
+
+
+def test_hash_var_golden(ctx, golden):
+    got = u64(ctx.hash_var(dev(golden["var_blob"]), dev(golden["var_off"].view(np.int64))))
+    np.testing.assert_array_equal(got, golden["var_sig"])
+
+
+def test_native_test_keys_histogram(ctx, golden):
+    keys = [str(i).encode() for i in range(1_000_000)]
+    off = np.zeros(len(keys) + 1, np.uint64)
+    off[1:] = np.cumsum([len(k) for k in keys])
+    blob = np.frombuffer(b"".join(keys), np.uint8)
+    sig = u64(ctx.hash_var(dev(blob), dev(off.view(np.int64))))
+    np.testing.assert_array_equal(sig[golden["native_sample_idx"]], golden["native_sample_sig"])
+    m = O.num_buckets(1_000_000)
+    counts = ctx.histogram_var(dev(blob), dev(off.view(np.int64)), m).cpu().numpy()
+    np.testing.assert_array_equal(counts.view(np.uint32), golden["native_counts"])
+
+
+@pytest.mark.parametrize("mode", [0, 2])
+def test_k13_histogram_golden(ctx, golden, mode):
+    keys = O.gen_keys13(0, 1_000_000)
+    m = O.num_buckets(1_000_000)
+    ctx.set_histogram_mode(mode)
+    try:
+        counts = ctx.histogram_fixed(dev(keys), 13, m).cpu().numpy().view(np.uint32)
+    finally:
+        ctx.set_histogram_mode(0)
+    np.testing.assert_array_equal(counts, golden["k13_counts"])
+
+
+def test_device_key_generator(ctx, golden):
+    d = ctx.gen_keys13(0, 1_000_000)
+    np.testing.assert_array_equal(d[: 13 * 1_000_000].cpu().numpy(), O.gen_keys13(0, 1_000_000))
+    d = ctx.gen_keys13(123_456_789_000, 5_000)
+    np.testing.assert_array_equal(d[: 13 * 5_000].cpu().numpy(), O.gen_keys13(123_456_789_000, 5_000))
+
+
+@pytest.mark.parametrize("L", [13, 5, 20, 40, 80])
+@pytest.mark.parametrize("m", [1, 667, 32_768, 32_769, 8_795_859])
+def test_histogram_partitioned_many_partitions(ctx, L, m):
+    # m up to the C4 bucket count: 269 partitions of 32768 buckets
+    n = 300_007
+    keys = rand_keys(n, L, m % 97 + L)
+    counts = ctx.histogram_fixed(dev(keys), L, m).cpu().numpy().view(np.uint32)
+    np.testing.assert_array_equal(counts, O.histogram_fixed(keys, L, m))
+
+
+def test_histogram_multi_chunk_and_accumulate(ctx):
+    n = 100_003
+    keys = O.gen_keys13(77, n)
+    m = 5_000
+    ctx.set_chunk_keys(8192 * 3)
+    try:
+        c = ctx.histogram_fixed(dev(keys), 13, m)
+        c = ctx.histogram_fixed(dev(keys), 13, m, counts=c)  # accumulates
+    finally:
+        ctx.set_chunk_keys(0)
+    np.testing.assert_array_equal(c.cpu().numpy().view(np.uint32), 2 * O.histogram_fixed(keys, 13, m))
+
+
+def test_histogram_overflow_fallback(ctx):
+    # one key repeated: every id lands in one partition region -> overflow ->
+    # the in-stream fallback recounts the chunk with direct atomics
+    n = 1_000_000
+    keys = np.tile(np.frombuffer(b"abcdefghijklm", np.uint8), n)
+    m = 8_795_859
+    counts = ctx.histogram_fixed(dev(keys), 13, m).cpu().numpy().view(np.uint32)
+    b = O.bucket(O.spooky_short(b"abcdefghijklm")[0], m)
+    assert counts[b] == n and counts.sum() == n
+
+
+def test_empty_and_tiny(ctx):
+    m = 10
+    keys = torch.zeros(16, dtype=torch.uint8, device="cuda")
+    c = ctx.histogram_fixed(keys, 13, m, n=0)
+    assert int(c.sum()) == 0
+    one = O.gen_keys13(5, 1)
+    c = ctx.histogram_fixed(dev(one), 13, m).cpu().numpy().view(np.uint32)
+    np.testing.assert_array_equal(c, O.histogram_fixed(one, 13, m))
+    assert ctx.hash_fixed(keys, 13).shape[0] == 1  # 16 bytes -> one 13-byte key
+
+
+def test_edge_offsets(ctx):
+    rng = np.random.default_rng(3)
+    for m in (1, 2, 1000, 8192, 8193, 3_000_001):
+        c = rng.integers(0, 3000, m, dtype=np.int64).astype(np.int32)
+        E = ctx.edge_offsets(dev(c)).cpu().numpy().view(np.uint64)
+        np.testing.assert_array_equal(E, O.edge_offsets(c.view(np.uint32)))
+
+
+def test_host_buffer_api(ctx):
+    keys = O.gen_keys13(1000, 200_000)
+    m = O.num_buckets(200_000)
+    np.testing.assert_array_equal(ctx.histogram_fixed_host(keys, 13, m), O.histogram_fixed(keys, 13, m))
+    np.testing.assert_array_equal(ctx.hash_fixed_host(keys, 13), O.hash_fixed(keys, 13))
+
+
+def test_full_size_properties(ctx):
+    """At a large size: total count, partitioned == atomic, sampled signatures."""
+    n = 400_000_000
+    keys = ctx.gen_keys13(0, n)
+    m = O.num_buckets(n)
+    c_part = ctx.histogram_fixed(keys, 13, m, n=n)
+    ctx.set_histogram_mode(2)
+    try:
+        c_atom = ctx.histogram_fixed(keys, 13, m, n=n)
+    finally:
+        ctx.set_histogram_mode(0)
+    assert int(c_part.sum(dtype=torch.int64)) == n
+    assert torch.equal(c_part, c_atom)
+    E = ctx.edge_offsets(c_part)
+    assert int(E[-1]) == n
+    idx = np.arange(0, n, 9_999_991)
+    sample = torch.cat([keys[13 * int(i): 13 * int(i) + 13] for i in idx]).cpu().numpy()
+    np.testing.assert_array_equal(sample, O.gen_keys13(0, 1) if False else np.concatenate([O.gen_keys13(int(i), 1) for i in idx]))
+    sig = u64(ctx.hash_fixed(dev(sample), 13))
+    np.testing.assert_array_equal(sig, O.hash_fixed(sample, 13))
+    del keys
