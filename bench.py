@@ -25,18 +25,12 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+from bsdb_amd.distributed import global_histogram, shard  # noqa: E402
+
 README_N = 13_193_787_549     # README.md:50-60 record count
 KEY_LEN = 13
 HBM_PEAK_GBS = 8000.0         # MI355X_MICROARCH.md chip table: 8.0 TB/s HBM3E
-TILE = 8192                   # pass-1 tile: shard boundaries stay tile aligned
 
-
-def shard(n: int, rank: int, world: int):
-    """Contiguous key shard of rank r, tile aligned (by input order)."""
-    tiles = (n + TILE - 1) // TILE
-    lo = tiles * rank // world * TILE
-    hi = min(n, tiles * (rank + 1) // world * TILE)
-    return lo, hi
 
 
 def cpu_baseline(m: int, target_s: float, threads: int):
@@ -111,10 +105,8 @@ def main():
     torch.cuda.synchronize()
 
     def step():
-        counts.zero_()
-        ctx.histogram_fixed(keys, KEY_LEN, m, counts=counts, n=nloc)
-        if world > 1:
-            dist.all_reduce(counts)             # RCCL over xGMI: the global histogram
+        # local shard histogram, then ONE all-reduce over RCCL/xGMI (N>1)
+        global_histogram(lambda c: ctx.histogram_fixed(keys, KEY_LEN, m, counts=c, n=nloc), counts)
         ctx.edge_offsets(counts, out=E)
 
     for _ in range(args.warmup):

@@ -84,7 +84,9 @@ int grow(void **p, size_t *have, size_t need) {
     return BSDB_OK;
 }
 
-hipStream_t pick(bsdb_ctx *c, void *stream) { return stream ? (hipStream_t)stream : c->stream; }
+// NULL is the HIP null stream (torch's default stream reports handle 0), not
+// the context's private stream, which only the host-buffer entry points use.
+hipStream_t pick(bsdb_ctx *, void *stream) { return (hipStream_t)stream; }
 
 int launch_status() { return hipGetLastError() == hipSuccess ? BSDB_OK : BSDB_EIO; }
 

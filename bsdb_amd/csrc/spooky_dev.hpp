@@ -14,7 +14,23 @@ constexpr uint64_t SC = 0x9e3779b97f4a7c13ULL;  // spooky.c:39
 constexpr uint64_t OFFSET_MASK = ~0ULL >> 8;    // GOV:157
 constexpr uint32_t BUCKET_SIZE = 1500;          // GOV:281
 
-__device__ __forceinline__ uint64_t rotl64(uint64_t x, int k) { return (x << k) | (x >> (64 - k)); }
+// 64-bit rotate by a constant as two v_alignbit_b32 (the generic shift/or form
+// costs 2 v_lshl*_b64 + 2 v_or_b32).
+__device__ __forceinline__ uint64_t rotl64(uint64_t x, int k) {
+    const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+    uint32_t nhi, nlo;
+    if (k < 32) {
+        nhi = __builtin_amdgcn_alignbit(hi, lo, 32 - k);
+        nlo = __builtin_amdgcn_alignbit(lo, hi, 32 - k);
+    } else if (k == 32) {
+        nhi = lo;
+        nlo = hi;
+    } else {
+        nhi = __builtin_amdgcn_alignbit(lo, hi, 64 - k);
+        nlo = __builtin_amdgcn_alignbit(hi, lo, 64 - k);
+    }
+    return ((uint64_t)nhi << 32) | nlo;
+}
 
 // spooky.c:55-68
 __device__ __forceinline__ void short_mix(uint64_t &h0, uint64_t &h1, uint64_t &h2, uint64_t &h3) {

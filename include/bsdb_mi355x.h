@@ -11,7 +11,7 @@
  *
  * Two families of entry points:
  *   bsdb_dev_*  operate on DEVICE pointers (HBM-resident keys) on a caller
- *               stream (hipStream_t passed as void*, NULL = the context stream).
+ *               stream (hipStream_t passed as void*; NULL = the HIP null stream).
  *               Asynchronous: they enqueue and return.
  *   bsdb_*      (no dev_) take HOST pointers (a Java DirectByteBuffer / LBuffer
  *               address), stream them through the context's device staging
