@@ -24,6 +24,7 @@ struct bsdb_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     int hist_mode = 0;
+    int frontend = 0;  // 13-byte keys: 0 auto (direct), 1 LDS-staged, 2 direct
     uint64_t chunk_keys = 0;
     std::mutex mu;
     // workspace
@@ -92,10 +93,12 @@ int launch_status() { return hipGetLastError() == hipSuccess ? BSDB_OK : BSDB_EI
 
 // ---- pass-1 dispatch over (source layout, epilogue) ------------------------
 template <int EPI>
-void launch_pass1(const P1Args &a, bool var, uint32_t key_len, uint64_t tiles, hipStream_t s) {
+void launch_pass1(const P1Args &a, bool var, uint32_t key_len, uint64_t tiles, hipStream_t s, int frontend) {
     const dim3 g((uint32_t)tiles), b(P1_THREADS);
     if (var) {
         k_pass1<SRC_VAR, EPI, 1, 0><<<g, b, 0, s>>>(a);
+    } else if (key_len == 13 && frontend != 1) {
+        k_pass1<SRC_DIRECT13, EPI, 4, 13><<<g, b, 0, s>>>(a);
     } else if (key_len == 13) {
         k_pass1<SRC_STAGED13, EPI, 4, 13><<<g, b, 0, s>>>(a);
     } else if (key_len >= 1 && key_len <= 13) {
@@ -154,7 +157,7 @@ int histogram_impl(bsdb_ctx *c, const uint8_t *keys, const uint64_t *offsets, ui
     if (atomic_mode) {
         a.n = n;
         ProfScope ps(c, s, 0, n);
-        launch_pass1<EPI_ATOMIC>(a, var, key_len, (n + P1_TILE - 1) / P1_TILE, s);
+        launch_pass1<EPI_ATOMIC>(a, var, key_len, (n + P1_TILE - 1) / P1_TILE, s, c->frontend);
         return launch_status();
     }
     uint64_t chunk = c->chunk_keys ? c->chunk_keys : DEFAULT_CHUNK_KEYS;
@@ -182,7 +185,7 @@ int histogram_impl(bsdb_ctx *c, const uint8_t *keys, const uint64_t *offsets, ui
         HIP_OK(hipMemsetAsync(c->overflow, 0, sizeof(uint32_t), s));
         {
             ProfScope ps(c, s, 0, nk);
-            launch_pass1<EPI_PARTITION>(ac, var, key_len, (nk + P1_TILE - 1) / P1_TILE, s);
+            launch_pass1<EPI_PARTITION>(ac, var, key_len, (nk + P1_TILE - 1) / P1_TILE, s, c->frontend);
         }
         {
             ProfScope ps(c, s, 1, nk);
@@ -199,7 +202,7 @@ int histogram_impl(bsdb_ctx *c, const uint8_t *keys, const uint64_t *offsets, ui
     return BSDB_OK;
 }
 
-int hash_impl(const uint8_t *keys, const uint64_t *offsets, uint64_t blob_bytes, uint32_t key_len,
+int hash_impl(bsdb_ctx *c, const uint8_t *keys, const uint64_t *offsets, uint64_t blob_bytes, uint32_t key_len,
               uint64_t n, uint64_t seed, uint64_t *sig, hipStream_t s) {
     if (n == 0) return BSDB_OK;
     P1Args a{};
@@ -210,7 +213,7 @@ int hash_impl(const uint8_t *keys, const uint64_t *offsets, uint64_t blob_bytes,
     a.n = n;
     a.seed = seed;
     a.sig = sig;
-    launch_pass1<EPI_SIG>(a, offsets != nullptr, key_len, (n + P1_TILE - 1) / P1_TILE, s);
+    launch_pass1<EPI_SIG>(a, offsets != nullptr, key_len, (n + P1_TILE - 1) / P1_TILE, s, c->frontend);
     return launch_status();
 }
 
@@ -282,6 +285,13 @@ int bsdb_set_histogram_mode(bsdb_ctx *c, int mode) {
     return BSDB_OK;
 }
 
+int bsdb_set_frontend(bsdb_ctx *c, int frontend) {
+    if (!c || frontend < 0 || frontend > 2) return BSDB_EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    c->frontend = frontend;
+    return BSDB_OK;
+}
+
 int bsdb_set_chunk_keys(bsdb_ctx *c, uint64_t chunk_keys) {
     if (!c) return BSDB_EINVAL;
     std::lock_guard<std::mutex> g(c->mu);
@@ -294,7 +304,7 @@ int bsdb_dev_hash_fixed(bsdb_ctx *c, const uint8_t *d_keys, uint32_t key_len, ui
     if (!c || (n && (!d_keys || !d_sig)) || !aligned16(d_keys) || !aligned16(d_sig)) return BSDB_EINVAL;
     std::lock_guard<std::mutex> g(c->mu);
     HIP_OK(hipSetDevice(c->device));
-    return hash_impl(d_keys, nullptr, n * key_len, key_len, n, seed, d_sig, pick(c, stream));
+    return hash_impl(c, d_keys, nullptr, n * key_len, key_len, n, seed, d_sig, pick(c, stream));
 }
 
 int bsdb_dev_hash_var(bsdb_ctx *c, const uint8_t *d_blob, uint64_t blob_bytes, const uint64_t *d_off, uint64_t n,
@@ -302,7 +312,7 @@ int bsdb_dev_hash_var(bsdb_ctx *c, const uint8_t *d_blob, uint64_t blob_bytes, c
     if (!c || (n && (!d_blob || !d_off || !d_sig)) || !aligned16(d_sig)) return BSDB_EINVAL;
     std::lock_guard<std::mutex> g(c->mu);
     HIP_OK(hipSetDevice(c->device));
-    return hash_impl(d_blob, d_off, blob_bytes, 0, n, seed, d_sig, pick(c, stream));
+    return hash_impl(c, d_blob, d_off, blob_bytes, 0, n, seed, d_sig, pick(c, stream));
 }
 
 int bsdb_dev_histogram_fixed(bsdb_ctx *c, const uint8_t *d_keys, uint32_t key_len, uint64_t n, uint64_t seed,
@@ -420,7 +430,7 @@ int bsdb_hash_fixed(bsdb_ctx *c, const uint8_t *h_keys, uint32_t key_len, uint64
     for (uint64_t k0 = 0; k0 < n; k0 += batch) {
         const uint64_t nk = std::min(batch, n - k0);
         HIP_OK(hipMemcpyAsync(c->d_keys, h_keys + k0 * key_len, nk * key_len, hipMemcpyHostToDevice, s));
-        if ((rc = hash_impl(c->d_keys, nullptr, nk * key_len, key_len, nk, seed, (uint64_t *)c->d_out, s))) return rc;
+        if ((rc = hash_impl(c, c->d_keys, nullptr, nk * key_len, key_len, nk, seed, (uint64_t *)c->d_out, s))) return rc;
         HIP_OK(hipMemcpyAsync(h_sig + 2 * k0, c->d_out, nk * 16, hipMemcpyDeviceToHost, s));
     }
     HIP_OK(hipStreamSynchronize(s));

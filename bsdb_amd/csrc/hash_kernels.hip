@@ -31,7 +31,7 @@ constexpr int NCOPY = 8;                                  // cursor/region copie
 constexpr int P2_THREADS = 1024;
 
 enum Epi { EPI_PARTITION = 0, EPI_ATOMIC = 1, EPI_SIG = 2 };
-enum Src { SRC_STAGED13 = 0, SRC_STAGED = 1, SRC_FIXED_DIRECT = 2, SRC_VAR = 3 };
+enum Src { SRC_STAGED13 = 0, SRC_STAGED = 1, SRC_FIXED_DIRECT = 2, SRC_VAR = 3, SRC_DIRECT13 = 4 };
 
 struct P1Args {
     const uint8_t *keys;      // fixed: n*key_len bytes; var: blob
@@ -54,6 +54,9 @@ struct P1Args {
 };
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+// 16-byte vector with 4-byte alignment: global_load_dwordx4 at a dword-aligned
+// address (the 13-byte-key windows of the direct front end).
+typedef unsigned int u32x4a __attribute__((ext_vector_type(4), aligned(4)));
 
 // Streaming 16-byte load, read-once data (keys, partition ids): nontemporal so
 // the stream does not evict the re-used tables from L2 / Infinity Cache.
@@ -62,15 +65,24 @@ __device__ __forceinline__ uint4 ntload16(const void *p) {
     return make_uint4(v.x, v.y, v.z, v.w);
 }
 
-// Bounds-checked little-endian u64 read from global memory.
+// Bounds-checked little-endian u64 read from global memory: dword loads in the
+// body, byte loads for the ragged last dword of the blob (never past `limit`).
+__device__ __forceinline__ uint32_t gload32(const uint8_t *base, uint64_t limit, uint64_t a) {
+    if (a + 4 <= limit) return *reinterpret_cast<const uint32_t *>(base + a);
+    uint32_t w = 0;
+    for (int b = 0; b < 4; ++b)
+        if (a + b < limit) w |= (uint32_t)base[a + b] << (8 * b);
+    return w;
+}
+
 __device__ __forceinline__ uint64_t gload64(const uint8_t *base, uint64_t limit, uint64_t pos) {
     const uint64_t a = pos & ~3ULL;
     const uint32_t sh = (uint32_t)(pos & 3) * 8;
-    const uint32_t *q = reinterpret_cast<const uint32_t *>(base + a);
-    const uint32_t d0 = a + 4 <= limit ? q[0] : 0;
-    const uint32_t d1 = a + 8 <= limit ? q[1] : 0;
-    const uint32_t d2 = a + 12 <= limit ? q[2] : 0;
-    return funnel64(d0, d1, d2, sh);
+    if (a + 12 <= limit) {
+        const uint32_t *q = reinterpret_cast<const uint32_t *>(base + a);
+        return funnel64(q[0], q[1], q[2], sh);
+    }
+    return funnel64(gload32(base, limit, a), gload32(base, limit, a + 4), gload32(base, limit, a + 8), sh);
 }
 
 // Copies bytes [src_lo, src_lo + nbytes) of global memory into LDS starting at
@@ -115,12 +127,10 @@ __device__ __forceinline__ void hash_staged(const uint32_t *stage, uint32_t k, u
     if (LFIX == 13) {
         const uint32_t *q = stage + (o >> 2);
         const uint32_t sh = (o & 3) * 8;
-        const uint32_t d0 = q[0], d1 = q[1], d2 = q[2], d3 = q[3];
-        const uint64_t w0 = funnel64(d0, d1, d2, sh);
-        const uint32_t w1lo = __builtin_amdgcn_alignbit(d3, d2, sh);
-        const uint32_t b12 = (d3 >> sh) & 0xFF;
-        const uint64_t w1 = ((uint64_t)b12 << 32) | w1lo;
-        spooky_8_15(w0, w1, 13, seed, s0, s1);
+        W64 a0, a1;
+        spooky13_w(q[0], q[1], q[2], q[3], sh, w64(seed), a0, a1);
+        s0 = u64(a0);
+        s1 = u64(a1);
     } else {
         auto rd = [&](uint32_t off) -> uint64_t {
             const uint32_t p = o + off;
@@ -175,11 +185,12 @@ __global__ __launch_bounds__(P1_THREADS, 4) void k_pass1(P1Args a) {
         for (int i = tid; i < MAX_PARTS; i += P1_THREADS) hist[i] = 0;
     }
 
+    const uint32_t mult = (uint32_t)a.multiplier;  // 2m < 2^32 (checked by the C ABI)
     auto emit = [&](uint32_t kt, uint64_t gk, uint64_t s0, uint64_t s1) {
         if (EPI == EPI_SIG) {
             reinterpret_cast<ulonglong2 *>(a.sig)[gk] = make_ulonglong2(s0, s1);
         } else {
-            const uint32_t b = bucket_of(s0, a.multiplier);
+            const uint32_t b = bucket_of_w(w64(s0), mult);
             if (EPI == EPI_ATOMIC) {
                 atomicAdd(a.counts + b, 1u);
             } else {
@@ -189,7 +200,43 @@ __global__ __launch_bounds__(P1_THREADS, 4) void k_pass1(P1Args a) {
         }
     };
 
-    if (SRC == SRC_STAGED13 || SRC == SRC_STAGED) {
+    if (SRC == SRC_DIRECT13) {
+        // 13-byte keys without LDS staging: lane t of a wave loads the
+        // dword-aligned 16-byte window holding its key (a wave covers 832
+        // contiguous bytes, so the loads coalesce into whole lines); all 16
+        // windows of a thread are issued before the first hash, keeping
+        // 16 KiB per wave in flight with no barrier until the tile epilogue.
+        if (EPI == EPI_PARTITION) __syncthreads();
+        const bool careful = (tile0 + P1_TILE) * 13 + 3 > a.blob_bytes;  // last tile: bounds-checked
+        if (!careful) {
+            u32x4a win[P1_KEYS_PER_THREAD];
+#pragma unroll
+            for (int j = 0; j < P1_KEYS_PER_THREAD; ++j) {
+                const uint64_t byte = (tile0 + tid + j * P1_THREADS) * 13;
+                win[j] = __builtin_nontemporal_load(reinterpret_cast<const u32x4a *>(a.keys + (byte & ~3ULL)));
+            }
+            const W64 seedw = w64(a.seed);
+#pragma unroll
+            for (int j = 0; j < P1_KEYS_PER_THREAD; ++j) {
+                const uint32_t kt = tid + j * P1_THREADS;
+                const uint32_t sh = ((kt * 13u) & 3u) * 8u;  // tile0*13 is a multiple of 4
+                W64 s0, s1;
+                spooky13_w(win[j].x, win[j].y, win[j].z, win[j].w, sh, seedw, s0, s1);
+                emit(kt, tile0 + kt, u64(s0), u64(s1));
+            }
+        } else {
+            for (int j = 0; j < P1_KEYS_PER_THREAD; ++j) {
+                const uint32_t kt = tid + j * P1_THREADS;
+                if (kt < tile_n) {
+                    const uint64_t pos = (tile0 + kt) * 13;
+                    auto rd = [&](uint32_t off) -> uint64_t { return gload64(a.keys, a.blob_bytes, pos + off); };
+                    uint64_t s0, s1;
+                    spooky_short(rd, 13, a.seed, s0, s1);
+                    emit(kt, tile0 + kt, s0, s1);
+                }
+            }
+        }
+    } else if (SRC == SRC_STAGED13 || SRC == SRC_STAGED) {
         // sub-tile = P1_THREADS*KPS keys staged through LDS with 16-B loads,
         // next sub-tile prefetched into registers while this one hashes.
         constexpr int SUB = P1_THREADS * KPS;

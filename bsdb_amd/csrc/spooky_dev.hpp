@@ -133,6 +133,65 @@ __device__ __forceinline__ uint64_t funnel64(uint32_t d0, uint32_t d1, uint32_t 
     return ((uint64_t)hi << 32) | lo;
 }
 
+// ---- 32-bit-half formulation --------------------------------------------
+// The same arithmetic with every 64-bit word held as two VGPRs: xor = 2
+// v_xor_b32, rotate = 2 v_alignbit_b32, add = v_add_co_u32 + v_addc_co_u32.
+// Unlike v_lshl_add_u64 this needs no even-aligned register pairs, so the
+// allocator inserts no v_mov_b32 shuffles (measured: ~34 moves/key saved).
+struct W64 {
+    uint32_t lo, hi;
+};
+
+__device__ __forceinline__ W64 w64(uint64_t x) { return W64{(uint32_t)x, (uint32_t)(x >> 32)}; }
+__device__ __forceinline__ uint64_t u64(W64 x) { return ((uint64_t)x.hi << 32) | x.lo; }
+
+__device__ __forceinline__ W64 add(W64 a, W64 b) {
+    unsigned int c;
+    W64 r;
+    r.lo = __builtin_addc(a.lo, b.lo, 0u, &c);
+    r.hi = __builtin_addc(a.hi, b.hi, c, &c);
+    return r;
+}
+__device__ __forceinline__ W64 xor_(W64 a, W64 b) { return W64{a.lo ^ b.lo, a.hi ^ b.hi}; }
+template <int K>
+__device__ __forceinline__ W64 rotl(W64 x) {
+    if (K < 32) return W64{__builtin_amdgcn_alignbit(x.lo, x.hi, 32 - K), __builtin_amdgcn_alignbit(x.hi, x.lo, 32 - K)};
+    if (K == 32) return W64{x.hi, x.lo};
+    return W64{__builtin_amdgcn_alignbit(x.hi, x.lo, 64 - K), __builtin_amdgcn_alignbit(x.lo, x.hi, 64 - K)};
+}
+
+#define BSDB_END_STEP(D, C, K) D = xor_(D, C); C = rotl<K>(C); D = add(D, C);
+// spooky.c:72-84 on W64 halves.
+__device__ __forceinline__ void short_end_w(W64 &h0, W64 &h1, W64 &h2, W64 &h3) {
+    BSDB_END_STEP(h3, h2, 15) BSDB_END_STEP(h0, h3, 52) BSDB_END_STEP(h1, h0, 26)
+    BSDB_END_STEP(h2, h1, 51) BSDB_END_STEP(h3, h2, 28) BSDB_END_STEP(h0, h3, 9)
+    BSDB_END_STEP(h1, h0, 47) BSDB_END_STEP(h2, h1, 54) BSDB_END_STEP(h3, h2, 32)
+    BSDB_END_STEP(h0, h3, 25) BSDB_END_STEP(h1, h0, 63)
+}
+#undef BSDB_END_STEP
+
+// 13-byte key given as its first 16 little-endian bytes d0..d3 shifted by sh
+// bits (the key starts at byte sh/8 of d0): spooky.c tail case 13 + ShortEnd.
+__device__ __forceinline__ void spooky13_w(uint32_t d0, uint32_t d1, uint32_t d2, uint32_t d3, uint32_t sh,
+                                           W64 seed, W64 &sig0, W64 &sig1) {
+    const W64 w0{__builtin_amdgcn_alignbit(d1, d0, sh), __builtin_amdgcn_alignbit(d2, d1, sh)};
+    const W64 w1{__builtin_amdgcn_alignbit(d3, d2, sh), (d3 >> sh) & 0xFFu};
+    const W64 sc = w64(SC);
+    W64 h0 = add(seed, W64{13 * 8, 0}), h1 = seed, h2 = add(sc, w0), h3 = add(sc, w1);
+    short_end_w(h0, h1, h2, h3);
+    sig0 = h0;
+    sig1 = h1;
+}
+
+// GOV:559 bucket with the multiplier 2m < 2^32 (GOV:349 caps m at
+// Integer.MAX_VALUE): hi64((sig0>>>1) * M) = (xh*M + hi32(xl*M)) >> 32.
+__device__ __forceinline__ uint32_t bucket_of_w(W64 sig0, uint32_t mult) {
+    const uint32_t xl = __builtin_amdgcn_alignbit(sig0.hi, sig0.lo, 1);
+    const uint32_t xh = sig0.hi >> 1;
+    const uint64_t t = (uint64_t)xh * mult + __umulhi(xl, mult);
+    return (uint32_t)(t >> 32);
+}
+
 // SURVEY.md §8(d) D2 synthetic keys (bench input generator only).
 __host__ __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
     uint64_t z = x + 0x9e3779b97f4a7c15ULL;

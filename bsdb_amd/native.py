@@ -35,6 +35,7 @@ SIGNATURES = [
     ("bsdb_dev_histogram_var", _i, [_vp, _vp, _u64, _vp, _u64, _u64, _u64, _vp, _vp]),
     ("bsdb_dev_edge_offsets", _i, [_vp, _vp, _u64, _vp, _vp]),
     ("bsdb_set_histogram_mode", _i, [_vp, _i]),
+    ("bsdb_set_frontend", _i, [_vp, _i]),
     ("bsdb_set_chunk_keys", _i, [_vp, _u64]),
     ("bsdb_set_profiling", _i, [_vp, _i]),
     ("bsdb_profile_read", _i, [_vp, _i, C.POINTER(C.c_double), C.POINTER(_u64), C.POINTER(_u64)]),
@@ -123,6 +124,9 @@ class Context:
     # ---- configuration
     def set_histogram_mode(self, mode: int):
         _check("bsdb_set_histogram_mode", lib().bsdb_set_histogram_mode(self._h, mode))
+
+    def set_frontend(self, frontend: int):
+        _check("bsdb_set_frontend", lib().bsdb_set_frontend(self._h, frontend))
 
     def set_chunk_keys(self, n: int):
         _check("bsdb_set_chunk_keys", lib().bsdb_set_chunk_keys(self._h, n))

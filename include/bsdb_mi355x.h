@@ -94,6 +94,9 @@ int bsdb_dev_edge_offsets(bsdb_ctx *ctx, const uint32_t *d_counts, uint64_t num_
 /* Histogram path selection for bsdb_dev_histogram_* (benchmarks/tests):
  *   0 = auto (partitioned two-pass), 1 = partitioned two-pass, 2 = direct atomics. */
 int bsdb_set_histogram_mode(bsdb_ctx *ctx, int mode);
+/* Key-load front end for 13-byte keys: 0 = auto (direct dword-aligned 16-byte
+ * windows), 1 = LDS-staged sub-tiles, 2 = direct. */
+int bsdb_set_frontend(bsdb_ctx *ctx, int frontend);
 /* Per-chunk key count of the partitioned path (0 = default). */
 int bsdb_set_chunk_keys(bsdb_ctx *ctx, uint64_t chunk_keys);
 

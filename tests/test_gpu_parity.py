@@ -75,16 +75,36 @@ def test_native_test_keys_histogram(ctx, golden):
     np.testing.assert_array_equal(counts.view(np.uint32), golden["native_counts"])
 
 
+@pytest.mark.parametrize("frontend", [0, 1])
 @pytest.mark.parametrize("mode", [0, 2])
-def test_k13_histogram_golden(ctx, golden, mode):
+def test_k13_histogram_golden(ctx, golden, mode, frontend):
     keys = O.gen_keys13(0, 1_000_000)
     m = O.num_buckets(1_000_000)
     ctx.set_histogram_mode(mode)
+    ctx.set_frontend(frontend)
     try:
         counts = ctx.histogram_fixed(dev(keys), 13, m).cpu().numpy().view(np.uint32)
+        sig = u64(ctx.hash_fixed(dev(keys[: 13 * 8192]), 13))
     finally:
         ctx.set_histogram_mode(0)
+        ctx.set_frontend(0)
     np.testing.assert_array_equal(counts, golden["k13_counts"])
+    np.testing.assert_array_equal(sig, golden["k13_sig"])
+
+
+@pytest.mark.parametrize("frontend", [0, 1])
+def test_k13_ragged_tail(ctx, frontend):
+    # last tile bounds-checked: the key buffer ends exactly at 13*n bytes
+    ctx.set_frontend(frontend)
+    try:
+        for n in (1, 2, 3, 8191, 8192, 8193, 16385, 24575):
+            keys = O.gen_keys13(9, n)
+            np.testing.assert_array_equal(u64(ctx.hash_fixed(dev(keys), 13)), O.hash_fixed(keys, 13))
+            m = 977
+            np.testing.assert_array_equal(ctx.histogram_fixed(dev(keys), 13, m).cpu().numpy().view(np.uint32),
+                                          O.histogram_fixed(keys, 13, m))
+    finally:
+        ctx.set_frontend(0)
 
 
 def test_device_key_generator(ctx, golden):

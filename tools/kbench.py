@@ -33,6 +33,7 @@ def main():
     ap.add_argument("--m", type=int, default=0, help="buckets (default n/1500+1)")
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--chunks", type=str, default="0")
+    ap.add_argument("--frontends", type=str, default="0")
     args = ap.parse_args()
     n = args.n
     m = args.m or n // 1500 + 1
@@ -42,26 +43,29 @@ def main():
     res = {"n": n, "m": m}
     sig_n = min(n, 2_000_000_000)
     sig = torch.empty((sig_n, 2), dtype=torch.int64, device="cuda")
-    ms = timed(lambda: ctx.hash_fixed(keys[: 13 * sig_n], 13, out=sig), args.reps)
-    res["hash_sig_ms"] = ms * n / sig_n
-    res["hash_sig_Gkeys"] = sig_n / ms / 1e6
+    for fe in [int(f) for f in args.frontends.split(",")]:
+        ctx.set_frontend(fe)
+        ms = timed(lambda: ctx.hash_fixed(keys[: 13 * sig_n], 13, out=sig), args.reps)
+        res[f"hash_sig_fe{fe}_Gkeys"] = sig_n / ms / 1e6
+    ctx.set_frontend(0)
     del sig
     ctx.set_histogram_mode(2)
     ms = timed(lambda: ctx.histogram_fixed(keys, 13, m, counts=counts, n=n), args.reps)
     res["atomic_ms"] = ms
     res["atomic_Gkeys"] = n / ms / 1e6
     ctx.set_histogram_mode(0)
-    for ch in [int(x) for x in args.chunks.split(",")]:
+    for fe, ch in [(int(f), int(x)) for f in args.frontends.split(",") for x in args.chunks.split(",")]:
         ctx.set_chunk_keys(ch)
+        ctx.set_frontend(fe)
         ms = timed(lambda: ctx.histogram_fixed(keys, 13, m, counts=counts, n=n), 1)
         ctx.set_profiling(True)
         ms = timed(lambda: ctx.histogram_fixed(keys, 13, m, counts=counts, n=n), args.reps)
         ctx.set_profiling(False)
         p1 = ctx.profile_read(0)
         p2 = ctx.profile_read(1)
-        res[f"part_chunk{ch}"] = {"ms": ms, "Gkeys": n / ms / 1e6,
-                                  "pass1_ms": p1[0] / (args.reps + 0), "pass2_ms": p2[0] / args.reps,
-                                  "launches_per_call": p1[1] / args.reps}
+        res[f"part_fe{fe}_chunk{ch}"] = {"ms": ms, "Gkeys": n / ms / 1e6,
+                                  "pass1_ms": p1[0] / (args.reps + 1), "pass2_ms": p2[0] / (args.reps + 1),
+                                  "launches_per_call": p1[1] / (args.reps + 1)}
     print(json.dumps(res))
 
 
