@@ -24,7 +24,8 @@ struct bsdb_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     int hist_mode = 0;
-    int frontend = 0;  // 13-byte keys: 0 auto (direct), 1 LDS-staged, 2 direct
+    int frontend = 0;  // 13-byte keys: 0 auto (pipelined), 1 LDS-staged, 2 direct per-tile
+    int num_cus = 256;
     uint64_t chunk_keys = 0;
     std::mutex mu;
     // workspace
@@ -185,7 +186,26 @@ int histogram_impl(bsdb_ctx *c, const uint8_t *keys, const uint64_t *offsets, ui
         HIP_OK(hipMemsetAsync(c->overflow, 0, sizeof(uint32_t), s));
         {
             ProfScope ps(c, s, 0, nk);
-            launch_pass1<EPI_PARTITION>(ac, var, key_len, (nk + P1_TILE - 1) / P1_TILE, s, c->frontend);
+            const uint64_t tiles = (nk + P1_TILE - 1) / P1_TILE;
+            if (!var && key_len == 13 && c->frontend == 0) {
+                // full tiles whose 16-byte windows stay inside the chunk go to the
+                // pipelined kernel; the rest (at most one or two) bounds-checked
+                uint64_t nfast = 0;
+                if (ac.blob_bytes >= 3) nfast = std::min(tiles, ((ac.blob_bytes - 3) / 13) / P1_TILE);
+                if (nfast) {
+                    const uint64_t grid = std::min<uint64_t>(nfast, (uint64_t)c->num_cus * 2);
+                    k_pass1_d13<<<(uint32_t)grid, P1_THREADS, 0, s>>>(ac, nfast);
+                }
+                if (nfast < tiles) {
+                    P1Args at = ac;
+                    at.keys = ac.keys + nfast * P1_TILE * 13;
+                    at.n = nk - nfast * P1_TILE;
+                    at.blob_bytes = at.n * 13;
+                    k_pass1<SRC_DIRECT13, EPI_PARTITION, 4, 13><<<(uint32_t)(tiles - nfast), P1_THREADS, 0, s>>>(at);
+                }
+            } else {
+                launch_pass1<EPI_PARTITION>(ac, var, key_len, tiles, s, c->frontend);
+            }
         }
         {
             ProfScope ps(c, s, 1, nk);
@@ -248,6 +268,9 @@ int bsdb_open(int device, bsdb_ctx **out) {
     bsdb_ctx *c = new (std::nothrow) bsdb_ctx();
     if (!c) return BSDB_ENOMEM;
     c->device = device;
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0)
+        c->num_cus = cus;
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
         delete c;
         return BSDB_EIO;

@@ -326,6 +326,112 @@ __global__ __launch_bounds__(P1_THREADS, 4) void k_pass1(P1Args a) {
     if (ovf) atomicOr(a.overflow, 1u);
 }
 
+// Pass 1, 13-byte keys, persistent and software-pipelined (the headline
+// kernel).  Each workgroup walks tiles t = blockIdx.x, blockIdx.x + gridDim.x,
+// ...; a thread owns keys tid + 512*j (j < 16) of a tile, split in two halves
+// of 8 whose 16-byte windows live in register sets X and Y.  While one quarter
+// of tile t hashes, the next is in flight; the next tile's first quarters are
+// issued as soon as a set is consumed, so HBM reads continue through the hashing and through the
+// tile epilogue (counting sort by partition, cursor reservation, run-wise
+// write-out).  Bucket ids stay in registers; LDS holds only the sorted tile.
+// (Two sets of 8 windows spilled at 4 waves/SIMD; quarters of 4 keys in two
+// alternating sets of 4 windows fit the 128-VGPR budget.)
+constexpr int D13_Q = 4;                          // keys per quarter
+constexpr int D13_NQ = P1_KEYS_PER_THREAD / D13_Q;  // quarters per tile
+
+__global__ __launch_bounds__(P1_THREADS, 4) void k_pass1_d13(P1Args a, uint64_t ntiles) {
+    __shared__ uint32_t sorted[P1_TILE];
+    __shared__ uint32_t hist[MAX_PARTS], start[MAX_PARTS], run[MAX_PARTS], base[MAX_PARTS];
+    __shared__ uint32_t wsum[P1_THREADS / 64];
+    const int tid = threadIdx.x;
+    const uint32_t P = a.nparts;
+    const uint32_t mult = (uint32_t)a.multiplier;
+    const W64 seedw = w64(a.seed);
+    const uint64_t G = gridDim.x;
+    for (int i = tid; i < MAX_PARTS; i += P1_THREADS) hist[i] = 0;
+
+    uint64_t t = blockIdx.x;
+    if (t >= ntiles) return;
+    // every tile here is full and readable 3 bytes past its last key: the host
+    // sends the ragged last tile to k_pass1<SRC_DIRECT13> (bounds-checked)
+    // two register sets of D13_Q windows, alternating over the quarters
+    u32x4a X[D13_Q], Y[D13_Q];
+    auto load_q = [&](u32x4a(&R)[D13_Q], uint64_t tt, int q) {
+        if (tt < ntiles) {
+#pragma unroll
+            for (int j = 0; j < D13_Q; ++j) {
+                const uint64_t byte = (tt * P1_TILE + tid + (q * D13_Q + j) * P1_THREADS) * 13;
+                R[j] = __builtin_nontemporal_load(reinterpret_cast<const u32x4a *>(a.keys + (byte & ~3ULL)));
+            }
+        }
+    };
+    load_q(X, t, 0);
+    load_q(Y, t, 1);
+    __syncthreads();  // hist zeroed
+
+    for (; t < ntiles; t += G) {
+        const uint32_t tile_n = P1_TILE;
+        uint32_t bk[P1_KEYS_PER_THREAD];
+        auto hash_q = [&](const u32x4a(&R)[D13_Q], int q) {
+#pragma unroll
+            for (int j = 0; j < D13_Q; ++j) {
+                const uint32_t kt = tid + (q * D13_Q + j) * P1_THREADS;
+                const uint32_t sh = ((kt * 13u) & 3u) * 8u;  // tile0*13 is a multiple of 4
+                W64 s0, s1;
+                spooky13_w(R[j].x, R[j].y, R[j].z, R[j].w, sh, seedw, s0, s1);
+                const uint32_t b = bucket_of_w(s0, mult);
+                bk[q * D13_Q + j] = b;
+                atomicAdd(&hist[b >> PART_SHIFT], 1u);
+            }
+        };
+        hash_q(X, 0);
+        load_q(X, t, 2);
+        hash_q(Y, 1);
+        load_q(Y, t, 3);
+        hash_q(X, 2);
+        load_q(X, t + G, 0);
+        hash_q(Y, 3);
+        load_q(Y, t + G, 1);
+        __syncthreads();  // all hist adds of this tile done
+        const int copy = (int)(t & (NCOPY - 1));
+        const uint32_t cnt = tid < (int)P ? hist[tid] : 0;
+        uint32_t total;
+        const uint32_t excl = block_excl_scan(cnt, wsum, tid, total);
+        uint32_t my_base = 0;
+        if (tid < (int)P) {
+            start[tid] = excl;
+            run[tid] = excl;
+            hist[tid] = 0;  // ready for the next tile
+            // reservation latency overlaps the LDS scatter below
+            if (cnt) my_base = atomicAdd(a.cursor + copy * P + tid, cnt);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < P1_KEYS_PER_THREAD; ++j) {
+            const uint32_t kt = tid + j * P1_THREADS;
+            if (kt < tile_n) {
+                const uint32_t b = bk[j];
+                sorted[atomicAdd(&run[b >> PART_SHIFT], 1u)] = b;
+            }
+        }
+        if (tid < (int)P) base[tid] = my_base;
+        __syncthreads();
+        bool ovf = false;
+        for (uint32_t j = tid; j < tile_n; j += P1_THREADS) {
+            const uint32_t b = sorted[j];
+            const uint32_t p = b >> PART_SHIFT;
+            const uint64_t idx = (uint64_t)base[p] + (j - start[p]);
+            if (idx < a.cap) {
+                a.ids[((uint64_t)p * NCOPY + copy) * a.cap + idx] = (uint16_t)(b & (PART_BUCKETS - 1));
+            } else {
+                ovf = true;
+            }
+        }
+        if (ovf) atomicOr(a.overflow, 1u);
+        __syncthreads();  // sorted / start / base reused by the next tile
+    }
+}
+
 // Pass 2: LDS histogram of one slice of one (partition, copy) region.
 __global__ __launch_bounds__(P2_THREADS, 4) void k_pass2(const uint16_t *ids, const uint32_t *cursor,
                                                          const uint32_t *overflow, uint64_t cap,

@@ -75,7 +75,7 @@ def test_native_test_keys_histogram(ctx, golden):
     np.testing.assert_array_equal(counts.view(np.uint32), golden["native_counts"])
 
 
-@pytest.mark.parametrize("frontend", [0, 1])
+@pytest.mark.parametrize("frontend", [0, 1, 2])
 @pytest.mark.parametrize("mode", [0, 2])
 def test_k13_histogram_golden(ctx, golden, mode, frontend):
     keys = O.gen_keys13(0, 1_000_000)
@@ -92,7 +92,7 @@ def test_k13_histogram_golden(ctx, golden, mode, frontend):
     np.testing.assert_array_equal(sig, golden["k13_sig"])
 
 
-@pytest.mark.parametrize("frontend", [0, 1])
+@pytest.mark.parametrize("frontend", [0, 1, 2])
 def test_k13_ragged_tail(ctx, frontend):
     # last tile bounds-checked: the key buffer ends exactly at 13*n bytes
     ctx.set_frontend(frontend)
