@@ -26,12 +26,14 @@ struct bsdb_ctx {
     int hist_mode = 0;
     int frontend = 0;  // 13-byte keys: 0 auto (pipelined), 1 LDS-staged, 2 direct per-tile
     int num_cus = 256;
+    int d13_variant = 0;  // profiling only (BSDB_D13_VARIANT): results are NOT valid when != 0
     uint64_t chunk_keys = 0;
     std::mutex mu;
     // workspace
     void *ids = nullptr;
     size_t ids_bytes = 0;
-    uint32_t *cursor = nullptr;   // NCOPY * MAX_PARTS
+    uint32_t *cursor = nullptr;   // region fills [nregions][P]
+    size_t cursor_bytes = 0;
     uint32_t *overflow = nullptr; // 1 word
     uint64_t *scan_part = nullptr;
     size_t scan_part_n = 0;
@@ -115,28 +117,48 @@ void launch_pass1(const P1Args &a, bool var, uint32_t key_len, uint64_t tiles, h
 
 struct PartPlan {
     uint32_t nparts;
-    uint64_t cap;    // ids per (partition, copy) region, multiple of 8
-    uint32_t slice;  // ids per pass-2 workgroup, multiple of 8
-    uint32_t slices;
+    uint32_t nregions;  // regions per partition in the id buffer
+    uint32_t region0;   // first shared (atomic-cursor) region
+    uint32_t grid_d13;  // persistent workgroups of the 13-byte kernel (0 = generic path)
+    uint64_t cap;       // ids per (partition, region), multiple of 8
+    uint32_t rpw;       // pass 2: regions per workgroup
+    uint32_t nslices;   // pass 2: slices per region
+    uint32_t slice;     // pass 2: ids per slice, multiple of 8
 };
 
-// Region capacity: the expected share of a full partition per copy plus
-// 8 sigma and one tile of slack (tiles go round-robin over the copies).
-PartPlan plan_partitions(uint64_t chunk, uint64_t m) {
+uint64_t round8(double x) { return ((uint64_t)x + 7) & ~7ULL; }
+
+// Region capacities: expected share of a full partition plus 8 sigma and
+// slack (a fill beyond cap raises the overflow flag: the chunk is recounted).
+PartPlan plan_partitions(const bsdb_ctx *c, uint64_t chunk, uint64_t m, bool d13) {
     PartPlan p{};
     p.nparts = (uint32_t)((m + PART_BUCKETS - 1) / PART_BUCKETS);
     const double frac = std::min(1.0, (double)PART_BUCKETS / (double)m);
-    const double e = (double)chunk * frac / NCOPY;
-    uint64_t cap = (uint64_t)(e * 1.02 + 8.0 * std::sqrt(e) + 2 * P1_TILE + 64);
-    cap = (cap + 7) & ~7ULL;
-    p.cap = cap;
-    // pass-2 workgroups: at least ~1024 in flight, each >= 64 Ki ids
-    const uint64_t regions = (uint64_t)p.nparts * NCOPY;
-    uint64_t slice = std::max<uint64_t>(65536, (uint64_t)std::ceil(e * regions / 1024.0));
-    slice = std::min<uint64_t>(slice, cap);
-    slice = (slice + 7) & ~7ULL;
-    p.slice = (uint32_t)slice;
-    p.slices = (uint32_t)((cap + slice - 1) / slice);
+    const uint64_t tiles = (chunk + P1_TILE - 1) / P1_TILE;
+    if (d13) {
+        // one private region per persistent workgroup + NCOPY shared regions
+        // for the bounds-checked tail tiles
+        p.grid_d13 = (uint32_t)std::min<uint64_t>(tiles, (uint64_t)c->num_cus * 2);
+        const uint64_t tw = (tiles + p.grid_d13 - 1) / p.grid_d13;
+        const double e = (double)tw * P1_TILE * frac;
+        p.cap = std::max<uint64_t>(P1_TILE + 64, round8(e * 1.02 + 8.0 * std::sqrt(e) + 64));
+        p.region0 = p.grid_d13;
+        p.nregions = p.grid_d13 + NCOPY;
+        const uint32_t groups = std::max<uint32_t>(1, std::min<uint32_t>(p.nregions, 2048 / p.nparts));
+        p.rpw = (p.nregions + groups - 1) / groups;
+        p.nslices = 1;
+        p.slice = (uint32_t)p.cap;
+    } else {
+        const double e = (double)chunk * frac / NCOPY;
+        p.cap = round8(e * 1.02 + 8.0 * std::sqrt(e) + 2 * P1_TILE + 64);
+        p.region0 = 0;
+        p.nregions = NCOPY;
+        p.rpw = 1;
+        uint64_t slice = std::max<uint64_t>(65536, (uint64_t)std::ceil(e * p.nparts * NCOPY / 1024.0));
+        slice = std::min<uint64_t>(round8((double)slice), p.cap);
+        p.slice = (uint32_t)slice;
+        p.nslices = (uint32_t)((p.cap + slice - 1) / slice);
+    }
     return p;
 }
 
@@ -164,14 +186,19 @@ int histogram_impl(bsdb_ctx *c, const uint8_t *keys, const uint64_t *offsets, ui
     uint64_t chunk = c->chunk_keys ? c->chunk_keys : DEFAULT_CHUNK_KEYS;
     chunk = std::max<uint64_t>(P1_TILE, chunk / P1_TILE * P1_TILE);
     chunk = std::min<uint64_t>(chunk, (n + P1_TILE - 1) / P1_TILE * P1_TILE);
-    const PartPlan pp = plan_partitions(chunk, m);
-    int rc = grow(&c->ids, &c->ids_bytes, (size_t)pp.nparts * NCOPY * pp.cap * sizeof(uint16_t));
+    const bool d13 = !var && key_len == 13 && c->frontend == 0;
+    const PartPlan pp = plan_partitions(c, chunk, m, d13);
+    int rc = grow(&c->ids, &c->ids_bytes, (size_t)pp.nparts * pp.nregions * pp.cap * sizeof(uint16_t));
+    if (rc) return rc;
+    rc = grow((void **)&c->cursor, &c->cursor_bytes, (size_t)pp.nparts * pp.nregions * sizeof(uint32_t));
     if (rc) return rc;
     a.ids = (uint16_t *)c->ids;
     a.cursor = c->cursor;
     a.overflow = c->overflow;
     a.cap = pp.cap;
     a.nparts = pp.nparts;
+    a.nregions = pp.nregions;
+    a.region0 = pp.region0;
     for (uint64_t k0 = 0; k0 < n; k0 += chunk) {
         const uint64_t nk = std::min(chunk, n - k0);
         P1Args ac = a;
@@ -182,19 +209,25 @@ int histogram_impl(bsdb_ctx *c, const uint8_t *keys, const uint64_t *offsets, ui
             ac.keys = keys + k0 * key_len;
             ac.blob_bytes = nk * key_len;
         }
-        HIP_OK(hipMemsetAsync(c->cursor, 0, sizeof(uint32_t) * NCOPY * pp.nparts, s));
+        HIP_OK(hipMemsetAsync(c->cursor, 0, sizeof(uint32_t) * pp.nregions * pp.nparts, s));
         HIP_OK(hipMemsetAsync(c->overflow, 0, sizeof(uint32_t), s));
         {
             ProfScope ps(c, s, 0, nk);
             const uint64_t tiles = (nk + P1_TILE - 1) / P1_TILE;
-            if (!var && key_len == 13 && c->frontend == 0) {
+            if (d13) {
                 // full tiles whose 16-byte windows stay inside the chunk go to the
-                // pipelined kernel; the rest (at most one or two) bounds-checked
+                // pipelined kernel (private regions); the rest (at most two) to the
+                // bounds-checked kernel (shared regions region0..region0+7)
                 uint64_t nfast = 0;
                 if (ac.blob_bytes >= 3) nfast = std::min(tiles, ((ac.blob_bytes - 3) / 13) / P1_TILE);
                 if (nfast) {
-                    const uint64_t grid = std::min<uint64_t>(nfast, (uint64_t)c->num_cus * 2);
-                    k_pass1_d13<<<(uint32_t)grid, P1_THREADS, 0, s>>>(ac, nfast);
+                    const uint64_t grid = std::min<uint64_t>(nfast, pp.grid_d13);
+                    if (c->d13_variant == 1)
+                        k_pass1_d13<1><<<(uint32_t)grid, P1_THREADS, 0, s>>>(ac, nfast);
+                    else if (c->d13_variant == 2)
+                        k_pass1_d13<2><<<(uint32_t)grid, P1_THREADS, 0, s>>>(ac, nfast);
+                    else
+                        k_pass1_d13<0><<<(uint32_t)grid, P1_THREADS, 0, s>>>(ac, nfast);
                 }
                 if (nfast < tiles) {
                     P1Args at = ac;
@@ -209,8 +242,10 @@ int histogram_impl(bsdb_ctx *c, const uint8_t *keys, const uint64_t *offsets, ui
         }
         {
             ProfScope ps(c, s, 1, nk);
-            k_pass2<<<dim3(pp.slices, pp.nparts * NCOPY), P2_THREADS, 0, s>>>(
-                (const uint16_t *)c->ids, c->cursor, c->overflow, pp.cap, pp.nparts, pp.slice, m, counts);
+            const uint32_t groups = (pp.nregions + pp.rpw - 1) / pp.rpw;
+            k_pass2<<<dim3(groups * pp.nslices, pp.nparts), P2_THREADS, 0, s>>>(
+                (const uint16_t *)c->ids, c->cursor, c->overflow, pp.cap, pp.nparts, pp.nregions, pp.rpw,
+                pp.nslices, pp.slice, m, counts);
         }
         if (var) {
             k_overflow_fallback<SRC_VAR, 0><<<1024, P1_THREADS, 0, s>>>(ac);
@@ -268,6 +303,7 @@ int bsdb_open(int device, bsdb_ctx **out) {
     bsdb_ctx *c = new (std::nothrow) bsdb_ctx();
     if (!c) return BSDB_ENOMEM;
     c->device = device;
+    if (const char *v = std::getenv("BSDB_D13_VARIANT")) c->d13_variant = std::atoi(v);
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0)
         c->num_cus = cus;
@@ -275,8 +311,7 @@ int bsdb_open(int device, bsdb_ctx **out) {
         delete c;
         return BSDB_EIO;
     }
-    if (hipMalloc(&c->cursor, sizeof(uint32_t) * NCOPY * MAX_PARTS) != hipSuccess ||
-        hipMalloc(&c->overflow, sizeof(uint32_t) * 4) != hipSuccess) {
+    if (hipMalloc(&c->overflow, sizeof(uint32_t) * 4) != hipSuccess) {
         bsdb_close(c);
         return BSDB_ENOMEM;
     }

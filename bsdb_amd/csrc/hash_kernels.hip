@@ -42,11 +42,13 @@ struct P1Args {
     uint64_t seed;
     uint64_t multiplier;      // 2 * num_buckets
     // EPI_PARTITION
-    uint16_t *ids;            // [P][NCOPY][cap]
-    uint32_t *cursor;         // [NCOPY][P]
+    uint16_t *ids;            // [P][nregions][cap]
+    uint32_t *cursor;         // [nregions][P] fill of each region
     uint32_t *overflow;       // set when a region would overflow
-    uint64_t cap;             // capacity of one (partition, copy) region, multiple of 8
+    uint64_t cap;             // capacity of one (partition, region) slot, multiple of 8
     uint32_t nparts;
+    uint32_t nregions;        // regions per partition in the id buffer
+    uint32_t region0;         // first region used by k_pass1's NCOPY shared regions
     // EPI_ATOMIC
     uint32_t *counts;
     // EPI_SIG
@@ -297,7 +299,7 @@ __global__ __launch_bounds__(P1_THREADS, 4) void k_pass1(P1Args a) {
     // ---- counting sort of the tile by partition, then run-wise write-out ----
     __syncthreads();
     const uint32_t P = a.nparts;
-    const int copy = blockIdx.x & (NCOPY - 1);
+    const uint32_t copy = a.region0 + (blockIdx.x & (NCOPY - 1));
     uint32_t cnt = tid < (int)P ? hist[tid] : 0, total;
     const uint32_t excl = block_excl_scan(cnt, wsum, tid, total);
     if (tid < (int)P) {
@@ -318,7 +320,7 @@ __global__ __launch_bounds__(P1_THREADS, 4) void k_pass1(P1Args a) {
         const uint32_t p = b >> PART_SHIFT;
         const uint64_t idx = (uint64_t)base[p] + (j - start[p]);
         if (idx < a.cap) {
-            a.ids[((uint64_t)p * NCOPY + copy) * a.cap + idx] = (uint16_t)(b & (PART_BUCKETS - 1));
+            a.ids[((uint64_t)p * a.nregions + copy) * a.cap + idx] = (uint16_t)(b & (PART_BUCKETS - 1));
         } else {
             ovf = true;
         }
@@ -339,19 +341,28 @@ __global__ __launch_bounds__(P1_THREADS, 4) void k_pass1(P1Args a) {
 constexpr int D13_Q = 4;                          // keys per quarter
 constexpr int D13_NQ = P1_KEYS_PER_THREAD / D13_Q;  // quarters per tile
 
+// VARIANT (profiling builds only; 0 in production): 1 = skip the tile
+// epilogue, 2 = also skip the LDS partition counts (pure load + hash + bucket).
+template <int VARIANT>
 __global__ __launch_bounds__(P1_THREADS, 4) void k_pass1_d13(P1Args a, uint64_t ntiles) {
     __shared__ uint32_t sorted[P1_TILE];
-    __shared__ uint32_t hist[MAX_PARTS], start[MAX_PARTS], run[MAX_PARTS], base[MAX_PARTS];
+    __shared__ uint32_t hist[MAX_PARTS], start[MAX_PARTS], run[MAX_PARTS], base[MAX_PARTS], cur[MAX_PARTS];
     __shared__ uint32_t wsum[P1_THREADS / 64];
     const int tid = threadIdx.x;
     const uint32_t P = a.nparts;
     const uint32_t mult = (uint32_t)a.multiplier;
     const W64 seedw = w64(a.seed);
     const uint64_t G = gridDim.x;
-    for (int i = tid; i < MAX_PARTS; i += P1_THREADS) hist[i] = 0;
+    for (int i = tid; i < MAX_PARTS; i += P1_THREADS) {
+        hist[i] = 0;
+        cur[i] = 0;
+    }
 
     uint64_t t = blockIdx.x;
-    if (t >= ntiles) return;
+    if (t >= ntiles) {
+        for (int i = tid; i < (int)P; i += P1_THREADS) a.cursor[(uint64_t)blockIdx.x * P + i] = 0;
+        return;
+    }
     // every tile here is full and readable 3 bytes past its last key: the host
     // sends the ragged last tile to k_pass1<SRC_DIRECT13> (bounds-checked)
     // two register sets of D13_Q windows, alternating over the quarters
@@ -381,7 +392,7 @@ __global__ __launch_bounds__(P1_THREADS, 4) void k_pass1_d13(P1Args a, uint64_t 
                 spooky13_w(R[j].x, R[j].y, R[j].z, R[j].w, sh, seedw, s0, s1);
                 const uint32_t b = bucket_of_w(s0, mult);
                 bk[q * D13_Q + j] = b;
-                atomicAdd(&hist[b >> PART_SHIFT], 1u);
+                if (VARIANT < 2) atomicAdd(&hist[b >> PART_SHIFT], 1u);
             }
         };
         hash_q(X, 0);
@@ -392,37 +403,40 @@ __global__ __launch_bounds__(P1_THREADS, 4) void k_pass1_d13(P1Args a, uint64_t 
         load_q(X, t + G, 0);
         hash_q(Y, 3);
         load_q(Y, t + G, 1);
+        if (VARIANT) {
+            uint32_t x = 0;
+#pragma unroll
+            for (int j = 0; j < P1_KEYS_PER_THREAD; ++j) x ^= bk[j];
+            if (x == 0xFFFFFFFFu) a.overflow[1] = x;  // keep the hashes live
+            continue;
+        }
         __syncthreads();  // all hist adds of this tile done
-        const int copy = (int)(t & (NCOPY - 1));
         const uint32_t cnt = tid < (int)P ? hist[tid] : 0;
         uint32_t total;
         const uint32_t excl = block_excl_scan(cnt, wsum, tid, total);
-        uint32_t my_base = 0;
         if (tid < (int)P) {
             start[tid] = excl;
             run[tid] = excl;
-            hist[tid] = 0;  // ready for the next tile
-            // reservation latency overlaps the LDS scatter below
-            if (cnt) my_base = atomicAdd(a.cursor + copy * P + tid, cnt);
+            hist[tid] = 0;            // ready for the next tile
+            base[tid] = cur[tid];     // this workgroup's private region: no global atomics
+            cur[tid] += cnt;
         }
         __syncthreads();
 #pragma unroll
         for (int j = 0; j < P1_KEYS_PER_THREAD; ++j) {
-            const uint32_t kt = tid + j * P1_THREADS;
-            if (kt < tile_n) {
-                const uint32_t b = bk[j];
-                sorted[atomicAdd(&run[b >> PART_SHIFT], 1u)] = b;
-            }
+            const uint32_t b = bk[j];
+            sorted[atomicAdd(&run[b >> PART_SHIFT], 1u)] = b;
         }
-        if (tid < (int)P) base[tid] = my_base;
         __syncthreads();
         bool ovf = false;
+        uint16_t *region = a.ids + (uint64_t)blockIdx.x * a.cap;
+        const uint64_t pstride = (uint64_t)a.nregions * a.cap;
         for (uint32_t j = tid; j < tile_n; j += P1_THREADS) {
             const uint32_t b = sorted[j];
             const uint32_t p = b >> PART_SHIFT;
             const uint64_t idx = (uint64_t)base[p] + (j - start[p]);
             if (idx < a.cap) {
-                a.ids[((uint64_t)p * NCOPY + copy) * a.cap + idx] = (uint16_t)(b & (PART_BUCKETS - 1));
+                region[p * pstride + idx] = (uint16_t)(b & (PART_BUCKETS - 1));
             } else {
                 ovf = true;
             }
@@ -430,35 +444,49 @@ __global__ __launch_bounds__(P1_THREADS, 4) void k_pass1_d13(P1Args a, uint64_t 
         if (ovf) atomicOr(a.overflow, 1u);
         __syncthreads();  // sorted / start / base reused by the next tile
     }
+    // publish this workgroup's region fills for pass 2 (plain stores; the
+    // kernel boundary orders them before pass 2 reads)
+    if (VARIANT == 0)
+        for (int i = tid; i < (int)P; i += P1_THREADS) a.cursor[(uint64_t)blockIdx.x * P + i] = cur[i];
 }
 
-// Pass 2: LDS histogram of one slice of one (partition, copy) region.
+// Pass 2: LDS histogram of partition p = blockIdx.y over a group of regions
+// (x / nslices) and one slice of each region (x % nslices), then one coalesced
+// atomic flush of the 32768-bucket table into counts.
 __global__ __launch_bounds__(P2_THREADS, 4) void k_pass2(const uint16_t *ids, const uint32_t *cursor,
                                                          const uint32_t *overflow, uint64_t cap,
-                                                         uint32_t nparts, uint32_t slice,
+                                                         uint32_t nparts, uint32_t nregions, uint32_t rpw,
+                                                         uint32_t nslices, uint32_t slice,
                                                          uint64_t num_buckets, uint32_t *counts) {
     __shared__ uint32_t hist[PART_BUCKETS];
     if (*overflow) return;
     const int tid = threadIdx.x;
-    const uint32_t p = blockIdx.y / NCOPY, c = blockIdx.y % NCOPY;
-    const uint64_t cnt = min((uint64_t)cursor[c * nparts + p], cap);
-    const uint64_t lo = (uint64_t)blockIdx.x * slice;
-    if (lo >= cnt) return;
-    const uint64_t hi = min(cnt, lo + slice);
+    const uint32_t p = blockIdx.y;
+    const uint32_t grp = blockIdx.x / nslices, sl = blockIdx.x % nslices;
+    const uint32_t r0 = grp * rpw, r1 = min(nregions, r0 + rpw);
+    const uint64_t lo = (uint64_t)sl * slice;
+    bool any = false;
+    for (uint32_t r = r0; r < r1; ++r) any |= min((uint64_t)cursor[(uint64_t)r * nparts + p], cap) > lo;
+    if (!any) return;
     for (int i = tid; i < PART_BUCKETS; i += P2_THREADS) hist[i] = 0;
     __syncthreads();
-    const uint16_t *src = ids + ((uint64_t)p * NCOPY + c) * cap;
-    // lo is a multiple of 8 (slice % 8 == 0, cap % 8 == 0): 16-B aligned vectors
-    const uint64_t nvec = (hi - lo) >> 3;
-    const uint4 *v = reinterpret_cast<const uint4 *>(src + lo);
-    for (uint64_t i = tid; i < nvec; i += P2_THREADS) {
-        const uint4 w = ntload16(v + i);
-        atomicAdd(&hist[w.x & 0xFFFF], 1u); atomicAdd(&hist[w.x >> 16], 1u);
-        atomicAdd(&hist[w.y & 0xFFFF], 1u); atomicAdd(&hist[w.y >> 16], 1u);
-        atomicAdd(&hist[w.z & 0xFFFF], 1u); atomicAdd(&hist[w.z >> 16], 1u);
-        atomicAdd(&hist[w.w & 0xFFFF], 1u); atomicAdd(&hist[w.w >> 16], 1u);
+    for (uint32_t r = r0; r < r1; ++r) {
+        const uint64_t fill = min((uint64_t)cursor[(uint64_t)r * nparts + p], cap);
+        if (fill <= lo) continue;
+        const uint64_t hi = min(fill, lo + slice);
+        const uint16_t *src = ids + ((uint64_t)p * nregions + r) * cap;
+        // lo and cap are multiples of 8: 16-B aligned vectors
+        const uint64_t nvec = (hi - lo) >> 3;
+        const uint4 *v = reinterpret_cast<const uint4 *>(src + lo);
+        for (uint64_t i = tid; i < nvec; i += P2_THREADS) {
+            const uint4 w = ntload16(v + i);
+            atomicAdd(&hist[w.x & 0xFFFF], 1u); atomicAdd(&hist[w.x >> 16], 1u);
+            atomicAdd(&hist[w.y & 0xFFFF], 1u); atomicAdd(&hist[w.y >> 16], 1u);
+            atomicAdd(&hist[w.z & 0xFFFF], 1u); atomicAdd(&hist[w.z >> 16], 1u);
+            atomicAdd(&hist[w.w & 0xFFFF], 1u); atomicAdd(&hist[w.w >> 16], 1u);
+        }
+        for (uint64_t i = lo + nvec * 8 + tid; i < hi; i += P2_THREADS) atomicAdd(&hist[src[i]], 1u);
     }
-    for (uint64_t i = lo + nvec * 8 + tid; i < hi; i += P2_THREADS) atomicAdd(&hist[src[i]], 1u);
     __syncthreads();
     const uint64_t b0 = (uint64_t)p << PART_SHIFT;
     const uint32_t nb = (uint32_t)min((uint64_t)PART_BUCKETS, num_buckets - b0);
