@@ -346,10 +346,14 @@ constexpr int D13_NQ = P1_KEYS_PER_THREAD / D13_Q;  // quarters per tile
 template <int VARIANT>
 __global__ __launch_bounds__(P1_THREADS, 4) void k_pass1_d13(P1Args a, uint64_t ntiles) {
     __shared__ uint32_t sorted[P1_TILE];
-    __shared__ uint32_t hist[MAX_PARTS], start[MAX_PARTS], run[MAX_PARTS], base[MAX_PARTS], cur[MAX_PARTS];
+    __shared__ uint32_t hist[MAX_PARTS], run[MAX_PARTS], cur[MAX_PARTS];
+    __shared__ uint64_t off64[MAX_PARTS];
     __shared__ uint32_t wsum[P1_THREADS / 64];
+    __shared__ uint32_t tile_ovf;
     const int tid = threadIdx.x;
     const uint32_t P = a.nparts;
+    const uint64_t pstride = (uint64_t)a.nregions * a.cap;
+    if (tid == 0) tile_ovf = 0;
     const uint32_t mult = (uint32_t)a.multiplier;
     const W64 seedw = w64(a.seed);
     const uint64_t G = gridDim.x;
@@ -381,7 +385,6 @@ __global__ __launch_bounds__(P1_THREADS, 4) void k_pass1_d13(P1Args a, uint64_t 
     __syncthreads();  // hist zeroed
 
     for (; t < ntiles; t += G) {
-        const uint32_t tile_n = P1_TILE;
         uint32_t bk[P1_KEYS_PER_THREAD];
         auto hash_q = [&](const u32x4a(&R)[D13_Q], int q) {
 #pragma unroll
@@ -415,34 +418,38 @@ __global__ __launch_bounds__(P1_THREADS, 4) void k_pass1_d13(P1Args a, uint64_t 
         uint32_t total;
         const uint32_t excl = block_excl_scan(cnt, wsum, tid, total);
         if (tid < (int)P) {
-            start[tid] = excl;
             run[tid] = excl;
-            hist[tid] = 0;            // ready for the next tile
-            base[tid] = cur[tid];     // this workgroup's private region: no global atomics
-            cur[tid] += cnt;
+            hist[tid] = 0;  // ready for the next tile
+            // private region of this workgroup: no global atomics.  off64[p] is
+            // the element offset of sorted position 0 for partition p, so the
+            // write-out address of sorted slot j is ids + off64[p] + j.
+            const uint32_t b0 = cur[tid];
+            cur[tid] = b0 + cnt;
+            if ((uint64_t)b0 + cnt > a.cap) tile_ovf = 1;
+            off64[tid] = (uint64_t)tid * pstride + (uint64_t)blockIdx.x * a.cap + b0 - excl;
         }
         __syncthreads();
+        uint32_t pos[P1_KEYS_PER_THREAD];
 #pragma unroll
-        for (int j = 0; j < P1_KEYS_PER_THREAD; ++j) {
-            const uint32_t b = bk[j];
-            sorted[atomicAdd(&run[b >> PART_SHIFT], 1u)] = b;
-        }
+        for (int j = 0; j < P1_KEYS_PER_THREAD; ++j) pos[j] = atomicAdd(&run[bk[j] >> PART_SHIFT], 1u);
+#pragma unroll
+        for (int j = 0; j < P1_KEYS_PER_THREAD; ++j) sorted[pos[j]] = bk[j];
         __syncthreads();
-        bool ovf = false;
-        uint16_t *region = a.ids + (uint64_t)blockIdx.x * a.cap;
-        const uint64_t pstride = (uint64_t)a.nregions * a.cap;
-        for (uint32_t j = tid; j < tile_n; j += P1_THREADS) {
-            const uint32_t b = sorted[j];
-            const uint32_t p = b >> PART_SHIFT;
-            const uint64_t idx = (uint64_t)base[p] + (j - start[p]);
-            if (idx < a.cap) {
-                region[p * pstride + idx] = (uint16_t)(b & (PART_BUCKETS - 1));
-            } else {
-                ovf = true;
-            }
+        if (!tile_ovf) {
+            // batched: 16 sorted reads, 16 offset reads, 16 two-byte stores
+            uint32_t sb[P1_KEYS_PER_THREAD];
+#pragma unroll
+            for (int j = 0; j < P1_KEYS_PER_THREAD; ++j) sb[j] = sorted[tid + j * P1_THREADS];
+            uint64_t so[P1_KEYS_PER_THREAD];
+#pragma unroll
+            for (int j = 0; j < P1_KEYS_PER_THREAD; ++j) so[j] = off64[sb[j] >> PART_SHIFT];
+#pragma unroll
+            for (int j = 0; j < P1_KEYS_PER_THREAD; ++j)
+                a.ids[so[j] + tid + j * P1_THREADS] = (uint16_t)(sb[j] & (PART_BUCKETS - 1));
+        } else if (tid == 0) {
+            atomicOr(a.overflow, 1u);
         }
-        if (ovf) atomicOr(a.overflow, 1u);
-        __syncthreads();  // sorted / start / base reused by the next tile
+        __syncthreads();  // sorted / run / off64 reused by the next tile
     }
     // publish this workgroup's region fills for pass 2 (plain stores; the
     // kernel boundary orders them before pass 2 reads)
