@@ -94,12 +94,18 @@ def main():
     if args.chunk:
         ctx.set_chunk_keys(args.chunk)
 
+    def log(msg):
+        print(f"[bench r{rank}] {time.strftime('%H:%M:%S')} {msg}", file=sys.stderr, flush=True)
+
     n = args.n
     m = n // 1500 + 1
     lo, hi = shard(n, rank, world)
     nloc = hi - lo
+    log(f"allocating {KEY_LEN * nloc / 1e9:.1f} GB of keys ({nloc} keys, m={m})")
     keys = torch.empty(KEY_LEN * nloc + 16, dtype=torch.uint8, device="cuda")
     ctx.gen_keys13(lo, nloc, out=keys)          # synthetic keys written in HBM (untimed)
+    torch.cuda.synchronize()
+    log("keys generated")
     counts = torch.zeros(m, dtype=torch.int32, device="cuda")
     E = torch.empty(m + 1, dtype=torch.int64, device="cuda")
     torch.cuda.synchronize()
@@ -111,7 +117,8 @@ def main():
 
     for _ in range(args.warmup):
         step()
-    torch.cuda.synchronize()
+        torch.cuda.synchronize()
+        log("warmup step done")
     ctx.profile_read(ctx.PASS1); ctx.profile_read(ctx.PASS2); ctx.profile_read(ctx.SCAN)
     ctx.set_profiling(True)
 
@@ -153,9 +160,11 @@ def main():
                     traffic = pj.get("hbm_bytes_per_launch")
             except Exception:
                 traffic = None
+        log(f"timed {args.steps} steps: {dt * 1e3 / args.steps:.2f} ms/step")
         cpu = None
         if not args.no_cpu:
             cpu = cpu_baseline(m, args.cpu_seconds, args.cpu_threads)
+            log("cpu baseline done")
         line = {
             "metric": "index-build keys/s (device-resident), 13B x 13-byte keys; % HBM roofline",
             "value": value,

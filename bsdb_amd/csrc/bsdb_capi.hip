@@ -95,8 +95,31 @@ hipStream_t pick(bsdb_ctx *, void *stream) { return (hipStream_t)stream; }
 int launch_status() { return hipGetLastError() == hipSuccess ? BSDB_OK : BSDB_EIO; }
 
 // ---- pass-1 dispatch over (source layout, epilogue) ------------------------
+// One-tile-per-workgroup launches: tiles * 512 work-items must stay below 2^32
+// (a dispatch packet's grid size is 32-bit), so callers split larger key sets.
+constexpr uint64_t MAX_TILES_PER_LAUNCH = (1ULL << 32) / P1_THREADS - 1;
+
 template <int EPI>
-void launch_pass1(const P1Args &a, bool var, uint32_t key_len, uint64_t tiles, hipStream_t s, int frontend) {
+void launch_pass1(const P1Args &a0, bool var, uint32_t key_len, uint64_t tiles, hipStream_t s, int frontend) {
+    if (tiles > MAX_TILES_PER_LAUNCH) {
+        // split into launches of whole tiles (keys, offsets and outputs shifted)
+        for (uint64_t t0 = 0; t0 < tiles; t0 += MAX_TILES_PER_LAUNCH) {
+            const uint64_t nt = std::min(MAX_TILES_PER_LAUNCH, tiles - t0);
+            P1Args a = a0;
+            const uint64_t k0 = t0 * P1_TILE;
+            a.n = std::min<uint64_t>(a0.n - k0, nt * P1_TILE);
+            if (var) {
+                a.offsets = a0.offsets + k0;
+            } else {
+                a.keys = a0.keys + k0 * key_len;
+                a.blob_bytes = a0.blob_bytes - k0 * key_len;
+            }
+            if (a.sig) a.sig = a0.sig + 2 * k0;
+            launch_pass1<EPI>(a, var, key_len, nt, s, frontend);
+        }
+        return;
+    }
+    const P1Args &a = a0;
     const dim3 g((uint32_t)tiles), b(P1_THREADS);
     if (var) {
         k_pass1<SRC_VAR, EPI, 1, 0><<<g, b, 0, s>>>(a);
@@ -411,7 +434,8 @@ int bsdb_dev_gen_keys13(bsdb_ctx *c, uint64_t first, uint64_t n, uint8_t *d_keys
     std::lock_guard<std::mutex> g(c->mu);
     HIP_OK(hipSetDevice(c->device));
     if (n == 0) return BSDB_OK;
-    k_gen_keys13<<<(uint32_t)((n + 255) / 256), 256, 0, pick(c, stream)>>>(first, n, d_keys);
+    const uint64_t blocks = std::min<uint64_t>((n + 255) / 256, (uint64_t)c->num_cus * 64);
+    k_gen_keys13<<<(uint32_t)blocks, 256, 0, pick(c, stream)>>>(first, n, d_keys);
     return launch_status();
 }
 

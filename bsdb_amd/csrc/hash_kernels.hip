@@ -597,25 +597,31 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan_final(const uint32_t *cou
 }
 
 // ---- synthetic 13-byte keys (bench input) ------------
+// Grid-stride over blocks of 256 keys: a dispatch holds < 2^32 work-items, so
+// a 13 B-key set (the README shape) cannot be one thread per key.
 __global__ __launch_bounds__(256) void k_gen_keys13(uint64_t first, uint64_t n, uint8_t *out) {
     __shared__ __align__(16) uint8_t buf[256 * 13];
-    const uint64_t k0 = (uint64_t)blockIdx.x * 256;
-    const uint64_t k = k0 + threadIdx.x;
-    if (k < n) {
-        const uint64_t i = first + k;
-        const uint64_t w0 = splitmix64(i ^ 0xB5DB0001ULL);
-        const uint64_t w1 = (i ^ (splitmix64(i + 1) >> 24)) & 0xFFFFFFFFFFULL;
-        uint8_t *d = buf + threadIdx.x * 13;
-        for (int b = 0; b < 8; ++b) d[b] = (uint8_t)(w0 >> (8 * b));
-        for (int b = 0; b < 5; ++b) d[8 + b] = (uint8_t)(w1 >> (8 * b));
+    const uint64_t nblk = (n + 255) / 256;
+    for (uint64_t blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
+        const uint64_t k0 = blk * 256;
+        const uint64_t k = k0 + threadIdx.x;
+        __syncthreads();
+        if (k < n) {
+            const uint64_t i = first + k;
+            const uint64_t w0 = splitmix64(i ^ 0xB5DB0001ULL);
+            const uint64_t w1 = (i ^ (splitmix64(i + 1) >> 24)) & 0xFFFFFFFFFFULL;
+            uint8_t *d = buf + threadIdx.x * 13;
+            for (int b = 0; b < 8; ++b) d[b] = (uint8_t)(w0 >> (8 * b));
+            for (int b = 0; b < 5; ++b) d[8 + b] = (uint8_t)(w1 >> (8 * b));
+        }
+        __syncthreads();
+        // k0*13 = blk*3328 is dword aligned: dword stores, byte tail
+        const uint32_t nbytes = (uint32_t)min((uint64_t)256, n - k0) * 13;
+        uint32_t *o32 = reinterpret_cast<uint32_t *>(out + k0 * 13);
+        const uint32_t *b32 = reinterpret_cast<const uint32_t *>(buf);
+        for (uint32_t w = threadIdx.x; w < nbytes / 4; w += 256) o32[w] = b32[w];
+        for (uint32_t b = (nbytes & ~3u) + threadIdx.x; b < nbytes; b += 256) out[k0 * 13 + b] = buf[b];
     }
-    __syncthreads();
-    // k0*13 = blockIdx*3328 is dword aligned: dword stores, byte tail
-    const uint32_t nbytes = (uint32_t)min((uint64_t)256, n - k0) * 13;
-    uint32_t *o32 = reinterpret_cast<uint32_t *>(out + k0 * 13);
-    const uint32_t *b32 = reinterpret_cast<const uint32_t *>(buf);
-    for (uint32_t w = threadIdx.x; w < nbytes / 4; w += 256) o32[w] = b32[w];
-    for (uint32_t b = (nbytes & ~3u) + threadIdx.x; b < nbytes; b += 256) out[k0 * 13 + b] = buf[b];
 }
 
 }  // namespace bsdb

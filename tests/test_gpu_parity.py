@@ -174,6 +174,19 @@ def test_host_buffer_api(ctx):
     np.testing.assert_array_equal(ctx.hash_fixed_host(keys, 13), O.hash_fixed(keys, 13))
 
 
+def test_generator_beyond_2e32_work_items(ctx):
+    # 5e9 keys: more than 2^32 keys -> the generator must grid-stride
+    n = 5_000_000_000
+    keys = ctx.gen_keys13(0, n)
+    for i in (0, 2**32 - 1, 2**32, 2**32 + 12345, n - 1):
+        np.testing.assert_array_equal(keys[13 * i: 13 * i + 13].cpu().numpy(), O.gen_keys13(i, 1))
+    m = O.num_buckets(n)
+    c = ctx.histogram_fixed(keys, 13, m, n=n)
+    assert int(c.sum(dtype=torch.int64)) == n
+    assert int(c.max()) < 3000  # no hot bucket: distinct random-like keys
+    del keys
+
+
 def test_full_size_properties(ctx):
     """At a large size: total count, partitioned == atomic, sampled signatures."""
     n = 400_000_000
