@@ -140,8 +140,8 @@ void launch_pass1(const P1Args &a0, bool var, uint32_t key_len, uint64_t tiles, 
 
 struct PartPlan {
     uint32_t nparts;
-    uint32_t nregions;  // regions per partition in the id buffer
-    uint32_t region0;   // first shared (atomic-cursor) region
+    uint32_t nregions;  // regions per partition in the id buffer (one per XCD)
+    uint32_t region0;   // first region used by k_pass1
     uint32_t grid_d13;  // persistent workgroups of the 13-byte kernel (0 = generic path)
     uint64_t cap;       // ids per (partition, region), multiple of 8
     uint32_t rpw;       // pass 2: regions per workgroup
@@ -151,27 +151,16 @@ struct PartPlan {
 
 uint64_t round8(double x) { return ((uint64_t)x + 7) & ~7ULL; }
 
-// Region capacities: expected share of a full partition plus 8 sigma and
-// slack (a fill beyond cap raises the overflow flag: the chunk is recounted).
+// Region capacities: expected share of a full partition per XCD copy plus 8
+// sigma and slack (a fill beyond cap raises the overflow flag: the chunk is
+// recounted with direct atomics).
 PartPlan plan_partitions(const bsdb_ctx *c, uint64_t chunk, uint64_t m, bool d13) {
     PartPlan p{};
     p.nparts = (uint32_t)((m + PART_BUCKETS - 1) / PART_BUCKETS);
     const double frac = std::min(1.0, (double)PART_BUCKETS / (double)m);
     const uint64_t tiles = (chunk + P1_TILE - 1) / P1_TILE;
-    if (d13) {
-        // one private region per persistent workgroup + NCOPY shared regions
-        // for the bounds-checked tail tiles
-        p.grid_d13 = (uint32_t)std::min<uint64_t>(tiles, (uint64_t)c->num_cus * 2);
-        const uint64_t tw = (tiles + p.grid_d13 - 1) / p.grid_d13;
-        const double e = (double)tw * P1_TILE * frac;
-        p.cap = std::max<uint64_t>(P1_TILE + 64, round8(e * 1.02 + 8.0 * std::sqrt(e) + 64));
-        p.region0 = p.grid_d13;
-        p.nregions = p.grid_d13 + NCOPY;
-        const uint32_t groups = std::max<uint32_t>(1, std::min<uint32_t>(p.nregions, 2048 / p.nparts));
-        p.rpw = (p.nregions + groups - 1) / groups;
-        p.nslices = 1;
-        p.slice = (uint32_t)p.cap;
-    } else {
+    p.grid_d13 = d13 ? (uint32_t)std::min<uint64_t>(tiles, (uint64_t)c->num_cus * 2) : 0;
+    {
         const double e = (double)chunk * frac / NCOPY;
         p.cap = round8(e * 1.02 + 8.0 * std::sqrt(e) + 2 * P1_TILE + 64);
         p.region0 = 0;
@@ -247,13 +236,17 @@ int histogram_impl(bsdb_ctx *c, const uint8_t *keys, const uint64_t *offsets, ui
                     const uint64_t grid = std::min<uint64_t>(nfast, pp.grid_d13);
                     if (c->d13_variant == 1)
                         k_pass1_d13<1><<<(uint32_t)grid, P1_THREADS, 0, s>>>(ac, nfast);
-                    else if (c->d13_variant == 2)
-                        k_pass1_d13<2><<<(uint32_t)grid, P1_THREADS, 0, s>>>(ac, nfast);
+                    else if (c->d13_variant == 3)
+                        k_pass1_d13<3><<<(uint32_t)grid, P1_THREADS, 0, s>>>(ac, nfast);
+                    else if (c->d13_variant == 4)
+                        k_pass1_d13<4><<<(uint32_t)grid, P1_THREADS, 0, s>>>(ac, nfast);
+                    else if (c->d13_variant == 5)
+                        k_pass1_d13<5><<<(uint32_t)grid, P1_THREADS, 0, s>>>(ac, nfast);
                     else
                         k_pass1_d13<0><<<(uint32_t)grid, P1_THREADS, 0, s>>>(ac, nfast);
                 }
                 if (nfast < tiles) {
-                    P1Args at = ac;
+                    P1Args at = ac;  // shares the 8 XCD regions (atomic cursors)
                     at.keys = ac.keys + nfast * P1_TILE * 13;
                     at.n = nk - nfast * P1_TILE;
                     at.blob_bytes = at.n * 13;

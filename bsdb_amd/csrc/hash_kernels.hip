@@ -42,7 +42,7 @@ struct P1Args {
     uint64_t seed;
     uint64_t multiplier;      // 2 * num_buckets
     // EPI_PARTITION
-    uint16_t *ids;            // [P][nregions][cap]
+    uint16_t *ids;            // [nregions][P][cap]
     uint32_t *cursor;         // [nregions][P] fill of each region
     uint32_t *overflow;       // set when a region would overflow
     uint64_t cap;             // capacity of one (partition, region) slot, multiple of 8
@@ -320,7 +320,7 @@ __global__ __launch_bounds__(P1_THREADS, 4) void k_pass1(P1Args a) {
         const uint32_t p = b >> PART_SHIFT;
         const uint64_t idx = (uint64_t)base[p] + (j - start[p]);
         if (idx < a.cap) {
-            a.ids[((uint64_t)p * a.nregions + copy) * a.cap + idx] = (uint16_t)(b & (PART_BUCKETS - 1));
+            a.ids[((uint64_t)copy * a.nparts + p) * a.cap + idx] = (uint16_t)(b & (PART_BUCKETS - 1));
         } else {
             ovf = true;
         }
@@ -335,38 +335,33 @@ __global__ __launch_bounds__(P1_THREADS, 4) void k_pass1(P1Args a) {
 // of tile t hashes, the next is in flight; the next tile's first quarters are
 // issued as soon as a set is consumed, so HBM reads continue through the hashing and through the
 // tile epilogue (counting sort by partition, cursor reservation, run-wise
-// write-out).  Bucket ids stay in registers; LDS holds only the sorted tile.
+// write-out into XCD-shared regions).  Bucket ids stay in registers; LDS holds
+// only the sorted tile.
 // (Two sets of 8 windows spilled at 4 waves/SIMD; quarters of 4 keys in two
 // alternating sets of 4 windows fit the 128-VGPR budget.)
 constexpr int D13_Q = 4;                          // keys per quarter
 constexpr int D13_NQ = P1_KEYS_PER_THREAD / D13_Q;  // quarters per tile
 
 // VARIANT (profiling builds only; 0 in production): 1 = skip the tile
-// epilogue, 2 = also skip the LDS partition counts (pure load + hash + bucket).
+// epilogue, 3 = no global id stores, 4 = no LDS scatter (stores of stale slots),
+// 5 = scan + barriers only.
 template <int VARIANT>
 __global__ __launch_bounds__(P1_THREADS, 4) void k_pass1_d13(P1Args a, uint64_t ntiles) {
     __shared__ uint32_t sorted[P1_TILE];
-    __shared__ uint32_t hist[MAX_PARTS], run[MAX_PARTS], cur[MAX_PARTS];
+    __shared__ uint32_t hist[MAX_PARTS], run[MAX_PARTS];
     __shared__ uint64_t off64[MAX_PARTS];
     __shared__ uint32_t wsum[P1_THREADS / 64];
     __shared__ uint32_t tile_ovf;
     const int tid = threadIdx.x;
     const uint32_t P = a.nparts;
-    const uint64_t pstride = (uint64_t)a.nregions * a.cap;
     if (tid == 0) tile_ovf = 0;
     const uint32_t mult = (uint32_t)a.multiplier;
     const W64 seedw = w64(a.seed);
     const uint64_t G = gridDim.x;
-    for (int i = tid; i < MAX_PARTS; i += P1_THREADS) {
-        hist[i] = 0;
-        cur[i] = 0;
-    }
+    for (int i = tid; i < MAX_PARTS; i += P1_THREADS) hist[i] = 0;
 
     uint64_t t = blockIdx.x;
-    if (t >= ntiles) {
-        for (int i = tid; i < (int)P; i += P1_THREADS) a.cursor[(uint64_t)blockIdx.x * P + i] = 0;
-        return;
-    }
+    if (t >= ntiles) return;
     // every tile here is full and readable 3 bytes past its last key: the host
     // sends the ragged last tile to k_pass1<SRC_DIRECT13> (bounds-checked)
     // two register sets of D13_Q windows, alternating over the quarters
@@ -406,7 +401,7 @@ __global__ __launch_bounds__(P1_THREADS, 4) void k_pass1_d13(P1Args a, uint64_t 
         load_q(X, t + G, 0);
         hash_q(Y, 3);
         load_q(Y, t + G, 1);
-        if (VARIANT) {
+        if (VARIANT == 1) {
             uint32_t x = 0;
 #pragma unroll
             for (int j = 0; j < P1_KEYS_PER_THREAD; ++j) x ^= bk[j];
@@ -414,19 +409,19 @@ __global__ __launch_bounds__(P1_THREADS, 4) void k_pass1_d13(P1Args a, uint64_t 
             continue;
         }
         __syncthreads();  // all hist adds of this tile done
+        // Regions are shared by the workgroups of one XCD (copy = t % 8: tiles
+        // are dealt round-robin, so copy c is written from one XCD's L2, where
+        // consecutive reservations by different workgroups complete 128-byte
+        // lines quickly).  The returning cursor atomic overlaps the LDS scatter.
+        const uint32_t copy = (uint32_t)(t & (NCOPY - 1));
         const uint32_t cnt = tid < (int)P ? hist[tid] : 0;
         uint32_t total;
         const uint32_t excl = block_excl_scan(cnt, wsum, tid, total);
+        uint32_t my_base = 0;
         if (tid < (int)P) {
             run[tid] = excl;
             hist[tid] = 0;  // ready for the next tile
-            // private region of this workgroup: no global atomics.  off64[p] is
-            // the element offset of sorted position 0 for partition p, so the
-            // write-out address of sorted slot j is ids + off64[p] + j.
-            const uint32_t b0 = cur[tid];
-            cur[tid] = b0 + cnt;
-            if ((uint64_t)b0 + cnt > a.cap) tile_ovf = 1;
-            off64[tid] = (uint64_t)tid * pstride + (uint64_t)blockIdx.x * a.cap + b0 - excl;
+            if (cnt) my_base = atomicAdd(a.cursor + copy * P + tid, cnt);
         }
         __syncthreads();
         uint32_t pos[P1_KEYS_PER_THREAD];
@@ -434,6 +429,11 @@ __global__ __launch_bounds__(P1_THREADS, 4) void k_pass1_d13(P1Args a, uint64_t 
         for (int j = 0; j < P1_KEYS_PER_THREAD; ++j) pos[j] = atomicAdd(&run[bk[j] >> PART_SHIFT], 1u);
 #pragma unroll
         for (int j = 0; j < P1_KEYS_PER_THREAD; ++j) sorted[pos[j]] = bk[j];
+        if (tid < (int)P) {
+            if ((uint64_t)my_base + cnt > a.cap) tile_ovf = 1;
+            // element offset of sorted slot 0 for partition p
+            off64[tid] = ((uint64_t)copy * P + tid) * a.cap + my_base - excl;
+        }
         __syncthreads();
         if (!tile_ovf) {
             // batched: 16 sorted reads, 16 offset reads, 16 two-byte stores
@@ -443,18 +443,21 @@ __global__ __launch_bounds__(P1_THREADS, 4) void k_pass1_d13(P1Args a, uint64_t 
             uint64_t so[P1_KEYS_PER_THREAD];
 #pragma unroll
             for (int j = 0; j < P1_KEYS_PER_THREAD; ++j) so[j] = off64[sb[j] >> PART_SHIFT];
+            if (VARIANT == 3) {
+                uint32_t x = 0;
 #pragma unroll
-            for (int j = 0; j < P1_KEYS_PER_THREAD; ++j)
-                a.ids[so[j] + tid + j * P1_THREADS] = (uint16_t)(sb[j] & (PART_BUCKETS - 1));
+                for (int j = 0; j < P1_KEYS_PER_THREAD; ++j) x ^= (uint32_t)so[j] ^ sb[j];
+                if (x == 0xFFFFFFFFu) a.overflow[1] = x;
+            } else {
+#pragma unroll
+                for (int j = 0; j < P1_KEYS_PER_THREAD; ++j)
+                    a.ids[so[j] + tid + j * P1_THREADS] = (uint16_t)(sb[j] & (PART_BUCKETS - 1));
+            }
         } else if (tid == 0) {
             atomicOr(a.overflow, 1u);
         }
         __syncthreads();  // sorted / run / off64 reused by the next tile
     }
-    // publish this workgroup's region fills for pass 2 (plain stores; the
-    // kernel boundary orders them before pass 2 reads)
-    if (VARIANT == 0)
-        for (int i = tid; i < (int)P; i += P1_THREADS) a.cursor[(uint64_t)blockIdx.x * P + i] = cur[i];
 }
 
 // Pass 2: LDS histogram of partition p = blockIdx.y over a group of regions
@@ -481,7 +484,7 @@ __global__ __launch_bounds__(P2_THREADS, 4) void k_pass2(const uint16_t *ids, co
         const uint64_t fill = min((uint64_t)cursor[(uint64_t)r * nparts + p], cap);
         if (fill <= lo) continue;
         const uint64_t hi = min(fill, lo + slice);
-        const uint16_t *src = ids + ((uint64_t)p * nregions + r) * cap;
+        const uint16_t *src = ids + ((uint64_t)r * nparts + p) * cap;
         // lo and cap are multiples of 8: 16-B aligned vectors
         const uint64_t nvec = (hi - lo) >> 3;
         const uint4 *v = reinterpret_cast<const uint4 *>(src + lo);
