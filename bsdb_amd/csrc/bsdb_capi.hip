@@ -198,8 +198,10 @@ int histogram_impl(bsdb_ctx *c, const uint8_t *keys, const uint64_t *offsets, ui
     uint64_t chunk = c->chunk_keys ? c->chunk_keys : DEFAULT_CHUNK_KEYS;
     chunk = std::max<uint64_t>(P1_TILE, chunk / P1_TILE * P1_TILE);
     chunk = std::min<uint64_t>(chunk, (n + P1_TILE - 1) / P1_TILE * P1_TILE);
-    const bool d13 = !var && key_len == 13 && c->frontend == 0;
-    const PartPlan pp = plan_partitions(c, chunk, m, d13);
+    bool d13 = !var && key_len == 13 && c->frontend == 0;
+    PartPlan pp = plan_partitions(c, chunk, m, d13);
+    // the 13-byte kernel addresses the id buffer with 32-bit element offsets
+    if (d13 && (uint64_t)pp.nparts * pp.nregions * pp.cap >= (1ULL << 32)) d13 = false;
     int rc = grow(&c->ids, &c->ids_bytes, (size_t)pp.nparts * pp.nregions * pp.cap * sizeof(uint16_t));
     if (rc) return rc;
     rc = grow((void **)&c->cursor, &c->cursor_bytes, (size_t)pp.nparts * pp.nregions * sizeof(uint32_t));

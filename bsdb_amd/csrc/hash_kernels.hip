@@ -349,7 +349,7 @@ template <int VARIANT>
 __global__ __launch_bounds__(P1_THREADS, 4) void k_pass1_d13(P1Args a, uint64_t ntiles) {
     __shared__ uint32_t sorted[P1_TILE];
     __shared__ uint32_t hist[MAX_PARTS], run[MAX_PARTS];
-    __shared__ uint64_t off64[MAX_PARTS];
+    __shared__ uint32_t off32[MAX_PARTS];
     __shared__ uint32_t wsum[P1_THREADS / 64];
     __shared__ uint32_t tile_ovf;
     const int tid = threadIdx.x;
@@ -381,6 +381,7 @@ __global__ __launch_bounds__(P1_THREADS, 4) void k_pass1_d13(P1Args a, uint64_t 
 
     for (; t < ntiles; t += G) {
         uint32_t bk[P1_KEYS_PER_THREAD];
+        uint32_t rk[P1_KEYS_PER_THREAD / 2];  // rank within (tile, partition), two u16 per register
         auto hash_q = [&](const u32x4a(&R)[D13_Q], int q) {
 #pragma unroll
             for (int j = 0; j < D13_Q; ++j) {
@@ -389,8 +390,11 @@ __global__ __launch_bounds__(P1_THREADS, 4) void k_pass1_d13(P1Args a, uint64_t 
                 W64 s0, s1;
                 spooky13_w(R[j].x, R[j].y, R[j].z, R[j].w, sh, seedw, s0, s1);
                 const uint32_t b = bucket_of_w(s0, mult);
-                bk[q * D13_Q + j] = b;
-                if (VARIANT < 2) atomicAdd(&hist[b >> PART_SHIFT], 1u);
+                const int jj = q * D13_Q + j;
+                bk[jj] = b;
+                // the count's old value is this key's rank in its partition run
+                const uint32_t r = atomicAdd(&hist[b >> PART_SHIFT], 1u);
+                if (jj & 1) rk[jj >> 1] |= r << 16; else rk[jj >> 1] = r;
             }
         };
         hash_q(X, 0);
@@ -419,20 +423,22 @@ __global__ __launch_bounds__(P1_THREADS, 4) void k_pass1_d13(P1Args a, uint64_t 
         const uint32_t excl = block_excl_scan(cnt, wsum, tid, total);
         uint32_t my_base = 0;
         if (tid < (int)P) {
-            run[tid] = excl;
-            hist[tid] = 0;  // ready for the next tile
+            run[tid] = excl;  // partition start in the sorted tile (read-only below)
+            hist[tid] = 0;    // ready for the next tile
             if (cnt) my_base = atomicAdd(a.cursor + copy * P + tid, cnt);
         }
         __syncthreads();
-        uint32_t pos[P1_KEYS_PER_THREAD];
+        // scatter: slot = start[p] + rank (plain LDS reads, broadcast on equal p)
 #pragma unroll
-        for (int j = 0; j < P1_KEYS_PER_THREAD; ++j) pos[j] = atomicAdd(&run[bk[j] >> PART_SHIFT], 1u);
-#pragma unroll
-        for (int j = 0; j < P1_KEYS_PER_THREAD; ++j) sorted[pos[j]] = bk[j];
+        for (int j = 0; j < P1_KEYS_PER_THREAD; ++j) {
+            const uint32_t r = (rk[j >> 1] >> ((j & 1) * 16)) & 0xFFFFu;
+            sorted[run[bk[j] >> PART_SHIFT] + r] = bk[j];
+        }
         if (tid < (int)P) {
             if ((uint64_t)my_base + cnt > a.cap) tile_ovf = 1;
-            // element offset of sorted slot 0 for partition p
-            off64[tid] = ((uint64_t)copy * P + tid) * a.cap + my_base - excl;
+            // element offset of sorted slot 0 for partition p (ids buffer < 2^32
+            // elements: checked by the host plan)
+            off32[tid] = (uint32_t)(((uint64_t)copy * P + tid) * a.cap + my_base - excl);
         }
         __syncthreads();
         if (!tile_ovf) {
@@ -440,9 +446,9 @@ __global__ __launch_bounds__(P1_THREADS, 4) void k_pass1_d13(P1Args a, uint64_t 
             uint32_t sb[P1_KEYS_PER_THREAD];
 #pragma unroll
             for (int j = 0; j < P1_KEYS_PER_THREAD; ++j) sb[j] = sorted[tid + j * P1_THREADS];
-            uint64_t so[P1_KEYS_PER_THREAD];
+            uint32_t so[P1_KEYS_PER_THREAD];
 #pragma unroll
-            for (int j = 0; j < P1_KEYS_PER_THREAD; ++j) so[j] = off64[sb[j] >> PART_SHIFT];
+            for (int j = 0; j < P1_KEYS_PER_THREAD; ++j) so[j] = off32[sb[j] >> PART_SHIFT];
             if (VARIANT == 3) {
                 uint32_t x = 0;
 #pragma unroll
@@ -451,7 +457,7 @@ __global__ __launch_bounds__(P1_THREADS, 4) void k_pass1_d13(P1Args a, uint64_t 
             } else {
 #pragma unroll
                 for (int j = 0; j < P1_KEYS_PER_THREAD; ++j)
-                    a.ids[so[j] + tid + j * P1_THREADS] = (uint16_t)(sb[j] & (PART_BUCKETS - 1));
+                    a.ids[(uint64_t)(so[j] + tid + j * P1_THREADS)] = (uint16_t)(sb[j] & (PART_BUCKETS - 1));
             }
         } else if (tid == 0) {
             atomicOr(a.overflow, 1u);
