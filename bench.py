@@ -156,8 +156,8 @@ def main():
         if os.path.exists(prof):
             try:
                 pj = json.load(open(prof))
-                if pj.get("keys_per_launch") == keys_per_launch:
-                    traffic = pj.get("hbm_bytes_per_launch")
+                if abs(pj.get("keys_per_launch", 0) - keys_per_launch) < 1.0:
+                    traffic = pj.get("hbm_bytes_per_launch")  # PMC bytes / launch (profiles/)
             except Exception:
                 traffic = None
         log(f"timed {args.steps} steps: {dt * 1e3 / args.steps:.2f} ms/step")
