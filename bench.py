@@ -65,12 +65,14 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--n", type=int, default=README_N, help="total keys (all ranks)")
+    ap.add_argument("--num-keys", dest="n", type=int, default=README_N, help="total keys (all ranks)")
     ap.add_argument("--mode", type=int, default=0, help="0 auto/partitioned, 2 direct atomics")
     ap.add_argument("--chunk", type=int, default=0, help="keys per partitioned chunk (0 = default)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="collective backend (nccl = RCCL over xGMI; gloo only to rehearse N ranks on one GPU)")
     args = ap.parse_args()
 
     import torch
@@ -82,13 +84,17 @@ def main():
     if world != args.gpus:
         if world == 1 and args.gpus > 1:
             raise SystemExit("--gpus N>1 must be launched with torch.distributed.run (one rank per GPU)")
-    torch.cuda.set_device(local_rank)
+    dev = local_rank % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(dev)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        else:
+            dist.init_process_group("gloo")
 
     from bsdb_amd import Context
-    ctx = Context(local_rank)
+    ctx = Context(dev)
     if args.mode:
         ctx.set_histogram_mode(args.mode)
     if args.chunk:
@@ -112,7 +118,14 @@ def main():
 
     def step():
         # local shard histogram, then ONE all-reduce over RCCL/xGMI (N>1)
-        global_histogram(lambda c: ctx.histogram_fixed(keys, KEY_LEN, m, counts=c, n=nloc), counts)
+        if world > 1 and args.backend == "gloo":
+            counts.zero_()
+            ctx.histogram_fixed(keys, KEY_LEN, m, counts=counts, n=nloc)
+            h = counts.cpu()
+            dist.all_reduce(h)
+            counts.copy_(h)
+        else:
+            global_histogram(lambda c: ctx.histogram_fixed(keys, KEY_LEN, m, counts=c, n=nloc), counts)
         ctx.edge_offsets(counts, out=E)
 
     for _ in range(args.warmup):
@@ -137,7 +150,7 @@ def main():
     p2_ms, p2_launches, _ = ctx.profile_read(ctx.PASS2)
     sc_ms, _, _ = ctx.profile_read(ctx.SCAN)
 
-    t = torch.tensor([dt, p1_ms, p2_ms], dtype=torch.float64, device="cuda")
+    t = torch.tensor([dt, p1_ms, p2_ms], dtype=torch.float64, device="cuda" if args.backend == "nccl" else "cpu")
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     dt, p1_ms_max, p2_ms_max = t.tolist()
@@ -183,7 +196,8 @@ def main():
                             "hash.checksum.bits=4; hash -> bucket -> histogram -> edge offsets",
                 "n_keys": n, "key_bytes": KEY_LEN, "num_buckets": m,
                 "keys_per_gpu": nloc if world == 1 else f"~{n // world}",
-                "parallelism": f"key-shard x{world}" + (" + RCCL all-reduce(histogram)" if world > 1 else ""),
+                "parallelism": f"key-shard x{world}" + ((" + RCCL all-reduce(histogram)" if args.backend == "nccl"
+                                                         else " + gloo all-reduce (rehearsal)") if world > 1 else ""),
                 "histogram_mode": "atomic" if args.mode == 2 else "partitioned-2pass",
             },
             "roofline": {
