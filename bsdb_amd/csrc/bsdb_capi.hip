@@ -27,6 +27,7 @@ struct bsdb_ctx {
     int frontend = 0;  // 13-byte keys: 0 auto (pipelined), 1 LDS-staged, 2 direct per-tile
     int num_cus = 256;
     int d13_variant = 0;  // profiling only (BSDB_D13_VARIANT): results are NOT valid when != 0
+    int d13_threads = 512;  // workgroup size of the pipelined 13-byte kernel (BSDB_D13_THREADS=256|512)
     uint64_t chunk_keys = 0;
     std::mutex mu;
     // workspace
@@ -232,27 +233,27 @@ int histogram_impl(bsdb_ctx *c, const uint8_t *keys, const uint64_t *offsets, ui
                 // full tiles whose 16-byte windows stay inside the chunk go to the
                 // pipelined kernel (private regions); the rest (at most two) to the
                 // bounds-checked kernel (shared regions region0..region0+7)
+                const uint64_t dtile = (uint64_t)c->d13_threads * P1_KEYS_PER_THREAD;
                 uint64_t nfast = 0;
-                if (ac.blob_bytes >= 3) nfast = std::min(tiles, ((ac.blob_bytes - 3) / 13) / P1_TILE);
+                if (ac.blob_bytes >= 3) nfast = std::min(nk / dtile, ((ac.blob_bytes - 3) / 13) / dtile);
                 if (nfast) {
-                    const uint64_t grid = std::min<uint64_t>(nfast, pp.grid_d13);
-                    if (c->d13_variant == 1)
-                        k_pass1_d13<1><<<(uint32_t)grid, P1_THREADS, 0, s>>>(ac, nfast);
-                    else if (c->d13_variant == 3)
-                        k_pass1_d13<3><<<(uint32_t)grid, P1_THREADS, 0, s>>>(ac, nfast);
-                    else if (c->d13_variant == 4)
-                        k_pass1_d13<4><<<(uint32_t)grid, P1_THREADS, 0, s>>>(ac, nfast);
-                    else if (c->d13_variant == 5)
-                        k_pass1_d13<5><<<(uint32_t)grid, P1_THREADS, 0, s>>>(ac, nfast);
-                    else
-                        k_pass1_d13<0><<<(uint32_t)grid, P1_THREADS, 0, s>>>(ac, nfast);
+                    const uint32_t per_cu = 2048 / c->d13_threads;  // 16 waves per CU
+                    const uint32_t grid = (uint32_t)std::min<uint64_t>(nfast, (uint64_t)c->num_cus * per_cu);
+#define BSDB_D13(V, T) k_pass1_d13<V, T><<<grid, T, 0, s>>>(ac, nfast)
+                    if (c->d13_threads == 256) {
+                        if (c->d13_variant == 1) BSDB_D13(1, 256); else if (c->d13_variant == 3) BSDB_D13(3, 256); else BSDB_D13(0, 256);
+                    } else {
+                        if (c->d13_variant == 1) BSDB_D13(1, 512); else if (c->d13_variant == 3) BSDB_D13(3, 512); else BSDB_D13(0, 512);
+                    }
+#undef BSDB_D13
                 }
-                if (nfast < tiles) {
+                const uint64_t done = nfast * dtile;
+                if (done < nk) {
                     P1Args at = ac;  // shares the 8 XCD regions (atomic cursors)
-                    at.keys = ac.keys + nfast * P1_TILE * 13;
-                    at.n = nk - nfast * P1_TILE;
+                    at.keys = ac.keys + done * 13;
+                    at.n = nk - done;
                     at.blob_bytes = at.n * 13;
-                    k_pass1<SRC_DIRECT13, EPI_PARTITION, 4, 13><<<(uint32_t)(tiles - nfast), P1_THREADS, 0, s>>>(at);
+                    k_pass1<SRC_DIRECT13, EPI_PARTITION, 4, 13><<<(uint32_t)((at.n + P1_TILE - 1) / P1_TILE), P1_THREADS, 0, s>>>(at);
                 }
             } else {
                 launch_pass1<EPI_PARTITION>(ac, var, key_len, tiles, s, c->frontend);
@@ -322,6 +323,7 @@ int bsdb_open(int device, bsdb_ctx **out) {
     if (!c) return BSDB_ENOMEM;
     c->device = device;
     if (const char *v = std::getenv("BSDB_D13_VARIANT")) c->d13_variant = std::atoi(v);
+    if (const char *v = std::getenv("BSDB_D13_THREADS")) c->d13_threads = std::atoi(v) == 256 ? 256 : 512;
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0)
         c->num_cus = cus;

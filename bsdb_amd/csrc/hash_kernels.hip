@@ -165,6 +165,29 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *wsum, 
     return pre + x - v;
 }
 
+// Block-wide exclusive scan of one u32 per thread (NT threads).
+template <int NT>
+__device__ __forceinline__ uint32_t block_excl_scan_n(uint32_t v, uint32_t *wsum, int tid, uint32_t &total) {
+    const int lane = tid & 63, wid = tid >> 6;
+    uint32_t x = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d, 64);
+        if (lane >= d) x += y;
+    }
+    if (lane == 63) wsum[wid] = x;
+    __syncthreads();
+    uint32_t pre = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < NT / 64; ++w) {
+        const uint32_t s = wsum[w];
+        pre += w < wid ? s : 0;
+        tot += s;
+    }
+    total = tot;
+    return pre + x - v;
+}
+
 // Pass 1: one workgroup = one tile of 8192 consecutive keys.
 template <int SRC, int EPI, int KPS, int LFIX>
 __global__ __launch_bounds__(P1_THREADS, 4) void k_pass1(P1Args a) {
@@ -345,12 +368,13 @@ constexpr int D13_NQ = P1_KEYS_PER_THREAD / D13_Q;  // quarters per tile
 // VARIANT (profiling builds only; 0 in production): 1 = skip the tile
 // epilogue, 3 = no global id stores, 4 = no LDS scatter (stores of stale slots),
 // 5 = scan + barriers only.
-template <int VARIANT>
-__global__ __launch_bounds__(P1_THREADS, 4) void k_pass1_d13(P1Args a, uint64_t ntiles) {
-    __shared__ uint32_t sorted[P1_TILE];
+template <int VARIANT, int NT>
+__global__ __launch_bounds__(NT, 4) void k_pass1_d13(P1Args a, uint64_t ntiles) {
+    constexpr int TILE = NT * P1_KEYS_PER_THREAD;
+    __shared__ uint32_t sorted[TILE];
     __shared__ uint32_t hist[MAX_PARTS], run[MAX_PARTS];
     __shared__ uint32_t off32[MAX_PARTS];
-    __shared__ uint32_t wsum[P1_THREADS / 64];
+    __shared__ uint32_t wsum[2 * NT / 64];
     __shared__ uint32_t tile_ovf;
     const int tid = threadIdx.x;
     const uint32_t P = a.nparts;
@@ -358,7 +382,7 @@ __global__ __launch_bounds__(P1_THREADS, 4) void k_pass1_d13(P1Args a, uint64_t 
     const uint32_t mult = (uint32_t)a.multiplier;
     const W64 seedw = w64(a.seed);
     const uint64_t G = gridDim.x;
-    for (int i = tid; i < MAX_PARTS; i += P1_THREADS) hist[i] = 0;
+    for (int i = tid; i < MAX_PARTS; i += NT) hist[i] = 0;
 
     uint64_t t = blockIdx.x;
     if (t >= ntiles) return;
@@ -370,7 +394,7 @@ __global__ __launch_bounds__(P1_THREADS, 4) void k_pass1_d13(P1Args a, uint64_t 
         if (tt < ntiles) {
 #pragma unroll
             for (int j = 0; j < D13_Q; ++j) {
-                const uint64_t byte = (tt * P1_TILE + tid + (q * D13_Q + j) * P1_THREADS) * 13;
+                const uint64_t byte = (tt * TILE + tid + (q * D13_Q + j) * NT) * 13;
                 R[j] = __builtin_nontemporal_load(reinterpret_cast<const u32x4a *>(a.keys + (byte & ~3ULL)));
             }
         }
@@ -385,7 +409,7 @@ __global__ __launch_bounds__(P1_THREADS, 4) void k_pass1_d13(P1Args a, uint64_t 
         auto hash_q = [&](const u32x4a(&R)[D13_Q], int q) {
 #pragma unroll
             for (int j = 0; j < D13_Q; ++j) {
-                const uint32_t kt = tid + (q * D13_Q + j) * P1_THREADS;
+                const uint32_t kt = tid + (q * D13_Q + j) * NT;
                 const uint32_t sh = ((kt * 13u) & 3u) * 8u;  // tile0*13 is a multiple of 4
                 W64 s0, s1;
                 spooky13_w(R[j].x, R[j].y, R[j].z, R[j].w, sh, seedw, s0, s1);
@@ -418,14 +442,22 @@ __global__ __launch_bounds__(P1_THREADS, 4) void k_pass1_d13(P1Args a, uint64_t 
         // consecutive reservations by different workgroups complete 128-byte
         // lines quickly).  The returning cursor atomic overlaps the LDS scatter.
         const uint32_t copy = (uint32_t)(t & (NCOPY - 1));
-        const uint32_t cnt = tid < (int)P ? hist[tid] : 0;
+        // partitions p = tid and p = tid + NT (P <= 2*NT)
+        const uint32_t p0 = tid, p1 = tid + NT;
+        const uint32_t c0 = p0 < P ? hist[p0] : 0, c1 = p1 < P ? hist[p1] : 0;
         uint32_t total;
-        const uint32_t excl = block_excl_scan(cnt, wsum, tid, total);
-        uint32_t my_base = 0;
-        if (tid < (int)P) {
-            run[tid] = excl;  // partition start in the sorted tile (read-only below)
-            hist[tid] = 0;    // ready for the next tile
-            if (cnt) my_base = atomicAdd(a.cursor + copy * P + tid, cnt);
+        const uint32_t e0 = block_excl_scan_n<NT>(c0 + c1, wsum, tid, total);
+        const uint32_t e1 = e0 + c0;
+        uint32_t b0 = 0, b1 = 0;
+        if (p0 < P) {
+            run[p0] = e0;  // partition start in the sorted tile (read-only below)
+            hist[p0] = 0;  // ready for the next tile
+            if (c0) b0 = atomicAdd(a.cursor + copy * P + p0, c0);
+        }
+        if (p1 < P) {
+            run[p1] = e1;
+            hist[p1] = 0;
+            if (c1) b1 = atomicAdd(a.cursor + copy * P + p1, c1);
         }
         __syncthreads();
         // scatter: slot = start[p] + rank (plain LDS reads, broadcast on equal p)
@@ -434,18 +466,22 @@ __global__ __launch_bounds__(P1_THREADS, 4) void k_pass1_d13(P1Args a, uint64_t 
             const uint32_t r = (rk[j >> 1] >> ((j & 1) * 16)) & 0xFFFFu;
             sorted[run[bk[j] >> PART_SHIFT] + r] = bk[j];
         }
-        if (tid < (int)P) {
-            if ((uint64_t)my_base + cnt > a.cap) tile_ovf = 1;
+        if (p0 < P) {
+            if ((uint64_t)b0 + c0 > a.cap) tile_ovf = 1;
             // element offset of sorted slot 0 for partition p (ids buffer < 2^32
             // elements: checked by the host plan)
-            off32[tid] = (uint32_t)(((uint64_t)copy * P + tid) * a.cap + my_base - excl);
+            off32[p0] = (uint32_t)(((uint64_t)copy * P + p0) * a.cap + b0 - e0);
+        }
+        if (p1 < P) {
+            if ((uint64_t)b1 + c1 > a.cap) tile_ovf = 1;
+            off32[p1] = (uint32_t)(((uint64_t)copy * P + p1) * a.cap + b1 - e1);
         }
         __syncthreads();
         if (!tile_ovf) {
             // batched: 16 sorted reads, 16 offset reads, 16 two-byte stores
             uint32_t sb[P1_KEYS_PER_THREAD];
 #pragma unroll
-            for (int j = 0; j < P1_KEYS_PER_THREAD; ++j) sb[j] = sorted[tid + j * P1_THREADS];
+            for (int j = 0; j < P1_KEYS_PER_THREAD; ++j) sb[j] = sorted[tid + j * NT];
             uint32_t so[P1_KEYS_PER_THREAD];
 #pragma unroll
             for (int j = 0; j < P1_KEYS_PER_THREAD; ++j) so[j] = off32[sb[j] >> PART_SHIFT];
@@ -457,7 +493,7 @@ __global__ __launch_bounds__(P1_THREADS, 4) void k_pass1_d13(P1Args a, uint64_t 
             } else {
 #pragma unroll
                 for (int j = 0; j < P1_KEYS_PER_THREAD; ++j)
-                    a.ids[(uint64_t)(so[j] + tid + j * P1_THREADS)] = (uint16_t)(sb[j] & (PART_BUCKETS - 1));
+                    a.ids[(uint64_t)(so[j] + tid + j * NT)] = (uint16_t)(sb[j] & (PART_BUCKETS - 1));
             }
         } else if (tid == 0) {
             atomicOr(a.overflow, 1u);
