@@ -17,6 +17,7 @@
 
 #include "../../include/bsdb_mi355x.h"
 #include "hash_kernels.hip"
+#include "mph_kernels.hip"
 
 using namespace bsdb;
 
@@ -466,6 +467,50 @@ int bsdb_profile_read(bsdb_ctx *c, int kind, double *total_ms, uint64_t *launche
     *launches = nl;
     *keys = nk;
     return BSDB_OK;
+}
+
+// ---- MPHF evaluation (A11-A13) ----------------------------------------------
+static uint32_t grid_for(const bsdb_ctx *c, uint64_t n) {
+    return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((n + 255) / 256, (uint64_t)c->num_cus * 16));
+}
+
+int bsdb_dev_lookup(bsdb_ctx *c, const uint64_t *d_sig, uint64_t nq, uint64_t n, uint64_t m, const uint64_t *d_E,
+                    const uint64_t *d_values, uint32_t width, const uint64_t *d_sigbits, int check, int64_t *d_out,
+                    void *stream) {
+    if (!c || m == 0 || m > 0x7FFFFFFFULL || width > 64 || (nq && (!d_sig || !d_out || !d_E || !d_values)) ||
+        (check && width && !d_sigbits) || !aligned16(d_sig))
+        return BSDB_EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    HIP_OK(hipSetDevice(c->device));
+    if (nq == 0) return BSDB_OK;
+    const MphView v{d_E, d_values, d_sigbits, n, (uint32_t)(2 * m), width};
+    k_lookup<<<grid_for(c, nq), 256, 0, pick(c, stream)>>>(v, d_sig, nq, check, d_out);
+    return launch_status();
+}
+
+int bsdb_dev_sign(bsdb_ctx *c, const uint64_t *d_sig, uint64_t n, uint64_t m, const uint64_t *d_E,
+                  const uint64_t *d_values, uint32_t width, uint64_t *d_sigbits, void *stream) {
+    if (!c || m == 0 || m > 0x7FFFFFFFULL || width == 0 || width > 64 || (n && (!d_sig || !d_E || !d_values || !d_sigbits)) ||
+        !aligned16(d_sig))
+        return BSDB_EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    HIP_OK(hipSetDevice(c->device));
+    if (n == 0) return BSDB_OK;
+    const MphView v{d_E, d_values, nullptr, n, (uint32_t)(2 * m), width};
+    k_sign<<<grid_for(c, n), 256, 0, pick(c, stream)>>>(v, d_sig, n, d_sigbits);
+    return launch_status();
+}
+
+int bsdb_dev_index_scatter(bsdb_ctx *c, const int64_t *d_rank, const uint64_t *d_addr, uint64_t count, uint64_t start,
+                           uint64_t len, uint64_t *d_index, const uint64_t *d_value8, const uint8_t *d_value_len,
+                           uint8_t *d_index_a, void *stream) {
+    if (!c || (count && (!d_rank || !d_addr || !d_index)) || (d_index_a && (!d_value8 || !d_value_len))) return BSDB_EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    HIP_OK(hipSetDevice(c->device));
+    if (count == 0) return BSDB_OK;
+    k_index_scatter<<<grid_for(c, count), 256, 0, pick(c, stream)>>>(d_rank, d_addr, count, start, len, d_index, d_value8,
+                                                                      d_value_len, d_index_a);
+    return launch_status();
 }
 
 // ---- host-buffer entry points ---------------------------------------------

@@ -34,6 +34,9 @@ SIGNATURES = [
     ("bsdb_dev_histogram_fixed", _i, [_vp, _vp, _u32, _u64, _u64, _u64, _vp, _vp]),
     ("bsdb_dev_histogram_var", _i, [_vp, _vp, _u64, _vp, _u64, _u64, _u64, _vp, _vp]),
     ("bsdb_dev_edge_offsets", _i, [_vp, _vp, _u64, _vp, _vp]),
+    ("bsdb_dev_lookup", _i, [_vp, _vp, _u64, _u64, _u64, _vp, _vp, _u32, _vp, _i, _vp, _vp]),
+    ("bsdb_dev_sign", _i, [_vp, _vp, _u64, _u64, _vp, _vp, _u32, _vp, _vp]),
+    ("bsdb_dev_index_scatter", _i, [_vp, _vp, _vp, _u64, _u64, _u64, _vp, _vp, _vp, _vp, _vp]),
     ("bsdb_set_histogram_mode", _i, [_vp, _i]),
     ("bsdb_set_frontend", _i, [_vp, _i]),
     ("bsdb_set_chunk_keys", _i, [_vp, _u64]),
@@ -190,6 +193,34 @@ class Context:
         _check("bsdb_dev_edge_offsets", lib().bsdb_dev_edge_offsets(
             self._h, _ptr(counts), m, _ptr(out), _stream(stream)))
         return out
+
+    # ---- A11-A13: MPHF evaluation over (E, values[, checksum bits])
+    def lookup(self, sig, n: int, E, values, width: int = 0, sigbits=None, check: bool = True, out=None,
+               stream=None):
+        import torch
+        nq = sig.shape[0]
+        if out is None:
+            out = torch.empty(nq, dtype=torch.int64, device=sig.device)
+        _check("bsdb_dev_lookup", lib().bsdb_dev_lookup(
+            self._h, _ptr(sig), nq, n, E.numel() - 1, _ptr(E), _ptr(values), width,
+            _ptr(sigbits) if sigbits is not None else None, 1 if check else 0, _ptr(out), _stream(stream)))
+        return out
+
+    def sign(self, sig, E, values, width: int, out=None, stream=None):
+        import torch
+        n = sig.shape[0]
+        if out is None:
+            out = torch.zeros((n * width + 63) // 64 + 1, dtype=torch.int64, device=sig.device)
+        _check("bsdb_dev_sign", lib().bsdb_dev_sign(
+            self._h, _ptr(sig), n, E.numel() - 1, _ptr(E), _ptr(values), width, _ptr(out), _stream(stream)))
+        return out
+
+    def index_scatter(self, rank, addr, start: int, length: int, index, value8=None, value_len=None, index_a=None,
+                      stream=None):
+        _check("bsdb_dev_index_scatter", lib().bsdb_dev_index_scatter(
+            self._h, _ptr(rank), _ptr(addr), rank.numel(), start, length, _ptr(index),
+            _ptr(value8) if value8 is not None else None, _ptr(value_len) if value_len is not None else None,
+            _ptr(index_a) if index_a is not None else None, _stream(stream)))
 
     def gen_keys13(self, first: int, n: int, out=None, stream=None):
         import torch

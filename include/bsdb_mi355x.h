@@ -91,6 +91,30 @@ int bsdb_dev_histogram_var(bsdb_ctx *ctx, const uint8_t *d_blob, uint64_t blob_b
 int bsdb_dev_edge_offsets(bsdb_ctx *ctx, const uint32_t *d_counts, uint64_t num_buckets,
                           uint64_t *d_E, void *stream);
 
+/* ---------------------------------------------------------------------------
+ * MPHF evaluation over a solved GOV structure (sux4j layout, GOV:292-313):
+ *   d_E       edgeOffsetAndSeed[num_buckets+1] (offset | local seed << 56)
+ *   d_values  the 2-bit value array (LongArrayBitVector words, LSB first)
+ *   d_sigbits the hash.checksum.bits list (width bits per rank), or NULL when width = 0
+ * A12 (GOV:557-569, mph.c:86-96): out[i] = rank of signature i, or -1 when the
+ * rank is >= n or the checksum bits differ (check != 0); check == 0 returns the
+ * unchecked rank (GOV:573-580).
+ * A11 (GOV:492-508): OR-s sig0 & mask(width) into d_sigbits at each key's rank
+ * (d_sigbits zeroed by the caller, ceil(n*width/64)+1 words).
+ * A13 (W:129-145): for records whose rank lies in [start, start+len):
+ * index[rank-start] = byte-reversed addr (REVERSE_ORDER, Common.java:61); with
+ * d_index_a, also the first min(value_len, 8) bytes of value8 (index.approximate).
+ * ------------------------------------------------------------------------- */
+int bsdb_dev_lookup(bsdb_ctx *ctx, const uint64_t *d_sig, uint64_t nq, uint64_t n, uint64_t num_buckets,
+                    const uint64_t *d_E, const uint64_t *d_values, uint32_t width,
+                    const uint64_t *d_sigbits, int check, int64_t *d_out, void *stream);
+int bsdb_dev_sign(bsdb_ctx *ctx, const uint64_t *d_sig, uint64_t n, uint64_t num_buckets,
+                  const uint64_t *d_E, const uint64_t *d_values, uint32_t width, uint64_t *d_sigbits,
+                  void *stream);
+int bsdb_dev_index_scatter(bsdb_ctx *ctx, const int64_t *d_rank, const uint64_t *d_addr, uint64_t count,
+                           uint64_t start, uint64_t len, uint64_t *d_index, const uint64_t *d_value8,
+                           const uint8_t *d_value_len, uint8_t *d_index_a, void *stream);
+
 /* Histogram path selection for bsdb_dev_histogram_* (benchmarks/tests):
  *   0 = auto (partitioned two-pass), 1 = partitioned two-pass, 2 = direct atomics. */
 int bsdb_set_histogram_mode(bsdb_ctx *ctx, int mode);

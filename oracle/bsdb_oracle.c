@@ -111,6 +111,9 @@ uint64_t bo_vertex_offset(uint64_t eos) { return ((eos & (~0ULL >> 8)) * 281) >>
 /* mph.c:63-71 (sux4j Linear3SystemSolver.signatureToEquation, GOV:564,577). */
 void bo_signature_to_equation(const uint64_t sig[2], uint64_t seed_bits, uint32_t nv, uint32_t e[3]) {
     uint64_t t[4];
+    /* nv == 0 (an empty bucket, reachable only by absent keys): Java's
+     * numberOfLeadingZeros(0) = 64 and shifts mod 64 give e = 0 */
+    if (nv == 0) { e[0] = e[1] = e[2] = 0; return; }
     bo_spooky_rehash(sig, seed_bits, t);
     const int shift = __builtin_clzll((uint64_t)nv);
     const uint64_t mask = (1ULL << shift) - 1;
@@ -341,3 +344,310 @@ int64_t bo_lookup(const bo_mph *m, const uint64_t sig[2]) {
 
 /* GOV:357,483-485 -- bitVector of 2*(1 + V) bits, V = n*281>>8. */
 uint64_t bo_values_words(uint64_t n) { return (2 * (1 + ((n * 281) >> 8)) + 63) / 64; }
+
+/* ======================================================================== *
+ * GOV build (A5 sort, A8 per-bucket solve, A11 signing).                   *
+ *                                                                          *
+ * Follows the GOV construction of GOV:329-508: bucket b holds the keys     *
+ * whose signature maps to b, sorted by unsigned (sig0, sig1) (CBHS:939-955)*
+ * with duplicates rejected (CBHS:969-972); its nv = vo(E[b+1]) - vo(E[b])  *
+ * variables (GOV:421-423); each key's equation is signatureToEquation     *
+ * (mph.c:63-71) under local seed j<<56, j = 0..255 (GOV:425-432); the     *
+ * solution stores 3 for a hinge whose value is 0 (GOV:126-139) and the    *
+ * lookup returns E[b] + #nonzero pairs before the hinge (GOV:557-580).    *
+ *                                                                          *
+ * The hinge assignment (orientation) and therefore the chosen solution is *
+ * this project's own deterministic algorithm, NOT sux4j 5.4.1's           *
+ * Linear3SystemSolver/Orient3Hypergraph (third-party, absent): parity     *
+ * unpinned; validity is checked through the reference's mph.c lookup.     *
+ *   1. peeling in rounds: every vertex of degree 1 at the start of a round *
+ *      claims its edge, the smallest such vertex of an edge wins;          *
+ *   2. the 2-core is oriented by greedy matching in edge order (first free *
+ *      vertex e0,e1,e2) plus BFS augmenting paths in edge order;           *
+ *   3. the core system (unknowns = core hinges, non-hinge vertices = 0) is *
+ *      solved over F3 by Gauss-Jordan (unique if nonsingular; a singular   *
+ *      or unorientable system moves to the next local seed);              *
+ *   4. peeled edges are solved in reverse round order.                     *
+ * ======================================================================== */
+static int cmp_sig(const void *a, const void *b) {
+    const uint64_t *x = (const uint64_t *)a, *y = (const uint64_t *)b;
+    if (x[0] != y[0]) return x[0] < y[0] ? -1 : 1;
+    if (x[1] != y[1]) return x[1] < y[1] ? -1 : 1;
+    return 0;
+}
+
+/* bit-sliced GF(3): value = p1 ? 1 : p2 ? 2 : 0 */
+static inline void gf3_add(uint64_t *x1, uint64_t *x2, const uint64_t y1, const uint64_t y2) {
+    const uint64_t a1 = *x1, a2 = *x2;
+    *x1 = (a1 & ~y1 & ~y2) | (~a1 & ~a2 & y1) | (a2 & y2);
+    *x2 = (a2 & ~y1 & ~y2) | (~a1 & ~a2 & y2) | (a1 & y1);
+}
+
+/* Solves one bucket.  sig: cnt sorted signatures; writes vals[nv] (0..3).
+ * Returns 0 solved, 1 unorientable/singular (try next seed). */
+static int solve_bucket(const uint64_t *sig, uint32_t cnt, uint32_t nv, uint64_t seed_bits, uint8_t *vals,
+                        int32_t *ws) {
+    memset(vals, 0, nv);
+    if (cnt == 0) return 0;
+    /* one key on one vertex: its edge is (0,0,0); h = 0 holds for any value and
+     * the hinge stores 3 (GOV:126-139).  Other triple edges take the next seed. */
+    if (cnt == 1 && nv == 1) { vals[0] = 3; return 0; }
+    int tiny = cnt <= 12;
+    /* workspace layout */
+    uint32_t *e = (uint32_t *)ws;                     /* 3*cnt */
+    uint32_t *deg = e + 3 * cnt;                      /* nv */
+    uint32_t *xe = deg + nv;                          /* nv: xor of incident edges */
+    int32_t *hinge = (int32_t *)(xe + nv);            /* cnt: hinge vertex of edge or -1 */
+    int32_t *round_of = hinge + cnt;                  /* cnt: peel round or -1 (core) */
+    int32_t *vowner = round_of + cnt;                 /* nv: edge owning vertex as hinge or -1 */
+    int32_t *claim = vowner + nv;                     /* cnt */
+    int32_t *bfs_prev = claim + cnt;                  /* cnt */
+    int32_t *bfs_via = bfs_prev + cnt;                /* cnt */
+    int32_t *queue = bfs_via + cnt;                   /* cnt */
+    uint8_t *seen_v = (uint8_t *)(queue + cnt);       /* nv */
+    uint8_t *xval = seen_v + nv;                      /* nv: solved F3 value per vertex */
+
+    for (uint32_t k = 0; k < cnt; k++) {
+        uint32_t ee[3];
+        bo_signature_to_equation(sig + 2 * k, seed_bits, nv, ee);
+        /* a repeated vertex is kept (coefficient 2); a triple one makes the
+         * equation 0 = h unsatisfiable for its orientation: next seed */
+        if (ee[0] == ee[1] && ee[1] == ee[2] && !tiny) return 1;
+        e[3 * k] = ee[0]; e[3 * k + 1] = ee[1]; e[3 * k + 2] = ee[2];
+    }
+    memset(deg, 0, nv * sizeof *deg);
+    memset(xe, 0, nv * sizeof *xe);
+    for (uint32_t k = 0; k < cnt; k++)
+        for (int i = 0; i < 3; i++) { deg[e[3 * k + i]]++; xe[e[3 * k + i]] ^= k; }
+    for (uint32_t k = 0; k < cnt; k++) { hinge[k] = -1; round_of[k] = -1; }
+    for (uint32_t v = 0; v < nv; v++) vowner[v] = -1;
+
+    /* 1. peeling in rounds */
+    int rounds = 0;
+    for (;;) {
+        int any = 0;
+        for (uint32_t k = 0; k < cnt; k++) claim[k] = -1;
+        for (uint32_t v = 0; v < nv; v++) {
+            if (deg[v] != 1) continue;
+            const uint32_t k = xe[v];
+            if (claim[k] < 0 || (uint32_t)claim[k] > v) claim[k] = (int32_t)v;
+        }
+        for (uint32_t k = 0; k < cnt; k++) {
+            if (claim[k] < 0) continue;
+            any = 1;
+            hinge[k] = claim[k];
+            vowner[claim[k]] = (int32_t)k;
+            round_of[k] = rounds;
+        }
+        if (!any) break;
+        for (uint32_t k = 0; k < cnt; k++) {
+            if (round_of[k] != rounds) continue;
+            for (int i = 0; i < 3; i++) { deg[e[3 * k + i]]--; xe[e[3 * k + i]] ^= k; }
+        }
+        rounds++;
+    }
+
+    /* 2. orientation of the 2-core: greedy, then BFS augmenting paths */
+    uint32_t ncore = 0;
+    for (uint32_t k = 0; k < cnt; k++) {
+        if (round_of[k] >= 0) continue;
+        ncore++;
+        for (int i = 0; i < 3; i++) {
+            const uint32_t v = e[3 * k + i];
+            if (vowner[v] < 0) { vowner[v] = (int32_t)k; hinge[k] = (int32_t)v; break; }
+        }
+    }
+    for (uint32_t k0 = 0; k0 < cnt; k0++) {
+        if (round_of[k0] >= 0 || hinge[k0] >= 0) continue;
+        /* BFS over edges: from edge k through vertex v to the edge owning v */
+        memset(seen_v, 0, nv);
+        int qh = 0, qt = 0, found_v = -1, found_e = -1;
+        queue[qt++] = (int32_t)k0;
+        bfs_prev[k0] = -1;
+        while (qh < qt && found_v < 0) {
+            const int32_t k = queue[qh++];
+            for (int i = 0; i < 3; i++) {
+                const uint32_t v = e[3 * k + i];
+                if (seen_v[v]) continue;
+                seen_v[v] = 1;
+                const int32_t o = vowner[v];
+                if (o < 0) { found_v = (int32_t)v; found_e = k; break; }
+                bfs_prev[o] = k;
+                bfs_via[o] = (int32_t)v;
+                queue[qt++] = o;
+            }
+        }
+        if (found_v < 0) return 1; /* unorientable */
+        /* flip along the path: found_e takes found_v, its old hinge goes to prev ... */
+        int32_t k = found_e, v = found_v;
+        for (;;) {
+            const int32_t old = hinge[k];
+            hinge[k] = v;
+            vowner[v] = k;
+            if (k == (int32_t)k0) break;
+            v = old;                 /* the vertex k gave up ... */
+            k = bfs_prev[k];         /* ... is taken by the edge we came from */
+            (void)bfs_via;
+        }
+    }
+
+    memset(xval, 0, nv);
+    /* tiny buckets (<= 12 keys: only in sets of n < ~1500) can be singular as a
+     * whole (nv == cnt makes every row sum to 0 mod 3): take the first assignment
+     * of the hinge values, in base-3 order with edge 0 least significant, that
+     * satisfies every equation */
+    if (tiny) {
+        uint32_t total = 1;
+        for (uint32_t k = 0; k < cnt; k++) total *= 3;
+        for (uint32_t a = 0; a < total; a++) {
+            uint32_t t = a;
+            for (uint32_t k = 0; k < cnt; k++) { xval[hinge[k]] = (uint8_t)(t % 3); t /= 3; }
+            int ok = 1;
+            for (uint32_t k = 0; k < cnt && ok; k++) {
+                int h = 0;
+                while (e[3 * k + h] != (uint32_t)hinge[k]) h++;
+                const uint32_t sum = xval[e[3 * k]] + xval[e[3 * k + 1]] + xval[e[3 * k + 2]];
+                ok = sum % 3 == (uint32_t)h;
+            }
+            if (ok) {
+                for (uint32_t k = 0; k < cnt; k++) vals[hinge[k]] = xval[hinge[k]] ? xval[hinge[k]] : 3;
+                return 0;
+            }
+        }
+        return 1;
+    }
+    /* 3. Gauss-Jordan over F3 on the core: rows = core edges, cols = core hinges */
+    if (ncore) {
+        int32_t *col_of = (int32_t *)malloc(nv * sizeof(int32_t));
+        int32_t *cols = (int32_t *)malloc(ncore * sizeof(int32_t));
+        int32_t *rows = (int32_t *)malloc(ncore * sizeof(int32_t));
+        uint32_t nc = 0, nr = 0;
+        for (uint32_t v = 0; v < nv; v++) col_of[v] = -1;
+        for (uint32_t k = 0; k < cnt; k++)
+            if (round_of[k] < 0) { rows[nr++] = (int32_t)k; col_of[hinge[k]] = (int32_t)nc; cols[nc++] = hinge[k]; }
+        const uint32_t W = (nc + 1 + 63) / 64; /* + RHS column nc */
+        uint64_t *m1 = (uint64_t *)calloc((size_t)nr * W, 8), *m2 = (uint64_t *)calloc((size_t)nr * W, 8);
+        for (uint32_t r = 0; r < nr; r++) {
+            const uint32_t k = (uint32_t)rows[r];
+            for (int i = 0; i < 3; i++) {
+                const int32_t c = col_of[e[3 * k + i]];
+                if (c < 0) continue;
+                uint64_t *w1 = &m1[(size_t)r * W + (c >> 6)], *w2 = &m2[(size_t)r * W + (c >> 6)];
+                const uint64_t bit = 1ULL << (c & 63);
+                gf3_add(w1, w2, bit, 0);  /* coefficient += 1 per occurrence */
+            }
+            int h = 0;
+            while (e[3 * k + h] != (uint32_t)hinge[k]) h++;
+            if (h == 1) m1[(size_t)r * W + (nc >> 6)] |= 1ULL << (nc & 63);
+            if (h == 2) m2[(size_t)r * W + (nc >> 6)] |= 1ULL << (nc & 63);
+        }
+        int singular = 0;
+        for (uint32_t c = 0; c < nc && !singular; c++) {
+            const uint32_t wc = c >> 6;
+            const uint64_t bit = 1ULL << (c & 63);
+            uint32_t p = c;
+            while (p < nr && !((m1[(size_t)p * W + wc] | m2[(size_t)p * W + wc]) & bit)) p++;
+            if (p == nr) { singular = 1; break; }
+            if (p != c)
+                for (uint32_t w = 0; w < W; w++) {
+                    uint64_t t = m1[(size_t)p * W + w]; m1[(size_t)p * W + w] = m1[(size_t)c * W + w]; m1[(size_t)c * W + w] = t;
+                    t = m2[(size_t)p * W + w]; m2[(size_t)p * W + w] = m2[(size_t)c * W + w]; m2[(size_t)c * W + w] = t;
+                }
+            if (m2[(size_t)c * W + wc] & bit) /* normalise pivot to 1: multiply row by 2 */
+                for (uint32_t w = 0; w < W; w++) {
+                    const uint64_t t = m1[(size_t)c * W + w]; m1[(size_t)c * W + w] = m2[(size_t)c * W + w]; m2[(size_t)c * W + w] = t;
+                }
+            for (uint32_t r = 0; r < nr; r++) {
+                if (r == c) continue;
+                const uint64_t f1 = m1[(size_t)r * W + wc] & bit, f2 = m2[(size_t)r * W + wc] & bit;
+                if (!f1 && !f2) continue;
+                /* row_r -= f * row_c: f=1 -> add 2*row_c (swapped planes); f=2 -> add row_c */
+                for (uint32_t w = 0; w < W; w++) {
+                    const uint64_t y1 = f1 ? m2[(size_t)c * W + w] : m1[(size_t)c * W + w];
+                    const uint64_t y2 = f1 ? m1[(size_t)c * W + w] : m2[(size_t)c * W + w];
+                    gf3_add(&m1[(size_t)r * W + w], &m2[(size_t)r * W + w], y1, y2);
+                }
+            }
+        }
+        if (!singular)
+            for (uint32_t c = 0; c < nc; c++) {
+                const uint64_t bit = 1ULL << (nc & 63);
+                const uint32_t wn = nc >> 6;
+                xval[cols[c]] = (m1[(size_t)c * W + wn] & bit) ? 1 : (m2[(size_t)c * W + wn] & bit) ? 2 : 0;
+            }
+        free(m1); free(m2); free(col_of); free(cols); free(rows);
+        if (singular) return 1;
+    }
+    /* 4. peeled edges, last round first */
+    for (int r = rounds - 1; r >= 0; r--)
+        for (uint32_t k = 0; k < cnt; k++) {
+            if (round_of[k] != r) continue;
+            int h = 0;
+            while (e[3 * k + h] != (uint32_t)hinge[k]) h++;
+            uint32_t s = 0, coef = 0;
+            for (int i = 0; i < 3; i++) {
+                if (e[3 * k + i] == (uint32_t)hinge[k]) coef++;
+                else s += xval[e[3 * k + i]];
+            }
+            const uint32_t rhs = ((uint32_t)h + 6 - s) % 3;
+            xval[hinge[k]] = (uint8_t)(coef == 1 ? rhs : (2 * rhs) % 3);  /* 2^-1 = 2 in F3 */
+        }
+    for (uint32_t k = 0; k < cnt; k++) vals[hinge[k]] = xval[hinge[k]] ? xval[hinge[k]] : 3;
+    return 0;
+}
+
+/* Scratch words needed by solve_bucket for a bucket of cnt keys, nv vertices. */
+static size_t solve_ws_words(uint32_t cnt, uint32_t nv) {
+    return (size_t)14 * cnt + 6 * (size_t)nv + 64;  /* 12 cnt + 4.5 nv + 1 used */
+}
+
+int bo_gov_build(const uint64_t *sig_in, uint64_t n, uint32_t sig_width, uint64_t *E, uint64_t *values,
+                 uint64_t values_words, uint64_t *signatures, uint64_t sig_words) {
+    const uint64_t m = bo_num_buckets(n);
+    uint64_t *sig = (uint64_t *)malloc((n ? n : 1) * 16);
+    memcpy(sig, sig_in, n * 16);
+    qsort(sig, n, 16, cmp_sig);
+    for (uint64_t i = 1; i < n; i++)
+        if (sig[2 * i] == sig[2 * i - 2] && sig[2 * i + 1] == sig[2 * i - 1]) { free(sig); return -1; }
+    /* A6: bucket histogram -> E low 56 bits (bucket is monotone in sig0) */
+    memset(E, 0, (m + 1) * sizeof *E);
+    for (uint64_t i = 0; i < n; i++) E[bo_bucket(sig[2 * i], m) + 1]++;
+    for (uint64_t b = 0; b < m; b++) E[b + 1] += E[b];
+    memset(values, 0, values_words * 8);
+    uint32_t maxc = 0;
+    for (uint64_t b = 0; b < m; b++) if (E[b + 1] - E[b] > maxc) maxc = (uint32_t)(E[b + 1] - E[b]);
+    const uint32_t maxnv = (uint32_t)(bo_vertex_offset(E[m]) + 2);
+    int32_t *ws = (int32_t *)malloc(solve_ws_words(maxc + 1, maxnv + 1) * 4 + 64);
+    uint8_t *vals = (uint8_t *)malloc(maxnv + 1);
+    int rc = 0;
+    for (uint64_t b = 0; b < m && !rc; b++) {
+        const uint64_t lo = E[b] & (~0ULL >> 8), hi = E[b + 1] & (~0ULL >> 8);
+        const uint64_t vo = bo_vertex_offset(lo);
+        const uint32_t nv = (uint32_t)(bo_vertex_offset(hi) - vo);
+        uint64_t j = 0;
+        for (; j < 256; j++)
+            if (!solve_bucket(sig + 2 * lo, (uint32_t)(hi - lo), nv, j << 56, vals, ws)) break;
+        if (j == 256) { rc = -2; break; }
+        E[b] |= j << 56;
+        for (uint32_t v = 0; v < nv; v++) values[(vo + v) >> 5] |= (uint64_t)vals[v] << (2 * ((vo + v) & 31));
+    }
+    free(ws);
+    free(vals);
+    if (!rc && sig_width) {
+        /* A11: signatures[rank] = sig0 & mask (GOV:492-508) */
+        memset(signatures, 0, sig_words * 8);
+        bo_mph mp = {n, 2 * m, 0, m, E, values, 0, NULL};
+        const uint64_t mask = sig_width == 64 ? ~0ULL : (1ULL << sig_width) - 1;
+        for (uint64_t i = 0; i < n; i++) {
+            const int64_t r = bo_lookup_nocheck(&mp, sig + 2 * i);
+            bo_bitlist_set(signatures, (uint64_t)r, sig_width, sig[2 * i] & mask);
+        }
+    }
+    free(sig);
+    return rc;
+}
+
+/* Batch lookup with or without the checksum test. */
+void bo_lookup_batch(const bo_mph *m, const uint64_t *sig, uint64_t n, int check, int64_t *out) {
+    for (uint64_t i = 0; i < n; i++) out[i] = check ? bo_lookup(m, sig + 2 * i) : bo_lookup_nocheck(m, sig + 2 * i);
+}

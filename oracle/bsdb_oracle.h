@@ -88,6 +88,7 @@ int bo_gov_build(const uint64_t *sig /* 2n, any order */, uint64_t n, uint32_t s
                  uint64_t *E, uint64_t *values, uint64_t values_words,
                  uint64_t *signatures, uint64_t sig_words);
 uint64_t bo_values_words(uint64_t n);    /* words of the 2-bit value array */
+void bo_lookup_batch(const bo_mph *m, const uint64_t *sig, uint64_t n, int check, int64_t *out);
 
 #ifdef __cplusplus
 }

@@ -205,3 +205,30 @@ def ref_lib():
         L.load_mph.restype = C.POINTER(RefMph)
         _ref = L
     return _ref
+
+
+def gov_build(sig: np.ndarray, width: int):
+    """CPU GOV build (own deterministic solver; see bsdb_oracle.c).  Returns
+    (rc, E, values, sigbits)."""
+    sig = np.ascontiguousarray(sig, np.uint64).reshape(-1, 2)
+    n = sig.shape[0]
+    m = num_buckets(n)
+    E = np.zeros(m + 1, np.uint64)
+    vw = int(lib().bo_values_words(n))
+    values = np.zeros(vw, np.uint64)
+    sw = (n * width + 63) // 64 + 1
+    sigbits = np.zeros(sw, np.uint64)
+    rc = lib().bo_gov_build(_p(sig, _u64p), n, width, _p(E, _u64p), _p(values, _u64p), vw, _p(sigbits, _u64p), sw)
+    return rc, E, values, sigbits
+
+
+def lookup_batch(sig: np.ndarray, n: int, E: np.ndarray, values: np.ndarray, width: int = 0, sigbits=None,
+                 check: bool = True) -> np.ndarray:
+    sig = np.ascontiguousarray(sig, np.uint64).reshape(-1, 2)
+    m = E.size - 1
+    sb = sigbits if sigbits is not None else np.zeros(1, np.uint64)
+    mp = BoMph(n, 2 * m, 0, m, _p(E, _u64p), _p(values, _u64p), width, _p(sb, _u64p))
+    out = np.zeros(max(sig.shape[0], 1), np.int64)
+    lib().bo_lookup_batch(C.byref(mp), _p(sig, _u64p), sig.shape[0], 1 if check else 0,
+                          out.ctypes.data_as(C.POINTER(C.c_int64)))
+    return out[: sig.shape[0]]

@@ -208,3 +208,75 @@ def test_full_size_properties(ctx):
     sig = u64(ctx.hash_fixed(dev(sample), 13))
     np.testing.assert_array_equal(sig, O.hash_fixed(sample, 13))
     del keys
+
+
+# ---------------------------------------------------------------- A11-A13
+@pytest.mark.parametrize("name", ["lk_ascii", "lk_k13"])
+def test_lookup_golden_reference_vectors(ctx, golden, name):
+    """Unchecked lookups == the reference's own mph_get_byte_array (golden)."""
+    blob, off = golden[name + "_blob"], golden[name + "_off"]
+    E, arr, res = golden[name + "_E"], golden[name + "_array"], golden[name + "_res"]
+    sig = ctx.hash_var(dev(blob), dev(off.view(np.int64)))
+    got = ctx.lookup(sig, off.size - 1, dev(E.view(np.int64)), dev(arr.view(np.int64)), check=False)
+    np.testing.assert_array_equal(got.cpu().numpy(), res)
+
+
+def _gov_set(n, width):
+    keys = [str(i).encode() for i in range(n)]
+    off = np.zeros(n + 1, np.uint64)
+    off[1:] = np.cumsum([len(k) for k in keys])
+    blob = np.frombuffer(b"".join(keys), np.uint8)
+    sig = O.hash_var(blob, off)
+    rc, E, values, sigbits = O.gov_build(sig, width)
+    assert rc == 0
+    return sig, E, values, sigbits
+
+
+@pytest.mark.parametrize("width", [0, 4, 12, 16, 64])
+def test_lookup_and_sign_match_oracle(ctx, width):
+    n = 20_000
+    sig, E, values, sigbits = _gov_set(n, width)
+    dsig, dE, dv = dev(sig.view(np.int64)), dev(E.view(np.int64)), dev(values.view(np.int64))
+    if width:
+        dsb = ctx.sign(dsig, dE, dv, width)
+        np.testing.assert_array_equal(dsb.cpu().numpy().view(np.uint64)[: sigbits.size - 1], sigbits[: sigbits.size - 1])
+    else:
+        dsb = None
+    got = ctx.lookup(dsig, n, dE, dv, width, dsb, check=True).cpu().numpy()
+    np.testing.assert_array_equal(got, O.lookup_batch(sig, n, E, values, width, sigbits))
+    assert np.array_equal(np.sort(got), np.arange(n))
+    # absent keys: same decisions as the oracle's checked lookup (GOV:567)
+    absent = np.random.default_rng(5).integers(0, 2**63, size=(50_000, 2), dtype=np.int64)
+    got2 = ctx.lookup(dev(absent), n, dE, dv, width, dsb, check=True).cpu().numpy()
+    np.testing.assert_array_equal(got2, O.lookup_batch(absent.view(np.uint64), n, E, values, width, sigbits))
+
+
+@pytest.mark.parametrize("approx", [False, True])
+def test_index_scatter(ctx, approx):
+    rng = np.random.default_rng(11)
+    n = 30_000
+    rank = rng.permutation(n).astype(np.int64)
+    rank[::97] = -1                      # rejected lookups are skipped
+    addr = rng.integers(0, 2**63, n, dtype=np.int64)
+    v8 = rng.integers(0, 2**63, n, dtype=np.int64)
+    vlen = rng.integers(1, 40, n).astype(np.uint8)
+    for start, length in ((0, n), (5000, 7000), (29_990, 10)):   # W:112-150 passes
+        idx = torch.zeros(length, dtype=torch.int64, device="cuda")
+        ia = torch.zeros(length * 8, dtype=torch.uint8, device="cuda") if approx else None
+        ctx.index_scatter(dev(rank), dev(addr), start, length, idx,
+                          dev(v8) if approx else None, dev(vlen) if approx else None, ia)
+        want = np.zeros(length, np.uint64)
+        want_a = np.zeros(length * 8, np.uint8)
+        for i in range(n):
+            r = rank[i]
+            if r < 0 or not (start <= r < start + length):
+                continue
+            want[r - start] = int(addr[i]).to_bytes(8, "little")[::-1].__int__() if False else \
+                int.from_bytes(int(addr[i]).to_bytes(8, "little"), "big")
+            if approx:
+                b = int(v8[i]).to_bytes(8, "little")
+                k = min(int(vlen[i]), 8)
+                want_a[(r - start) * 8:(r - start) * 8 + k] = np.frombuffer(b[:k], np.uint8)
+        np.testing.assert_array_equal(idx.cpu().numpy().view(np.uint64), want)
+        if approx:
+            np.testing.assert_array_equal(ia.cpu().numpy(), want_a)
