@@ -271,8 +271,8 @@ def test_index_scatter(ctx, approx):
             r = rank[i]
             if r < 0 or not (start <= r < start + length):
                 continue
-            want[r - start] = int(addr[i]).to_bytes(8, "little")[::-1].__int__() if False else \
-                int.from_bytes(int(addr[i]).to_bytes(8, "little"), "big")
+            # Long.reverseBytes(addr) (W:138, REVERSE_ORDER on little-endian hosts)
+            want[r - start] = int.from_bytes(int(addr[i]).to_bytes(8, "little"), "big")
             if approx:
                 b = int(v8[i]).to_bytes(8, "little")
                 k = min(int(vlen[i]), 8)
