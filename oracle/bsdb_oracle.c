@@ -365,10 +365,12 @@ uint64_t bo_values_words(uint64_t n) { return (2 * (1 + ((n * 281) >> 8)) + 63) 
  *   2. the 2-core is oriented by greedy matching in edge order (first free *
  *      vertex e0,e1,e2) plus BFS augmenting paths in edge order;           *
  *   3. the core system (unknowns = core hinges, non-hinge vertices = 0) is *
- *      solved over F3 by Gauss-Jordan (unique if nonsingular; a singular   *
- *      or unorientable system moves to the next local seed);              *
+ *      solved over F3 block by block on the SCCs of its dependency graph   *
+ *      (Gauss-Jordan per block; a singular block or an unorientable core   *
+ *      moves to the next local seed);                                      *
  *   4. peeled edges are solved in reverse round order.                     *
  * ======================================================================== */
+
 static int cmp_sig(const void *a, const void *b) {
     const uint64_t *x = (const uint64_t *)a, *y = (const uint64_t *)b;
     if (x[0] != y[0]) return x[0] < y[0] ? -1 : 1;
@@ -516,67 +518,118 @@ static int solve_bucket(const uint64_t *sig, uint32_t cnt, uint32_t nv, uint64_t
         }
         return 1;
     }
-    /* 3. Gauss-Jordan over F3 on the core: rows = core edges, cols = core hinges */
+    /* 3. the core system, unknowns = core hinges (non-hinge vertices are 0),
+     * solved block by block over the strongly connected components of "edge k
+     * uses the hinge of edge k'" (Tarjan, iterative, edges in increasing order;
+     * components come out sinks first, so every block sees its dependencies
+     * solved).  A singular block fails the seed.  (When every block is
+     * nonsingular the core matrix is, and the solution is its unique one.) */
     if (ncore) {
-        int32_t *col_of = (int32_t *)malloc(nv * sizeof(int32_t));
-        int32_t *cols = (int32_t *)malloc(ncore * sizeof(int32_t));
-        int32_t *rows = (int32_t *)malloc(ncore * sizeof(int32_t));
-        uint32_t nc = 0, nr = 0;
-        for (uint32_t v = 0; v < nv; v++) col_of[v] = -1;
-        for (uint32_t k = 0; k < cnt; k++)
-            if (round_of[k] < 0) { rows[nr++] = (int32_t)k; col_of[hinge[k]] = (int32_t)nc; cols[nc++] = hinge[k]; }
-        const uint32_t W = (nc + 1 + 63) / 64; /* + RHS column nc */
-        uint64_t *m1 = (uint64_t *)calloc((size_t)nr * W, 8), *m2 = (uint64_t *)calloc((size_t)nr * W, 8);
-        for (uint32_t r = 0; r < nr; r++) {
-            const uint32_t k = (uint32_t)rows[r];
-            for (int i = 0; i < 3; i++) {
-                const int32_t c = col_of[e[3 * k + i]];
-                if (c < 0) continue;
-                uint64_t *w1 = &m1[(size_t)r * W + (c >> 6)], *w2 = &m2[(size_t)r * W + (c >> 6)];
-                const uint64_t bit = 1ULL << (c & 63);
-                gf3_add(w1, w2, bit, 0);  /* coefficient += 1 per occurrence */
+        int32_t *tidx = (int32_t *)malloc(cnt * sizeof(int32_t));
+        int32_t *tlow = (int32_t *)malloc(cnt * sizeof(int32_t));
+        int32_t *tstk = (int32_t *)malloc(cnt * sizeof(int32_t));
+        int32_t *cstk = (int32_t *)malloc(cnt * sizeof(int32_t));
+        uint8_t *cpos = (uint8_t *)malloc(cnt);
+        uint8_t *onst = (uint8_t *)calloc(cnt, 1);
+        int32_t *members = (int32_t *)malloc(cnt * sizeof(int32_t));
+        int32_t *col_of = (int32_t *)malloc(cnt * sizeof(int32_t));
+        int fail = 0, counter = 0, sp = 0;
+        for (uint32_t k = 0; k < cnt; k++) { tidx[k] = -1; col_of[k] = -1; }
+        /* successor i (0..2) of core edge k: owner of e_k[i] when that vertex is
+         * another edge's hinge */
+#define BO_SUCC(k, i) ((e[3 * (k) + (i)] != (uint32_t)hinge[k] && vowner[e[3 * (k) + (i)]] >= 0) ? vowner[e[3 * (k) + (i)]] : -1)
+        for (uint32_t r0 = 0; r0 < cnt && !fail; r0++) {
+            if (round_of[r0] >= 0 || tidx[r0] >= 0) continue;
+            int csp = 0;
+            cstk[csp] = (int32_t)r0; cpos[csp] = 0; csp++;
+            tidx[r0] = tlow[r0] = counter++; tstk[sp++] = (int32_t)r0; onst[r0] = 1;
+            while (csp && !fail) {
+                const int32_t k = cstk[csp - 1];
+                if (cpos[csp - 1] < 3) {
+                    const int32_t w = BO_SUCC(k, cpos[csp - 1]);
+                    cpos[csp - 1]++;
+                    if (w < 0) continue;
+                    if (tidx[w] < 0) {
+                        tidx[w] = tlow[w] = counter++; tstk[sp++] = w; onst[w] = 1;
+                        cstk[csp] = w; cpos[csp] = 0; csp++;
+                    } else if (onst[w] && tidx[w] < tlow[k]) {
+                        tlow[k] = tidx[w];
+                    }
+                    continue;
+                }
+                csp--;
+                if (csp && tlow[k] < tlow[cstk[csp - 1]]) tlow[cstk[csp - 1]] = tlow[k];
+                if (tlow[k] != tidx[k]) continue;
+                /* pop one component: members in stack order */
+                int sz = 0;
+                for (;;) {
+                    const int32_t w = tstk[--sp];
+                    onst[w] = 0;
+                    members[sz++] = w;
+                    if (w == k) break;
+                }
+                for (int i = 0; i < sz; i++) col_of[members[i]] = i;
+                /* dense block: rows/cols = members (col i = hinge of members[i]) */
+                const int W = (sz + 1 + 63) / 64;
+                uint64_t *m1 = (uint64_t *)calloc((size_t)sz * W, 8), *m2 = (uint64_t *)calloc((size_t)sz * W, 8);
+                for (int r = 0; r < sz; r++) {
+                    const uint32_t kk = (uint32_t)members[r];
+                    uint32_t rhs_sub = 0;
+                    int h = 0;
+                    while (e[3 * kk + h] != (uint32_t)hinge[kk]) h++;
+                    for (int i = 0; i < 3; i++) {
+                        const uint32_t v = e[3 * kk + i];
+                        const int32_t o = vowner[v];
+                        if (o >= 0 && col_of[o] >= 0) {  /* a hinge of this block */
+                            const int c = col_of[o];
+                            gf3_add(&m1[(size_t)r * W + (c >> 6)], &m2[(size_t)r * W + (c >> 6)], 1ULL << (c & 63), 0);
+                        } else {
+                            rhs_sub += xval[v];
+                        }
+                    }
+                    const uint32_t rhs = ((uint32_t)h + 6 - rhs_sub % 3) % 3;
+                    if (rhs == 1) m1[(size_t)r * W + (sz >> 6)] |= 1ULL << (sz & 63);
+                    if (rhs == 2) m2[(size_t)r * W + (sz >> 6)] |= 1ULL << (sz & 63);
+                }
+                for (int c = 0; c < sz && !fail; c++) {
+                    const int wc = c >> 6;
+                    const uint64_t bit = 1ULL << (c & 63);
+                    int p = c;
+                    while (p < sz && !((m1[(size_t)p * W + wc] | m2[(size_t)p * W + wc]) & bit)) p++;
+                    if (p == sz) { fail = 1; break; }
+                    if (p != c)
+                        for (int w2 = 0; w2 < W; w2++) {
+                            uint64_t t = m1[(size_t)p * W + w2]; m1[(size_t)p * W + w2] = m1[(size_t)c * W + w2]; m1[(size_t)c * W + w2] = t;
+                            t = m2[(size_t)p * W + w2]; m2[(size_t)p * W + w2] = m2[(size_t)c * W + w2]; m2[(size_t)c * W + w2] = t;
+                        }
+                    if (m2[(size_t)c * W + wc] & bit)
+                        for (int w2 = 0; w2 < W; w2++) {
+                            const uint64_t t = m1[(size_t)c * W + w2]; m1[(size_t)c * W + w2] = m2[(size_t)c * W + w2]; m2[(size_t)c * W + w2] = t;
+                        }
+                    for (int r = 0; r < sz; r++) {
+                        if (r == c) continue;
+                        const uint64_t f1 = m1[(size_t)r * W + wc] & bit, f2 = m2[(size_t)r * W + wc] & bit;
+                        if (!f1 && !f2) continue;
+                        for (int w2 = 0; w2 < W; w2++) {
+                            const uint64_t y1 = f1 ? m2[(size_t)c * W + w2] : m1[(size_t)c * W + w2];
+                            const uint64_t y2 = f1 ? m1[(size_t)c * W + w2] : m2[(size_t)c * W + w2];
+                            gf3_add(&m1[(size_t)r * W + w2], &m2[(size_t)r * W + w2], y1, y2);
+                        }
+                    }
+                }
+                if (!fail)
+                    for (int c = 0; c < sz; c++) {
+                        const uint64_t bit = 1ULL << (sz & 63);
+                        const int wn = sz >> 6;
+                        xval[hinge[members[c]]] = (m1[(size_t)c * W + wn] & bit) ? 1 : (m2[(size_t)c * W + wn] & bit) ? 2 : 0;
+                    }
+                for (int i = 0; i < sz; i++) col_of[members[i]] = -1;
+                free(m1); free(m2);
             }
-            int h = 0;
-            while (e[3 * k + h] != (uint32_t)hinge[k]) h++;
-            if (h == 1) m1[(size_t)r * W + (nc >> 6)] |= 1ULL << (nc & 63);
-            if (h == 2) m2[(size_t)r * W + (nc >> 6)] |= 1ULL << (nc & 63);
         }
-        int singular = 0;
-        for (uint32_t c = 0; c < nc && !singular; c++) {
-            const uint32_t wc = c >> 6;
-            const uint64_t bit = 1ULL << (c & 63);
-            uint32_t p = c;
-            while (p < nr && !((m1[(size_t)p * W + wc] | m2[(size_t)p * W + wc]) & bit)) p++;
-            if (p == nr) { singular = 1; break; }
-            if (p != c)
-                for (uint32_t w = 0; w < W; w++) {
-                    uint64_t t = m1[(size_t)p * W + w]; m1[(size_t)p * W + w] = m1[(size_t)c * W + w]; m1[(size_t)c * W + w] = t;
-                    t = m2[(size_t)p * W + w]; m2[(size_t)p * W + w] = m2[(size_t)c * W + w]; m2[(size_t)c * W + w] = t;
-                }
-            if (m2[(size_t)c * W + wc] & bit) /* normalise pivot to 1: multiply row by 2 */
-                for (uint32_t w = 0; w < W; w++) {
-                    const uint64_t t = m1[(size_t)c * W + w]; m1[(size_t)c * W + w] = m2[(size_t)c * W + w]; m2[(size_t)c * W + w] = t;
-                }
-            for (uint32_t r = 0; r < nr; r++) {
-                if (r == c) continue;
-                const uint64_t f1 = m1[(size_t)r * W + wc] & bit, f2 = m2[(size_t)r * W + wc] & bit;
-                if (!f1 && !f2) continue;
-                /* row_r -= f * row_c: f=1 -> add 2*row_c (swapped planes); f=2 -> add row_c */
-                for (uint32_t w = 0; w < W; w++) {
-                    const uint64_t y1 = f1 ? m2[(size_t)c * W + w] : m1[(size_t)c * W + w];
-                    const uint64_t y2 = f1 ? m1[(size_t)c * W + w] : m2[(size_t)c * W + w];
-                    gf3_add(&m1[(size_t)r * W + w], &m2[(size_t)r * W + w], y1, y2);
-                }
-            }
-        }
-        if (!singular)
-            for (uint32_t c = 0; c < nc; c++) {
-                const uint64_t bit = 1ULL << (nc & 63);
-                const uint32_t wn = nc >> 6;
-                xval[cols[c]] = (m1[(size_t)c * W + wn] & bit) ? 1 : (m2[(size_t)c * W + wn] & bit) ? 2 : 0;
-            }
-        free(m1); free(m2); free(col_of); free(cols); free(rows);
-        if (singular) return 1;
+#undef BO_SUCC
+        free(tidx); free(tlow); free(tstk); free(cstk); free(cpos); free(onst); free(members); free(col_of);
+        if (fail) return 1;
     }
     /* 4. peeled edges, last round first */
     for (int r = rounds - 1; r >= 0; r--)
