@@ -18,6 +18,7 @@
 #include "../../include/bsdb_mi355x.h"
 #include "hash_kernels.hip"
 #include "mph_kernels.hip"
+#include "gov_kernels.hip"
 
 using namespace bsdb;
 
@@ -44,6 +45,9 @@ struct bsdb_ctx {
     size_t d_keys_bytes = 0;
     void *d_out = nullptr;
     size_t d_out_bytes = 0;
+    // GOV build workspace
+    void *g_sorted = nullptr, *g_counts = nullptr, *g_cursor = nullptr, *g_scratch = nullptr, *g_status = nullptr;
+    size_t g_sorted_bytes = 0, g_counts_bytes = 0, g_cursor_bytes = 0, g_scratch_bytes = 0, g_status_bytes = 0;
     // live profiling: event pairs per launch, per kind
     bool profiling = false;
     struct Rec { hipEvent_t a, b; int kind; uint64_t keys; };
@@ -309,6 +313,7 @@ const char *bsdb_strerror(int code) {
         case BSDB_ENODEV: return "no such HIP device";
         case BSDB_EDUP: return "duplicate key signature";
         case BSDB_ESEEDS: return "exhausted local seeds";
+        case BSDB_E2BIG: return "bucket too large for the device solver";
         default: return "unknown error";
     }
 }
@@ -350,6 +355,11 @@ int bsdb_close(bsdb_ctx *c) {
     (void)hipFree(c->scan_part);
     (void)hipFree(c->d_keys);
     (void)hipFree(c->d_out);
+    (void)hipFree(c->g_sorted);
+    (void)hipFree(c->g_counts);
+    (void)hipFree(c->g_cursor);
+    (void)hipFree(c->g_scratch);
+    (void)hipFree(c->g_status);
     for (auto &r : c->recs) { (void)hipEventDestroy(r.a); (void)hipEventDestroy(r.b); }
     for (auto e : c->pool) (void)hipEventDestroy(e);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -410,10 +420,16 @@ int bsdb_dev_histogram_var(bsdb_ctx *c, const uint8_t *d_blob, uint64_t blob_byt
     return histogram_impl(c, d_blob, d_off, blob_bytes, 0, n, seed, m, d_counts, pick(c, stream));
 }
 
+static int edge_offsets_impl(bsdb_ctx *c, const uint32_t *d_counts, uint64_t m, uint64_t *d_E, void *stream);
+
 int bsdb_dev_edge_offsets(bsdb_ctx *c, const uint32_t *d_counts, uint64_t m, uint64_t *d_E, void *stream) {
     if (!c || m == 0 || !d_counts || !d_E) return BSDB_EINVAL;
     std::lock_guard<std::mutex> g(c->mu);
     HIP_OK(hipSetDevice(c->device));
+    return edge_offsets_impl(c, d_counts, m, d_E, stream);
+}
+
+static int edge_offsets_impl(bsdb_ctx *c, const uint32_t *d_counts, uint64_t m, uint64_t *d_E, void *stream) {
     const uint64_t nb = (m + SCAN_BLOCK - 1) / SCAN_BLOCK;
     size_t have = c->scan_part_n * sizeof(uint64_t);
     int rc = grow((void **)&c->scan_part, &have, nb * sizeof(uint64_t));
@@ -469,10 +485,60 @@ int bsdb_profile_read(bsdb_ctx *c, int kind, double *total_ms, uint64_t *launche
     return BSDB_OK;
 }
 
-// ---- MPHF evaluation (A11-A13) ----------------------------------------------
 static uint32_t grid_for(const bsdb_ctx *c, uint64_t n) {
     return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((n + 255) / 256, (uint64_t)c->num_cus * 16));
 }
+
+// ---- GOV build on the device (A5, A6, A8, A11) -------------------------------
+uint64_t bsdb_values_words(uint64_t n) { return (2 * (1 + ((n * 281) >> 8)) + 63) / 64; }
+
+int bsdb_dev_gov_build(bsdb_ctx *c, const uint64_t *d_sig, uint64_t n, uint32_t width, uint64_t *d_E,
+                       uint64_t *d_values, uint64_t *d_sigbits, void *stream) {
+    const uint64_t m = n / BUCKET_SIZE + 1;
+    if (!c || width > 64 || !d_E || !d_values || (n && !d_sig) || (width && !d_sigbits) || !aligned16(d_sig) ||
+        m > 0x7FFFFFFFULL)
+        return BSDB_EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    HIP_OK(hipSetDevice(c->device));
+    hipStream_t s = pick(c, stream);
+    const uint32_t mult = (uint32_t)(2 * m);
+    int rc;
+    if ((rc = grow(&c->g_sorted, &c->g_sorted_bytes, std::max<uint64_t>(n, 1) * 16))) return rc;
+    if ((rc = grow(&c->g_counts, &c->g_counts_bytes, m * 4))) return rc;
+    if ((rc = grow(&c->g_cursor, &c->g_cursor_bytes, m * 8))) return rc;
+    if ((rc = grow(&c->g_status, &c->g_status_bytes, 16))) return rc;
+    const uint32_t solve_grid = (uint32_t)std::min<uint64_t>(m, (uint64_t)c->num_cus);
+    if ((rc = grow(&c->g_scratch, &c->g_scratch_bytes, (size_t)solve_grid * 2 * GS_CMAX * GS_WMAX * 8))) return rc;
+    uint32_t *counts = (uint32_t *)c->g_counts, *status = (uint32_t *)c->g_status;
+    HIP_OK(hipMemsetAsync(counts, 0, m * 4, s));
+    HIP_OK(hipMemsetAsync(status, 0, 16, s));
+    HIP_OK(hipMemsetAsync(d_values, 0, bsdb_values_words(n) * 8, s));
+    const uint32_t grid = grid_for(c, n);
+    if (n) k_bucket_count<<<grid, 256, 0, s>>>(d_sig, n, mult, counts);
+    if ((rc = edge_offsets_impl(c, counts, m, d_E, s))) return rc;                 // A6
+    k_cursor_init<<<grid_for(c, m), 256, 0, s>>>(d_E, m, (uint64_t *)c->g_cursor);
+    if (n) k_bucket_scatter<<<grid, 256, 0, s>>>(d_sig, n, mult, (unsigned long long *)c->g_cursor,
+                                                 (uint64_t *)c->g_sorted);
+    k_bucket_sort<<<(uint32_t)std::min<uint64_t>(m, (uint64_t)c->num_cus * 8), 256, 0, s>>>(
+        (uint64_t *)c->g_sorted, d_E, m, status);                                 // A5
+    SolveArgs sa{(const uint64_t *)c->g_sorted, m, d_E, d_values, (uint64_t *)c->g_scratch, status};
+    k_gov_solve<<<solve_grid, GS_THREADS, 0, s>>>(sa);                              // A8
+    if (width) {
+        HIP_OK(hipMemsetAsync(d_sigbits, 0, ((n * width + 63) / 64 + 1) * 8, s));
+        const MphView v{d_E, d_values, nullptr, n, mult, width};
+        if (n) k_sign<<<grid, 256, 0, s>>>(v, (const uint64_t *)c->g_sorted, n, d_sigbits);   // A11
+    }
+    if ((rc = launch_status())) return rc;
+    uint32_t st = 0;
+    HIP_OK(hipMemcpyAsync(&st, status, 4, hipMemcpyDeviceToHost, s));
+    HIP_OK(hipStreamSynchronize(s));
+    if (st & GOV_DUP) return BSDB_EDUP;
+    if (st & GOV_TOO_BIG) return BSDB_E2BIG;
+    if (st & GOV_SEEDS) return BSDB_ESEEDS;
+    return BSDB_OK;
+}
+
+// ---- MPHF evaluation (A11-A13) ----------------------------------------------
 
 int bsdb_dev_lookup(bsdb_ctx *c, const uint64_t *d_sig, uint64_t nq, uint64_t n, uint64_t m, const uint64_t *d_E,
                     const uint64_t *d_values, uint32_t width, const uint64_t *d_sigbits, int check, int64_t *d_out,

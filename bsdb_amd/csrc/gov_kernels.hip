@@ -1,0 +1,525 @@
+// gov_kernels.hip -- GOV MPHF construction on gfx950: bucket sort (A5),
+// per-bucket solve (A8).  One workgroup owns one bucket at a time.
+//
+// The algorithm is the oracle's (oracle/bsdb_oracle.c, "GOV build"), step for
+// step, so the device output is bit-identical to it:
+//   edges   signatureToEquation(sorted sig, j<<56, nv)       (mph.c:63-71)
+//   peel    rounds: every degree-1 vertex claims its edge (smallest wins)
+//   orient  greedy first-free vertex in edge order + BFS augmenting paths
+//           (one lane: sequential by definition, ~1000 edges)
+//   solve   core blocks = SCCs of the hinge dependency graph (Tarjan, one
+//           lane), each block Gauss-Jordan over F3 with the whole workgroup
+//           (bit-sliced rows in a per-workgroup global scratch: a ~900-row
+//           block needs ~250 KB, more than LDS), peeled edges by rounds
+//   store   hinge value or 3 if 0, non-hinge 0 (GOV:126-139); local seed in
+//           the top 8 bits of edgeOffsetAndSeed[b] (GOV:434-436)
+// The reference's own solver (sux4j 5.4.1 Linear3SystemSolver) is not
+// available: its specific solution is parity-unpinned.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "mph_kernels.hip"
+#include "spooky_dev.hpp"
+
+namespace bsdb {
+
+constexpr int GS_THREADS = 256;
+constexpr int GS_CMAX = 2048;    // keys per bucket handled (expected ~1500, sigma ~39)
+constexpr int GS_NVMAX = 2304;   // > vertex_offset span of GS_CMAX keys
+constexpr int GS_TINY = 12;      // brute-force buckets (only in sets of < ~1500 keys)
+constexpr int GS_WMAX = (GS_CMAX + 1 + 63) / 64;  // words per bit-sliced row
+
+enum GovStatus : uint32_t { GOV_TOO_BIG = 1u, GOV_SEEDS = 2u, GOV_DUP = 4u };
+
+// ---- A5: signatures grouped by bucket, sorted by unsigned (sig0, sig1) -------
+__global__ __launch_bounds__(256) void k_bucket_count(const uint64_t *sig, uint64_t n, uint32_t mult, uint32_t *counts) {
+    const uint64_t stride = (uint64_t)gridDim.x * 256;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride)
+        atomicAdd(counts + bucket_of_w(w64(sig[2 * i]), mult), 1u);
+}
+
+__global__ __launch_bounds__(256) void k_cursor_init(const uint64_t *E, uint64_t m, uint64_t *cursor) {
+    const uint64_t stride = (uint64_t)gridDim.x * 256;
+    for (uint64_t b = (uint64_t)blockIdx.x * 256 + threadIdx.x; b < m; b += stride) cursor[b] = E[b] & OFFSET_MASK;
+}
+
+__global__ __launch_bounds__(256) void k_bucket_scatter(const uint64_t *sig, uint64_t n, uint32_t mult,
+                                                        unsigned long long *cursor, uint64_t *out) {
+    const uint64_t stride = (uint64_t)gridDim.x * 256;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
+        const ulonglong2 s = reinterpret_cast<const ulonglong2 *>(sig)[i];
+        const uint64_t pos = atomicAdd(cursor + bucket_of_w(w64(s.x), mult), 1ULL);
+        reinterpret_cast<ulonglong2 *>(out)[pos] = s;
+    }
+}
+
+__device__ __forceinline__ bool sig_less(ulonglong2 a, ulonglong2 b) { return a.x < b.x || (a.x == b.x && a.y < b.y); }
+
+// Bitonic sort of one bucket in LDS (padded with all-ones sentinels) +
+// duplicate check on neighbours (CBHS:969-972).
+__global__ __launch_bounds__(256) void k_bucket_sort(uint64_t *sig, const uint64_t *E, uint64_t m, uint32_t *status) {
+    __shared__ ulonglong2 s[GS_CMAX];
+    for (uint64_t b = blockIdx.x; b < m; b += gridDim.x) {
+        const uint64_t lo = E[b] & OFFSET_MASK, hi = E[b + 1] & OFFSET_MASK;
+        const uint32_t cnt = (uint32_t)(hi - lo);
+        if (cnt > GS_CMAX) {
+            if (threadIdx.x == 0) atomicOr(status, (uint32_t)GOV_TOO_BIG);
+            continue;
+        }
+        uint32_t p2 = 1;
+        while (p2 < cnt) p2 <<= 1;
+        ulonglong2 *g = reinterpret_cast<ulonglong2 *>(sig) + lo;
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < p2; i += 256) s[i] = i < cnt ? g[i] : make_ulonglong2(~0ULL, ~0ULL);
+        __syncthreads();
+        for (uint32_t k = 2; k <= p2; k <<= 1) {
+            for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+                for (uint32_t i = threadIdx.x; i < p2; i += 256) {
+                    const uint32_t l = i ^ j;
+                    if (l > i) {
+                        const ulonglong2 a = s[i], c = s[l];
+                        const bool up = (i & k) == 0;
+                        if (up ? sig_less(c, a) : sig_less(a, c)) {
+                            s[i] = c;
+                            s[l] = a;
+                        }
+                    }
+                }
+                __syncthreads();
+            }
+        }
+        bool dup = false;
+        for (uint32_t i = threadIdx.x; i < cnt; i += 256) {
+            g[i] = s[i];
+            if (i && s[i].x == s[i - 1].x && s[i].y == s[i - 1].y) dup = true;
+        }
+        if (dup) atomicOr(status, (uint32_t)GOV_DUP);
+    }
+}
+
+// ---- A8: per-bucket solve --------------------------------------------------
+struct SolveArgs {
+    const uint64_t *sig;  // sorted signatures
+    uint64_t m;
+    uint64_t *E;          // in: offsets; out: | seed << 56
+    uint64_t *values;     // zeroed 2-bit value array
+    uint64_t *scratch;    // per workgroup: 2 * GS_CMAX * GS_WMAX words
+    uint32_t *status;
+};
+
+struct SolveLds {
+    uint16_t e[3 * GS_CMAX];
+    uint32_t deg[GS_NVMAX];
+    uint32_t xe[GS_NVMAX];
+    uint32_t claim[GS_CMAX];
+    int16_t hinge[GS_CMAX];
+    int16_t round_of[GS_CMAX];
+    int16_t vowner[GS_NVMAX];
+    uint8_t xval[GS_NVMAX];
+    // orientation BFS / Tarjan (not live together)
+    int16_t a0[GS_CMAX], a1[GS_CMAX], a2[GS_CMAX], a3[GS_CMAX];
+    uint8_t b0[GS_NVMAX], b1[GS_CMAX];
+    int16_t members[GS_CMAX];   // components, in emission order
+    int16_t comp_end[GS_CMAX];  // end (exclusive) of component c in members
+    int16_t col_of[GS_CMAX];
+    uint64_t prow[2 * GS_WMAX]; // pivot row
+    uint32_t ncomp, flag, pivot, rounds;
+};
+
+__device__ __forceinline__ void gf3_add(uint64_t &x1, uint64_t &x2, uint64_t y1, uint64_t y2) {
+    const uint64_t a1 = x1, a2 = x2;
+    x1 = (a1 & ~y1 & ~y2) | (~a1 & ~a2 & y1) | (a2 & y2);
+    x2 = (a2 & ~y1 & ~y2) | (~a1 & ~a2 & y2) | (a1 & y1);
+}
+
+// Tries local seed j on bucket (sig, cnt, nv).  Returns (WG-uniform) true on
+// success with L.xval / L.vowner describing the solution.
+__device__ bool try_seed(SolveLds &L, const ulonglong2 *sig, uint32_t cnt, uint32_t nv, uint64_t seed_bits,
+                         uint64_t *scr) {
+    const int tid = threadIdx.x;
+    const bool tiny = cnt <= GS_TINY;
+    if (tid == 0) L.flag = 0;
+    for (uint32_t v = tid; v < nv; v += GS_THREADS) {
+        L.deg[v] = 0;
+        L.xe[v] = 0;
+        L.vowner[v] = -1;
+        L.xval[v] = 0;
+    }
+    __syncthreads();
+    for (uint32_t k = tid; k < cnt; k += GS_THREADS) {
+        const ulonglong2 s = sig[k];
+        uint32_t e[3];
+        sig_to_equation(s.x, s.y, seed_bits, nv, e);
+        if (e[0] == e[1] && e[1] == e[2] && !tiny) L.flag = 1;
+        for (int i = 0; i < 3; ++i) {
+            L.e[3 * k + i] = (uint16_t)e[i];
+            atomicAdd(&L.deg[e[i]], 1u);
+            atomicXor(&L.xe[e[i]], k);
+        }
+        L.hinge[k] = -1;
+        L.round_of[k] = -1;
+    }
+    __syncthreads();
+    if (L.flag) return false;
+    if (cnt == 1 && nv == 1) {
+        if (tid == 0) {
+            L.vowner[0] = 0;
+            L.hinge[0] = 0;
+            L.xval[0] = 0;
+        }
+        __syncthreads();
+        return true;
+    }
+
+    // ---- 1. peeling in rounds
+    int r = 0;
+    for (;; ++r) {
+        for (uint32_t k = tid; k < cnt; k += GS_THREADS) L.claim[k] = 0xFFFFFFFFu;
+        if (tid == 0) L.flag = 0;
+        __syncthreads();
+        for (uint32_t v = tid; v < nv; v += GS_THREADS)
+            if (L.deg[v] == 1) atomicMin(&L.claim[L.xe[v]], v);
+        __syncthreads();
+        for (uint32_t k = tid; k < cnt; k += GS_THREADS) {
+            const uint32_t c = L.claim[k];
+            if (c != 0xFFFFFFFFu) {
+                L.hinge[k] = (int16_t)c;
+                L.vowner[c] = (int16_t)k;
+                L.round_of[k] = (int16_t)r;
+                L.flag = 1;
+            }
+        }
+        __syncthreads();
+        if (!L.flag) break;
+        for (uint32_t k = tid; k < cnt; k += GS_THREADS)
+            if (L.round_of[k] == r)
+                for (int i = 0; i < 3; ++i) {
+                    atomicSub(&L.deg[L.e[3 * k + i]], 1u);
+                    atomicXor(&L.xe[L.e[3 * k + i]], k);
+                }
+        __syncthreads();
+    }
+    const int rounds = r;
+
+    // ---- 2. orientation of the core (lane 0): greedy, then BFS augmenting paths
+    if (tid == 0) {
+        int16_t *bfs_prev = L.a0, *queue = L.a1;
+        uint8_t *seen = L.b0;
+        uint32_t ok = 1;
+        for (uint32_t k = 0; k < cnt; ++k) {
+            if (L.round_of[k] >= 0) continue;
+            for (int i = 0; i < 3; ++i) {
+                const uint32_t v = L.e[3 * k + i];
+                if (L.vowner[v] < 0) {
+                    L.vowner[v] = (int16_t)k;
+                    L.hinge[k] = (int16_t)v;
+                    break;
+                }
+            }
+        }
+        for (uint32_t k0 = 0; k0 < cnt && ok; ++k0) {
+            if (L.round_of[k0] >= 0 || L.hinge[k0] >= 0) continue;
+            for (uint32_t v = 0; v < nv; ++v) seen[v] = 0;
+            int qh = 0, qt = 0, found_v = -1, found_e = -1;
+            queue[qt++] = (int16_t)k0;
+            bfs_prev[k0] = -1;
+            while (qh < qt && found_v < 0) {
+                const int k = queue[qh++];
+                for (int i = 0; i < 3; ++i) {
+                    const uint32_t v = L.e[3 * k + i];
+                    if (seen[v]) continue;
+                    seen[v] = 1;
+                    const int o = L.vowner[v];
+                    if (o < 0) {
+                        found_v = (int)v;
+                        found_e = k;
+                        break;
+                    }
+                    bfs_prev[o] = (int16_t)k;
+                    queue[qt++] = (int16_t)o;
+                }
+            }
+            if (found_v < 0) {
+                ok = 0;
+                break;
+            }
+            int k = found_e, v = found_v;
+            for (;;) {
+                const int old = L.hinge[k];
+                L.hinge[k] = (int16_t)v;
+                L.vowner[v] = (int16_t)k;
+                if (k == (int)k0) break;
+                v = old;
+                k = bfs_prev[k];
+            }
+        }
+        L.flag = ok;
+    }
+    __syncthreads();
+    if (!L.flag) return false;
+
+    // ---- tiny buckets: first satisfying assignment in base-3 order (lane 0)
+    if (tiny) {
+        if (tid == 0) {
+            uint32_t total = 1;
+            for (uint32_t k = 0; k < cnt; ++k) total *= 3;
+            uint32_t found = 0;
+            for (uint32_t a = 0; a < total && !found; ++a) {
+                uint32_t t = a;
+                for (uint32_t k = 0; k < cnt; ++k) {
+                    L.xval[L.hinge[k]] = (uint8_t)(t % 3);
+                    t /= 3;
+                }
+                uint32_t okk = 1;
+                for (uint32_t k = 0; k < cnt && okk; ++k) {
+                    int h = 0;
+                    while (L.e[3 * k + h] != (uint32_t)L.hinge[k]) ++h;
+                    const uint32_t sum = L.xval[L.e[3 * k]] + L.xval[L.e[3 * k + 1]] + L.xval[L.e[3 * k + 2]];
+                    okk = sum % 3 == (uint32_t)h;
+                }
+                found = okk;
+            }
+            L.flag = found;
+        }
+        __syncthreads();
+        return L.flag != 0;
+    }
+
+    // ---- 3a. SCCs of the core dependency graph (lane 0, iterative Tarjan)
+    if (tid == 0) {
+        int16_t *tidx = L.a0, *tlow = L.a1, *tstk = L.a2, *cstk = L.a3;
+        uint8_t *onst = L.b0, *cpos = L.b1;
+        for (uint32_t k = 0; k < cnt; ++k) {
+            tidx[k] = -1;
+            L.col_of[k] = -1;
+            onst[k] = 0;
+        }
+        int counter = 0, sp = 0, nm = 0, nc = 0;
+        for (uint32_t r0 = 0; r0 < cnt; ++r0) {
+            if (L.round_of[r0] >= 0 || tidx[r0] >= 0) continue;
+            int csp = 0;
+            cstk[csp] = (int16_t)r0;
+            cpos[csp] = 0;
+            ++csp;
+            tidx[r0] = tlow[r0] = (int16_t)counter++;
+            tstk[sp++] = (int16_t)r0;
+            onst[r0] = 1;
+            while (csp) {
+                const int k = cstk[csp - 1];
+                if (cpos[csp - 1] < 3) {
+                    const uint32_t v = L.e[3 * k + cpos[csp - 1]];
+                    ++cpos[csp - 1];
+                    const int w = (v != (uint32_t)L.hinge[k]) ? L.vowner[v] : -1;
+                    if (w < 0) continue;
+                    if (tidx[w] < 0) {
+                        tidx[w] = tlow[w] = (int16_t)counter++;
+                        tstk[sp++] = (int16_t)w;
+                        onst[w] = 1;
+                        cstk[csp] = (int16_t)w;
+                        cpos[csp] = 0;
+                        ++csp;
+                    } else if (onst[w] && tidx[w] < tlow[k]) {
+                        tlow[k] = tidx[w];
+                    }
+                    continue;
+                }
+                --csp;
+                if (csp && tlow[k] < tlow[cstk[csp - 1]]) tlow[cstk[csp - 1]] = tlow[k];
+                if (tlow[k] != tidx[k]) continue;
+                for (;;) {
+                    const int w = tstk[--sp];
+                    onst[w] = 0;
+                    L.members[nm++] = (int16_t)w;
+                    if (w == k) break;
+                }
+                L.comp_end[nc++] = (int16_t)nm;
+            }
+        }
+        L.ncomp = (uint32_t)nc;
+    }
+    __syncthreads();
+
+    // ---- 3b. blocks in emission order: singletons on lane 0, blocks with the WG
+    const uint32_t ncomp = L.ncomp;
+    uint32_t c = 0;
+    while (c < ncomp) {
+        if (tid == 0) {
+            // run of singletons
+            while (c < ncomp) {
+                const int beg = c ? L.comp_end[c - 1] : 0;
+                if (L.comp_end[c] - beg != 1) break;
+                const int k = L.members[beg];
+                int h = 0;
+                while (L.e[3 * k + h] != (uint32_t)L.hinge[k]) ++h;
+                uint32_t s = 0, coef = 0;
+                for (int i = 0; i < 3; ++i) {
+                    if (L.e[3 * k + i] == (uint32_t)L.hinge[k]) ++coef;
+                    else s += L.xval[L.e[3 * k + i]];
+                }
+                const uint32_t rhs = ((uint32_t)h + 6 - s % 3) % 3;
+                if (coef % 3 == 0) {
+                    L.flag = 0;  // singular singleton (cannot happen: triple edges rejected)
+                    c = ncomp;
+                    break;
+                }
+                L.xval[L.hinge[k]] = (uint8_t)(coef == 1 ? rhs : (2 * rhs) % 3);
+                ++c;
+            }
+            L.pivot = c;
+        }
+        __syncthreads();
+        c = L.pivot;
+        if (c >= ncomp) break;
+        // dense block c
+        const uint32_t beg = c ? (uint32_t)L.comp_end[c - 1] : 0;
+        const uint32_t sz = (uint32_t)L.comp_end[c] - beg;
+        const uint32_t W = (sz + 1 + 63) / 64;
+        for (uint32_t i = tid; i < sz; i += GS_THREADS) L.col_of[L.members[beg + i]] = (int16_t)i;
+        __syncthreads();
+        for (uint32_t rr = tid; rr < sz; rr += GS_THREADS) {
+            uint64_t *r1 = scr + (size_t)rr * 2 * W, *r2 = r1 + W;
+            for (uint32_t w = 0; w < W; ++w) r1[w] = r2[w] = 0;
+            const int k = L.members[beg + rr];
+            int h = 0;
+            while (L.e[3 * k + h] != (uint32_t)L.hinge[k]) ++h;
+            uint32_t sub = 0;
+            for (int i = 0; i < 3; ++i) {
+                const uint32_t v = L.e[3 * k + i];
+                const int o = L.vowner[v];
+                if (o >= 0 && L.col_of[o] >= 0) {
+                    const uint32_t cc = (uint32_t)L.col_of[o];
+                    gf3_add(r1[cc >> 6], r2[cc >> 6], 1ULL << (cc & 63), 0);
+                } else {
+                    sub += L.xval[v];
+                }
+            }
+            const uint32_t rhs = ((uint32_t)h + 6 - sub % 3) % 3;
+            if (rhs == 1) r1[sz >> 6] |= 1ULL << (sz & 63);
+            if (rhs == 2) r2[sz >> 6] |= 1ULL << (sz & 63);
+        }
+        if (tid == 0) L.flag = 1;
+        __threadfence_block();
+        __syncthreads();
+        for (uint32_t cc = 0; cc < sz; ++cc) {
+            const uint32_t wc = cc >> 6;
+            const uint64_t bit = 1ULL << (cc & 63);
+            if (tid == 0) L.pivot = 0xFFFFFFFFu;
+            __syncthreads();
+            for (uint32_t rr = cc + tid; rr < sz; rr += GS_THREADS) {
+                const uint64_t *r1 = scr + (size_t)rr * 2 * W;
+                if ((r1[wc] | r1[W + wc]) & bit) {
+                    atomicMin(&L.pivot, rr);
+                    break;
+                }
+            }
+            __syncthreads();
+            const uint32_t p = L.pivot;
+            if (p == 0xFFFFFFFFu) {
+                if (tid == 0) L.flag = 0;
+                __syncthreads();
+                break;
+            }
+            // pivot row -> LDS (normalised to coefficient 1), then swap rows p and cc
+            {
+                uint64_t *rp = scr + (size_t)p * 2 * W, *rc = scr + (size_t)cc * 2 * W;
+                const bool two = (rp[W + wc] & bit) != 0;
+                for (uint32_t w = tid; w < W; w += GS_THREADS) {
+                    const uint64_t p1 = rp[w], p2 = rp[W + w];
+                    L.prow[w] = two ? p2 : p1;
+                    L.prow[W + w] = two ? p1 : p2;
+                }
+                __syncthreads();
+                if (p != cc)
+                    for (uint32_t w = tid; w < 2 * W; w += GS_THREADS) rp[w] = rc[w];
+                __syncthreads();
+                for (uint32_t w = tid; w < 2 * W; w += GS_THREADS) rc[w] = L.prow[w];
+                __syncthreads();
+            }
+            for (uint32_t rr = tid; rr < sz; rr += GS_THREADS) {
+                if (rr == cc) continue;
+                uint64_t *r1 = scr + (size_t)rr * 2 * W, *r2 = r1 + W;
+                const uint64_t f1 = r1[wc] & bit, f2 = r2[wc] & bit;
+                if (!f1 && !f2) continue;
+                for (uint32_t w = 0; w < W; ++w) {
+                    const uint64_t y1 = f1 ? L.prow[W + w] : L.prow[w];
+                    const uint64_t y2 = f1 ? L.prow[w] : L.prow[W + w];
+                    gf3_add(r1[w], r2[w], y1, y2);
+                }
+            }
+            __syncthreads();
+        }
+        if (!L.flag) return false;
+        for (uint32_t i = tid; i < sz; i += GS_THREADS) {
+            const uint64_t *r1 = scr + (size_t)i * 2 * W;
+            const uint64_t bit = 1ULL << (sz & 63);
+            L.xval[L.hinge[L.members[beg + i]]] = (r1[sz >> 6] & bit) ? 1 : (r1[W + (sz >> 6)] & bit) ? 2 : 0;
+        }
+        for (uint32_t i = tid; i < sz; i += GS_THREADS) L.col_of[L.members[beg + i]] = -1;
+        __syncthreads();
+        ++c;
+    }
+    if (!L.flag) return false;
+
+    // ---- 4. peeled edges, last round first
+    for (int rr = rounds - 1; rr >= 0; --rr) {
+        for (uint32_t k = tid; k < cnt; k += GS_THREADS) {
+            if (L.round_of[k] != rr) continue;
+            int h = 0;
+            while (L.e[3 * k + h] != (uint32_t)L.hinge[k]) ++h;
+            uint32_t s = 0, coef = 0;
+            for (int i = 0; i < 3; ++i) {
+                if (L.e[3 * k + i] == (uint32_t)L.hinge[k]) ++coef;
+                else s += L.xval[L.e[3 * k + i]];
+            }
+            const uint32_t rhs = ((uint32_t)h + 6 - s) % 3;
+            L.xval[L.hinge[k]] = (uint8_t)(coef == 1 ? rhs : (2 * rhs) % 3);
+        }
+        __syncthreads();
+    }
+    return true;
+}
+
+__global__ __launch_bounds__(GS_THREADS) void k_gov_solve(SolveArgs a) {
+    __shared__ SolveLds L;
+    uint64_t *scr = a.scratch + (size_t)blockIdx.x * 2 * GS_CMAX * GS_WMAX;
+    for (uint64_t b = blockIdx.x; b < a.m; b += gridDim.x) {
+        const uint64_t lo = a.E[b] & OFFSET_MASK, hi = a.E[b + 1] & OFFSET_MASK;
+        const uint32_t cnt = (uint32_t)(hi - lo);
+        const uint64_t vo = vertex_offset(lo);
+        const uint32_t nv = (uint32_t)(vertex_offset(hi) - vo);
+        if (cnt == 0) continue;
+        if (cnt > GS_CMAX || nv > GS_NVMAX) {
+            if (threadIdx.x == 0) atomicOr(a.status, (uint32_t)GOV_TOO_BIG);
+            continue;
+        }
+        const ulonglong2 *sig = reinterpret_cast<const ulonglong2 *>(a.sig) + lo;
+        uint32_t j = 0;
+        for (; j < 256; ++j)
+            if (try_seed(L, sig, cnt, nv, (uint64_t)j << 56, scr)) break;
+        if (j == 256) {
+            if (threadIdx.x == 0) atomicOr(a.status, (uint32_t)GOV_SEEDS);
+            continue;
+        }
+        // values: hinge -> xval or 3, other vertices 0; words shared with the
+        // neighbouring buckets are OR-ed
+        const uint64_t w0 = vo >> 5, w1 = (vo + nv + 31) >> 5;
+        for (uint64_t w = w0 + threadIdx.x; w < w1; w += GS_THREADS) {
+            uint64_t word = 0;
+            for (uint32_t t = 0; t < 32; ++t) {
+                const uint64_t pos = w * 32 + t;
+                if (pos < vo || pos >= vo + nv) continue;
+                const uint32_t v = (uint32_t)(pos - vo);
+                const uint32_t val = L.vowner[v] >= 0 ? (L.xval[v] ? L.xval[v] : 3u) : 0u;
+                word |= (uint64_t)val << (2 * t);
+            }
+            const bool inner = w * 32 >= vo && (w + 1) * 32 <= vo + nv;
+            if (inner) a.values[w] = word;
+            else if (word) atomicOr((unsigned long long *)(a.values + w), (unsigned long long)word);
+        }
+        if (threadIdx.x == 0) a.E[b] |= (uint64_t)j << 56;
+        __syncthreads();
+    }
+}
+
+}  // namespace bsdb

@@ -19,7 +19,7 @@ LIB_PATH = os.path.join(HERE, "libbsdb_mi355x.so")
 HEADER = os.path.join(os.path.dirname(HERE), "include", "bsdb_mi355x.h")
 
 BSDB_OK = 0
-ERRORS = {-22: "EINVAL", -12: "ENOMEM", -5: "EIO", -19: "ENODEV", -17: "EDUP", -34: "ESEEDS"}
+ERRORS = {-22: "EINVAL", -12: "ENOMEM", -5: "EIO", -19: "ENODEV", -17: "EDUP", -34: "ESEEDS", -7: "E2BIG"}
 
 # (name, restype, argtypes) -- kept in the order of include/bsdb_mi355x.h
 _vp, _u64, _u32, _i = C.c_void_p, C.c_uint64, C.c_uint32, C.c_int
@@ -37,6 +37,8 @@ SIGNATURES = [
     ("bsdb_dev_lookup", _i, [_vp, _vp, _u64, _u64, _u64, _vp, _vp, _u32, _vp, _i, _vp, _vp]),
     ("bsdb_dev_sign", _i, [_vp, _vp, _u64, _u64, _vp, _vp, _u32, _vp, _vp]),
     ("bsdb_dev_index_scatter", _i, [_vp, _vp, _vp, _u64, _u64, _u64, _vp, _vp, _vp, _vp, _vp]),
+    ("bsdb_values_words", _u64, [_u64]),
+    ("bsdb_dev_gov_build", _i, [_vp, _vp, _u64, _u32, _vp, _vp, _vp, _vp]),
     ("bsdb_set_histogram_mode", _i, [_vp, _i]),
     ("bsdb_set_frontend", _i, [_vp, _i]),
     ("bsdb_set_chunk_keys", _i, [_vp, _u64]),
@@ -193,6 +195,19 @@ class Context:
         _check("bsdb_dev_edge_offsets", lib().bsdb_dev_edge_offsets(
             self._h, _ptr(counts), m, _ptr(out), _stream(stream)))
         return out
+
+    # ---- A5/A6/A8/A11: GOV build on the device
+    def gov_build(self, sig, width: int, stream=None):
+        import torch
+        n = sig.shape[0]
+        m = n // 1500 + 1
+        E = torch.empty(m + 1, dtype=torch.int64, device=sig.device)
+        values = torch.empty(int(lib().bsdb_values_words(n)), dtype=torch.int64, device=sig.device)
+        sigbits = torch.empty((n * width + 63) // 64 + 1, dtype=torch.int64, device=sig.device) if width else None
+        _check("bsdb_dev_gov_build", lib().bsdb_dev_gov_build(
+            self._h, _ptr(sig), n, width, _ptr(E), _ptr(values), _ptr(sigbits) if sigbits is not None else None,
+            _stream(stream)))
+        return E, values, sigbits
 
     # ---- A11-A13: MPHF evaluation over (E, values[, checksum bits])
     def lookup(self, sig, n: int, E, values, width: int = 0, sigbits=None, check: bool = True, out=None,

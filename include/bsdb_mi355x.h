@@ -115,6 +115,22 @@ int bsdb_dev_index_scatter(bsdb_ctx *ctx, const int64_t *d_rank, const uint64_t 
                            uint64_t start, uint64_t len, uint64_t *d_index, const uint64_t *d_value8,
                            const uint8_t *d_value_len, uint8_t *d_index_a, void *stream);
 
+/* ---------------------------------------------------------------------------
+ * A5 + A6 + A8 + A11 on the device: GOV MPHF over n signatures (any order).
+ * Buckets are sorted by unsigned (sig0, sig1) (CBHS:939-955), duplicates
+ * rejected (BSDB_EDUP, CBHS:969-972), every bucket solved with local seeds
+ * 0..255 (BSDB_ESEEDS when exhausted, GOV:431), values written with 3 for a
+ * zero hinge (GOV:126-139), and, for width > 0, the checksum list signed
+ * (GOV:492-508).  Outputs: d_E[num_buckets+1], d_values[bsdb_values_words(n)],
+ * d_sigbits[(n*width+63)/64 + 1] (zeroed here).  The solution choice is this
+ * project's deterministic solver (bit-identical to oracle/bo_gov_build), not
+ * sux4j's; synchronous (returns after the device finished).
+ * ------------------------------------------------------------------------- */
+#define BSDB_E2BIG     (-7)   /* a bucket holds more keys than the solver supports */
+uint64_t bsdb_values_words(uint64_t n);
+int bsdb_dev_gov_build(bsdb_ctx *ctx, const uint64_t *d_sig, uint64_t n, uint32_t width, uint64_t *d_E,
+                       uint64_t *d_values, uint64_t *d_sigbits, void *stream);
+
 /* Histogram path selection for bsdb_dev_histogram_* (benchmarks/tests):
  *   0 = auto (partitioned two-pass), 1 = partitioned two-pass, 2 = direct atomics. */
 int bsdb_set_histogram_mode(bsdb_ctx *ctx, int mode);

@@ -280,3 +280,69 @@ def test_index_scatter(ctx, approx):
         np.testing.assert_array_equal(idx.cpu().numpy().view(np.uint64), want)
         if approx:
             np.testing.assert_array_equal(ia.cpu().numpy(), want_a)
+
+
+# ---------------------------------------------------------------- A5/A6/A8/A11 device build
+def _rand_sigs(n, seed):
+    return np.random.default_rng(seed).integers(0, 2**63, size=(n, 2), dtype=np.int64).view(np.uint64) * np.uint64(2) \
+        + np.random.default_rng(seed + 1).integers(0, 2, size=(n, 2), dtype=np.int64).view(np.uint64)
+
+
+@pytest.mark.parametrize("n,width", [(1, 0), (2, 8), (9, 0), (10, 16), (12, 3), (39, 64), (777, 5),
+                                     (1500, 0), (1501, 12), (3000, 1), (20_000, 4), (150_000, 32)])
+def test_gov_build_matches_oracle(ctx, n, width):
+    """Device GOV build (sort, E, solve, sign) is bit-identical to oracle/bo_gov_build."""
+    sig = _rand_sigs(n, n * 7 + width)
+    rc, E, values, sigbits = O.gov_build(sig, width)
+    assert rc == 0
+    dE, dv, dsb = ctx.gov_build(dev(sig.view(np.int64)), width)
+    np.testing.assert_array_equal(dE.cpu().numpy().view(np.uint64), E)
+    np.testing.assert_array_equal(dv.cpu().numpy().view(np.uint64), values)
+    if width:
+        np.testing.assert_array_equal(dsb.cpu().numpy().view(np.uint64), sigbits)
+    got = ctx.lookup(dev(sig.view(np.int64)), n, dE, dv, width, dsb, check=True).cpu().numpy()
+    assert np.array_equal(np.sort(got), np.arange(n))
+
+
+def test_gov_build_string_keys_and_order_independence(ctx):
+    """NativeTest-style keys; the device sorts, so input order does not matter (CBHS:939-955)."""
+    n = 60_000
+    sig, E, values, sigbits = _gov_set(n, 10)
+    perm = np.random.default_rng(3).permutation(n)
+    for s in (sig, sig[perm]):
+        dE, dv, dsb = ctx.gov_build(dev(np.ascontiguousarray(s).view(np.int64)), 10)
+        np.testing.assert_array_equal(dE.cpu().numpy().view(np.uint64), E)
+        np.testing.assert_array_equal(dv.cpu().numpy().view(np.uint64), values)
+        np.testing.assert_array_equal(dsb.cpu().numpy().view(np.uint64), sigbits)
+
+
+def test_gov_build_empty(ctx):
+    rc, E, values, _ = O.gov_build(np.zeros((0, 2), np.uint64), 0)
+    dE, dv, _ = ctx.gov_build(torch.zeros((0, 2), dtype=torch.int64, device="cuda"), 0)
+    np.testing.assert_array_equal(dE.cpu().numpy().view(np.uint64), E)
+    np.testing.assert_array_equal(dv.cpu().numpy().view(np.uint64), values)
+
+
+def test_gov_build_duplicate_rejected(ctx):
+    """Duplicate signatures -> BSDB_EDUP (CBHS:969-972 DuplicateException)."""
+    sig = _rand_sigs(5000, 99)
+    sig[4321] = sig[17]
+    with pytest.raises(Exception, match="EDUP"):
+        ctx.gov_build(dev(sig.view(np.int64)), 0)
+
+
+def test_gov_build_large_valid(ctx):
+    """2 M keys: sizes the oracle is slow on; checked by the bijection + checksum properties."""
+    n = 2_000_000
+    sig = _rand_sigs(n, 2024)
+    dsig = dev(sig.view(np.int64))
+    dE, dv, dsb = ctx.gov_build(dsig, 8)
+    assert int(dE[-1]) & ((1 << 56) - 1) == n
+    got = ctx.lookup(dsig, n, dE, dv, 8, dsb, check=True)
+    assert torch.equal(torch.sort(got).values, torch.arange(n, device="cuda"))
+    # a sample of buckets against the oracle's per-bucket lookup on the device-built structure
+    idx = np.arange(0, n, 997)
+    np.testing.assert_array_equal(got.cpu().numpy()[idx],
+                                  O.lookup_batch(sig[idx], n, dE.cpu().numpy().view(np.uint64),
+                                                 dv.cpu().numpy().view(np.uint64), 8,
+                                                 dsb.cpu().numpy().view(np.uint64)))
