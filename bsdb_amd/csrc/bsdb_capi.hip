@@ -127,8 +127,10 @@ void launch_pass1(const P1Args &a0, bool var, uint32_t key_len, uint64_t tiles, 
     }
     const P1Args &a = a0;
     const dim3 g((uint32_t)tiles), b(P1_THREADS);
-    if (var) {
+    if (var && frontend == 2) {
         k_pass1<SRC_VAR, EPI, 1, 0><<<g, b, 0, s>>>(a);
+    } else if (var) {
+        k_pass1<SRC_VARSTAGED, EPI, 1, 0><<<g, b, 0, s>>>(a);
     } else if (key_len == 13 && frontend != 1) {
         k_pass1<SRC_DIRECT13, EPI, 4, 13><<<g, b, 0, s>>>(a);
     } else if (key_len == 13) {
@@ -450,6 +452,30 @@ int bsdb_dev_gen_keys13(bsdb_ctx *c, uint64_t first, uint64_t n, uint8_t *d_keys
     if (n == 0) return BSDB_OK;
     const uint64_t blocks = std::min<uint64_t>((n + 255) / 256, (uint64_t)c->num_cus * 64);
     k_gen_keys13<<<(uint32_t)blocks, 256, 0, pick(c, stream)>>>(first, n, d_keys);
+    return launch_status();
+}
+
+int bsdb_dev_gen_keys_var(bsdb_ctx *c, uint64_t first, uint64_t n, uint64_t *d_offsets, uint8_t *d_blob,
+                          uint64_t blob_cap, void *stream) {
+    if (!c || !d_offsets) return BSDB_EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    HIP_OK(hipSetDevice(c->device));
+    hipStream_t s = pick(c, stream);
+    if (n == 0) {
+        HIP_OK(hipMemsetAsync(d_offsets, 0, 8, s));
+        return launch_status();
+    }
+    int rc = grow(&c->g_counts, &c->g_counts_bytes, n * 4);
+    if (rc) return rc;
+    const uint32_t blocks = (uint32_t)std::min<uint64_t>((n + 255) / 256, (uint64_t)c->num_cus * 64);
+    k_gen_var_len<<<blocks, 256, 0, s>>>(first, n, (uint32_t *)c->g_counts);
+    if ((rc = edge_offsets_impl(c, (const uint32_t *)c->g_counts, n, d_offsets, s))) return rc;
+    if (!d_blob) return launch_status();
+    uint64_t total = 0;
+    HIP_OK(hipMemcpyAsync(&total, d_offsets + n, 8, hipMemcpyDeviceToHost, s));
+    HIP_OK(hipStreamSynchronize(s));
+    if (total > blob_cap) return BSDB_EINVAL;
+    k_gen_var_fill<<<blocks, 256, 0, s>>>(first, n, d_offsets, d_blob);
     return launch_status();
 }
 

@@ -31,7 +31,7 @@ constexpr int NCOPY = 8;                                  // cursor/region copie
 constexpr int P2_THREADS = 1024;
 
 enum Epi { EPI_PARTITION = 0, EPI_ATOMIC = 1, EPI_SIG = 2 };
-enum Src { SRC_STAGED13 = 0, SRC_STAGED = 1, SRC_FIXED_DIRECT = 2, SRC_VAR = 3, SRC_DIRECT13 = 4 };
+enum Src { SRC_STAGED13 = 0, SRC_STAGED = 1, SRC_FIXED_DIRECT = 2, SRC_VAR = 3, SRC_DIRECT13 = 4, SRC_VARSTAGED = 5 };
 
 struct P1Args {
     const uint8_t *keys;      // fixed: n*key_len bytes; var: blob
@@ -292,6 +292,57 @@ __global__ __launch_bounds__(P1_THREADS, 4) void k_pass1(P1Args a) {
                     emit(kt, tile0 + kt, s0, s1);
                 }
             }
+        }
+    } else if (SRC == SRC_VARSTAGED) {
+        // variable-length keys, LDS-staged: sub-tile s = keys [512s, 512s+512)
+        // of the tile; its byte range [off[k0], off[k0+cnt]) (rounded down to
+        // 16 B) is copied into LDS with coalesced 16-byte loads, the next
+        // sub-tile's range prefetched into registers while this one hashes.
+        // A sub-tile longer than the stage (mean key > ~63 B) is hashed from
+        // global memory instead (uniform branch).
+        constexpr uint64_t STAGE_CAP = (uint64_t)UNION_WORDS * 4 - 16;
+        auto range = [&](int s, uint64_t &lo, uint64_t &nb) {
+            const uint32_t k0 = (uint32_t)s * P1_THREADS;
+            if (k0 >= tile_n) { lo = 0; nb = 0; return; }
+            const uint32_t cnt = min((uint32_t)P1_THREADS, tile_n - k0);
+            lo = a.offsets[tile0 + k0] & ~15ULL;
+            nb = a.offsets[tile0 + k0 + cnt] - lo;
+        };
+        uint64_t lo, nb, nlo, nnb;
+        range(0, lo, nb);
+        StageRegs pre;
+        if (nb <= STAGE_CAP) stage_load(pre, a.keys + lo, nb, tid);
+        if (EPI == EPI_PARTITION) __syncthreads();  // hist zeroed
+        for (int s = 0; s < P1_KEYS_PER_THREAD; ++s) {
+            if ((uint32_t)s * P1_THREADS >= tile_n) break;
+            const bool staged = nb <= STAGE_CAP;
+            if (s) __syncthreads();  // all reads of the previous sub-tile done
+            if (staged) stage_store(pre, stage, nb, tid);
+            __syncthreads();
+            range(s + 1, nlo, nnb);
+            if (s + 1 < P1_KEYS_PER_THREAD && nnb <= STAGE_CAP) stage_load(pre, a.keys + nlo, nnb, tid);
+            const uint32_t kt = s * P1_THREADS + tid;
+            if (kt < tile_n) {
+                const uint64_t gk = tile0 + kt;
+                const uint64_t pos = a.offsets[gk];
+                const uint32_t len = (uint32_t)(a.offsets[gk + 1] - pos);
+                uint64_t s0, s1;
+                if (staged) {
+                    const uint32_t o = (uint32_t)(pos - lo);
+                    auto rd = [&](uint32_t off) -> uint64_t {
+                        const uint32_t p = o + off;
+                        const uint32_t *q = stage + (p >> 2);
+                        return funnel64(q[0], q[1], q[2], (p & 3) * 8);
+                    };
+                    spooky_short(rd, len, a.seed, s0, s1);
+                } else {
+                    auto rd = [&](uint32_t off) -> uint64_t { return gload64(a.keys, a.blob_bytes, pos + off); };
+                    spooky_short(rd, len, a.seed, s0, s1);
+                }
+                emit(kt, gk, s0, s1);
+            }
+            lo = nlo;
+            nb = nnb;
         }
     } else {
         // direct global reads: long fixed keys (L > 52) and variable-length keys
@@ -638,6 +689,38 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan_final(const uint32_t *cou
     for (int j = 0; j < SCAN_PER_THREAD; ++j) {
         run += c[j];
         if (i0 + j < m) E[i0 + j + 1] = run;
+    }
+}
+
+// key i has length 8 + r, r drawn Zipf(s=1.1)
+// over the 57 lengths 8..64 (rank 1 = length 8) by inverse CDF on
+// u = splitmix64(i ^ 0xB5DB0005); bytes 0-7 = i big-endian (BaseTest.java:16-24),
+// tail word w (bytes 8+8w..) = splitmix64(((i << 3) + w) ^ 0xB5DB0005A5A5A5A5)
+// little-endian.  Thresholds = floor(CDF(r) * 2^64), r = 1..56.
+__constant__ uint64_t ZIPF_CDF[56] = {0x415ff50621eab000ULL, 0x5fdf8ea4661c1800ULL, 0x7365cc48cd422800ULL, 0x81a02c160ca0d800ULL, 0x8cc1c51827e0f000ULL, 0x95dd881c0eabb000ULL, 0x9d8d9c8bd387d800ULL, 0xa430d6d3c06da800ULL, 0xaa0593efa19cb800ULL, 0xaf36f652f272a000ULL, 0xb3e4079390b42800ULL, 0xb823d5bdeb558000ULL, 0xbc07f52bb16ae800ULL, 0xbf9e197287e21000ULL, 0xc2f123c939aa0800ULL, 0xc609db869ad6f800ULL, 0xc8ef6f73a3a9d800ULL, 0xcba7d2952de20000ULL, 0xce38001f766e2000ULL, 0xd0a42e21797a3800ULL, 0xd2eff3ea03b6c000ULL, 0xd51e678ba501e800ULL, 0xd73234d900b38000ULL, 0xd92daf816c491000ULL, 0xdb12e17da86ff800ULL, 0xdce396a9b5e6c000ULL, 0xdea1662ec6fe5800ULL, 0xe04dba370d317800ULL, 0xe1e9d64761753000ULL, 0xe376dc8509ffe800ULL, 0xe4f5d21dcfad2800ULL, 0xe667a2fc93d9d000ULL, 0xe7cd24eb876f7000ULL, 0xe9271a3e3b92e800ULL, 0xea76341874c6f000ULL, 0xebbb14628b26f800ULL, 0xecf64f78eaa7d000ULL, 0xee286da1bdeba000ULL, 0xef51ec51cc50e000ULL, 0xf0733f47f9ee2000ULL, 0xf18cd1858f189800ULL, 0xf29f062863636800ULL, 0xf3aa392b30515800ULL, 0xf4aec00f9fea5000ULL, 0xf5acea751b007800ULL, 0xf6a5029ee3f44800ULL, 0xf7974deba8448800ULL, 0xf8840d40614fb000ULL, 0xf96b7d68184c6800ULL, 0xfa4dd769e82e0000ULL, 0xfb2b50d667f27000ULL, 0xfc041c0d7f209800ULL, 0xfcd8687d83bcc000ULL, 0xfda862dc63a64800ULL, 0xfe74355b824d6000ULL, 0xff3c07d6de49e800ULL};
+
+__device__ __forceinline__ uint32_t varkey_len(uint64_t i) {
+    const uint64_t u = splitmix64(i ^ 0xB5DB0005ULL);
+    uint32_t r = 0;
+#pragma unroll 8
+    for (int t = 0; t < 56; ++t) r += u >= ZIPF_CDF[t];
+    return 8 + r;
+}
+
+__global__ __launch_bounds__(256) void k_gen_var_len(uint64_t first, uint64_t n, uint32_t *len) {
+    for (uint64_t k = (uint64_t)blockIdx.x * 256 + threadIdx.x; k < n; k += (uint64_t)gridDim.x * 256)
+        len[k] = varkey_len(first + k);
+}
+
+__global__ __launch_bounds__(256) void k_gen_var_fill(uint64_t first, uint64_t n, const uint64_t *off, uint8_t *blob) {
+    for (uint64_t k = (uint64_t)blockIdx.x * 256 + threadIdx.x; k < n; k += (uint64_t)gridDim.x * 256) {
+        const uint64_t i = first + k, p = off[k];
+        const uint32_t len = (uint32_t)(off[k + 1] - p);
+        for (int b = 0; b < 8; ++b) blob[p + b] = (uint8_t)(i >> (56 - 8 * b));
+        for (uint32_t j = 8; j < len; j += 8) {
+            const uint64_t w = splitmix64(((i << 3) + ((j - 8) >> 3)) ^ 0xB5DB0005A5A5A5A5ULL);
+            for (uint32_t b = 0; b < 8 && j + b < len; ++b) blob[p + j + b] = (uint8_t)(w >> (8 * b));
+        }
     }
 }
 

@@ -47,6 +47,7 @@ SIGNATURES = [
     ("bsdb_histogram_fixed", _i, [_vp, _vp, _u32, _u64, _u64, _u64, _vp]),
     ("bsdb_hash_fixed", _i, [_vp, _vp, _u32, _u64, _u64, _vp]),
     ("bsdb_dev_gen_keys13", _i, [_vp, _u64, _u64, _vp, _vp]),
+    ("bsdb_dev_gen_keys_var", _i, [_vp, _u64, _u64, _vp, _vp, _u64, _vp]),
 ]
 
 HIST_AUTO, HIST_PARTITIONED, HIST_ATOMIC = 0, 1, 2
@@ -236,6 +237,18 @@ class Context:
             self._h, _ptr(rank), _ptr(addr), rank.numel(), start, length, _ptr(index),
             _ptr(value8) if value8 is not None else None, _ptr(value_len) if value_len is not None else None,
             _ptr(index_a) if index_a is not None else None, _stream(stream)))
+
+    def gen_keys_var(self, first: int, n: int, stream=None):
+        """Config C5 var-len keys on the device: (blob u8, offsets int64[n+1])."""
+        import torch
+        off = torch.empty(n + 1, dtype=torch.int64, device=f"cuda:{self.device}")
+        _check("bsdb_dev_gen_keys_var", lib().bsdb_dev_gen_keys_var(self._h, first, n, _ptr(off), None, 0,
+                                                                    _stream(stream)))
+        total = int(off[-1])
+        blob = torch.empty(total + 16, dtype=torch.uint8, device=f"cuda:{self.device}")
+        _check("bsdb_dev_gen_keys_var", lib().bsdb_dev_gen_keys_var(self._h, first, n, _ptr(off), _ptr(blob),
+                                                                    total + 16, _stream(stream)))
+        return blob, off
 
     def gen_keys13(self, first: int, n: int, out=None, stream=None):
         import torch

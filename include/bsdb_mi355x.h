@@ -162,6 +162,13 @@ int bsdb_hash_fixed(bsdb_ctx *ctx, const uint8_t *h_keys, uint32_t key_len, uint
  * written on device (benchmark input generator; not part of the build path). */
 int bsdb_dev_gen_keys13(bsdb_ctx *ctx, uint64_t first, uint64_t n, uint8_t *d_keys, void *stream);
 
+/* Config C5 synthetic var-len keys: lengths 8..64 drawn
+ * Zipf(1.1), bytes 0-7 = i big-endian, splitmix tail.  Writes d_offsets[n+1]
+ * (offsets[0] = 0); with d_blob != NULL also the key bytes, after checking
+ * offsets[n] <= blob_cap (synchronises).  Bench/test input generator only. */
+int bsdb_dev_gen_keys_var(bsdb_ctx *ctx, uint64_t first, uint64_t n, uint64_t *d_offsets, uint8_t *d_blob,
+                          uint64_t blob_cap, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

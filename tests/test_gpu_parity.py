@@ -346,3 +346,78 @@ def test_gov_build_large_valid(ctx):
                                   O.lookup_batch(sig[idx], n, dE.cpu().numpy().view(np.uint64),
                                                  dv.cpu().numpy().view(np.uint64), 8,
                                                  dsb.cpu().numpy().view(np.uint64)))
+
+
+# ---------------------------------------------------------------- config C5 var-len keys
+def _splitmix64_np(x):
+    with np.errstate(over="ignore"):
+        z = x.astype(np.uint64) + np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        return z ^ (z >> np.uint64(31))
+
+
+def _varkeys_np(first, n):
+    """Python restatement of the C5 generator (hash_kernels.hip k_gen_var_*)."""
+    w = [1 / r ** 1.1 for r in range(1, 58)]
+    tot, c, thr = sum(w), 0.0, []
+    for x in w[:-1]:
+        c += x
+        thr.append(int(c / tot * 2 ** 64))
+    thr = np.array(thr, dtype=np.uint64)
+    i = np.arange(first, first + n, dtype=np.uint64)
+    u = _splitmix64_np(i ^ np.uint64(0xB5DB0005))
+    lens = 8 + (u[:, None] >= thr[None, :]).sum(1)
+    keys = []
+    for k in range(n):
+        ii = int(i[k])
+        b = bytearray(ii.to_bytes(8, "big"))
+        for wdx in range((lens[k] - 8 + 7) // 8):
+            t = int(_splitmix64_np(np.array([((ii << 3) + wdx) ^ 0xB5DB0005A5A5A5A5], np.uint64))[0])
+            b += t.to_bytes(8, "little")
+        keys.append(bytes(b[: lens[k]]))
+    off = np.zeros(n + 1, np.uint64)
+    off[1:] = np.cumsum(lens)
+    return np.frombuffer(b"".join(keys), np.uint8), off
+
+
+def test_var_key_generator(ctx):
+    for first, n in ((0, 3000), (2 ** 32 - 700, 1500)):
+        blob, off = ctx.gen_keys_var(first, n)
+        want_blob, want_off = _varkeys_np(first, n)
+        np.testing.assert_array_equal(u64(off), want_off)
+        np.testing.assert_array_equal(blob.cpu().numpy()[: want_blob.size], want_blob)
+
+
+@pytest.mark.parametrize("mode", [0, 2])
+def test_var_staged_matches_oracle_and_direct(ctx, mode):
+    """LDS-staged var-len front end (default) == direct front end == oracle."""
+    n = 300_001
+    blob, off = ctx.gen_keys_var(5, n)
+    hb, ho = blob.cpu().numpy(), u64(off)
+    sig = u64(ctx.hash_var(blob, off))
+    np.testing.assert_array_equal(sig, O.hash_var(hb[: int(ho[-1])], ho))
+    m = O.num_buckets(n) * 7
+    ctx.set_histogram_mode(mode)
+    try:
+        c0 = ctx.histogram_var(blob, off, m).cpu().numpy().view(np.uint32)
+        ctx.set_frontend(2)
+        c2 = ctx.histogram_var(blob, off, m).cpu().numpy().view(np.uint32)
+    finally:
+        ctx.set_frontend(0)
+        ctx.set_histogram_mode(0)
+    np.testing.assert_array_equal(c0, c2)
+    np.testing.assert_array_equal(c0, O.histogram_var(hb[: int(ho[-1])], ho, m))
+
+
+def test_var_staged_long_subtiles_fall_back(ctx):
+    """Sub-tiles whose bytes exceed the LDS stage (long keys) hash from global memory."""
+    rng = np.random.default_rng(17)
+    lens = rng.integers(0, 30, 40_000)
+    lens[9000:9600] = rng.integers(60, 180, 600)     # one sub-tile far over 32 KiB
+    lens[20_000:20_512] = 63                          # exactly at the stage limit
+    off = np.zeros(lens.size + 1, np.uint64)
+    off[1:] = np.cumsum(lens)
+    blob = rng.integers(0, 256, int(off[-1]), dtype=np.uint8)
+    sig = u64(ctx.hash_var(dev(blob), dev(off.view(np.int64))))
+    np.testing.assert_array_equal(sig, O.hash_var(blob, off))
