@@ -248,9 +248,9 @@ int histogram_impl(bsdb_ctx *c, const uint8_t *keys, const uint64_t *offsets, ui
                     const uint32_t grid = (uint32_t)std::min<uint64_t>(nfast, (uint64_t)c->num_cus * per_cu);
 #define BSDB_D13(V, T) k_pass1_d13<V, T><<<grid, T, 0, s>>>(ac, nfast)
                     if (c->d13_threads == 256) {
-                        if (c->d13_variant == 1) BSDB_D13(1, 256); else if (c->d13_variant == 3) BSDB_D13(3, 256); else BSDB_D13(0, 256);
+                        if (c->d13_variant == 1) BSDB_D13(1, 256); else if (c->d13_variant == 3) BSDB_D13(3, 256); else if (c->d13_variant == 6) BSDB_D13(6, 256); else BSDB_D13(0, 256);
                     } else {
-                        if (c->d13_variant == 1) BSDB_D13(1, 512); else if (c->d13_variant == 3) BSDB_D13(3, 512); else BSDB_D13(0, 512);
+                        if (c->d13_variant == 1) BSDB_D13(1, 512); else if (c->d13_variant == 3) BSDB_D13(3, 512); else if (c->d13_variant == 6) BSDB_D13(6, 512); else BSDB_D13(0, 512);
                     }
 #undef BSDB_D13
                 }
@@ -547,8 +547,34 @@ int bsdb_dev_gov_build(bsdb_ctx *c, const uint64_t *d_sig, uint64_t n, uint32_t 
                                                  (uint64_t *)c->g_sorted);
     k_bucket_sort<<<(uint32_t)std::min<uint64_t>(m, (uint64_t)c->num_cus * 8), 256, 0, s>>>(
         (uint64_t *)c->g_sorted, d_E, m, status);                                 // A5
-    SolveArgs sa{(const uint64_t *)c->g_sorted, m, d_E, d_values, (uint64_t *)c->g_scratch, status};
+    // BSDB_GOV_PROFILE=1: per-phase cycle totals of the solver printed to stderr
+    const bool gprof = getenv("BSDB_GOV_PROFILE") != nullptr;
+    uint64_t *d_prof = nullptr;
+    if (gprof) {
+        HIP_OK(hipMalloc(&d_prof, (size_t)solve_grid * GP_N * 8));
+        HIP_OK(hipMemsetAsync(d_prof, 0, (size_t)solve_grid * GP_N * 8, s));
+    }
+    SolveArgs sa{(const uint64_t *)c->g_sorted, m, d_E, d_values, (uint64_t *)c->g_scratch, status, d_prof};
     k_gov_solve<<<solve_grid, GS_THREADS, 0, s>>>(sa);                              // A8
+    if (gprof) {
+        std::vector<uint64_t> h((size_t)solve_grid * GP_N);
+        HIP_OK(hipMemcpyAsync(h.data(), d_prof, h.size() * 8, hipMemcpyDeviceToHost, s));
+        HIP_OK(hipStreamSynchronize(s));
+        (void)hipFree(d_prof);
+        const char *names[GP_N] = {"edges", "peel", "greedy", "bfs", "tarjan", "singletons", "dense", "back",
+                                   "store", "n_seeds", "n_bfs", "n_bfs_pops", "n_dense_rows", "n_dense_max",
+                                   "n_core"};
+        std::vector<double> tot(GP_N, 0.0);
+        for (uint32_t w = 0; w < solve_grid; ++w)
+            for (int k = 0; k < GP_N; ++k) {
+                const double v = (double)h[(size_t)w * GP_N + k];
+                tot[k] = k == GP_N_DENSE_MAX ? std::max(tot[k], v) : tot[k] + v;
+            }
+        fprintf(stderr, "[gov-profile] m=%llu grid=%u", (unsigned long long)m, solve_grid);
+        for (int k = 0; k < GP_N; ++k)
+            fprintf(stderr, " %s=%.4g", names[k], k == GP_N_DENSE_MAX ? tot[k] : tot[k] / (k < GP_N_SEEDS ? solve_grid : 1));
+        fprintf(stderr, "  (cycles: mean per workgroup; counts: totals)\n");
+    }
     if (width) {
         HIP_OK(hipMemsetAsync(d_sigbits, 0, ((n * width + 63) / 64 + 1) * 8, s));
         const MphView v{d_E, d_values, nullptr, n, mult, width};

@@ -106,7 +106,12 @@ struct SolveArgs {
     uint64_t *values;     // zeroed 2-bit value array
     uint64_t *scratch;    // per workgroup: 2 * GS_CMAX * GS_WMAX words
     uint32_t *status;
+    uint64_t *prof;       // optional per-workgroup phase cycle counters [grid][GP_N] (BSDB_GOV_PROFILE)
 };
+
+// phase counters (cycles, or counts for the GP_N_* slots)
+enum GovProf { GP_EDGES, GP_PEEL, GP_GREEDY, GP_BFS, GP_TARJAN, GP_SINGLE, GP_DENSE, GP_BACK, GP_STORE,
+               GP_N_SEEDS, GP_N_BFS, GP_N_BFS_POPS, GP_N_DENSE_ROWS, GP_N_DENSE_MAX, GP_N_CORE, GP_N };
 
 struct SolveLds {
     uint16_t e[3 * GS_CMAX];
@@ -133,11 +138,28 @@ __device__ __forceinline__ void gf3_add(uint64_t &x1, uint64_t &x2, uint64_t y1,
     x2 = (a2 & ~y1 & ~y2) | (~a1 & ~a2 & y2) | (a1 & y1);
 }
 
+struct PhaseClock {
+    uint64_t *acc;  // nullptr = off
+    uint64_t t;
+    __device__ void start() { if (acc) t = clock64(); }
+    __device__ void lap(int slot) {
+        if (acc) {
+            const uint64_t now = clock64();
+            if (threadIdx.x == 0) acc[slot] += now - t;
+            t = now;
+        }
+    }
+    __device__ void add(int slot, uint64_t v) { if (acc && threadIdx.x == 0) acc[slot] += v; }
+    __device__ void max(int slot, uint64_t v) { if (acc && threadIdx.x == 0 && v > acc[slot]) acc[slot] = v; }
+};
+
 // Tries local seed j on bucket (sig, cnt, nv).  Returns (WG-uniform) true on
 // success with L.xval / L.vowner describing the solution.
 __device__ bool try_seed(SolveLds &L, const ulonglong2 *sig, uint32_t cnt, uint32_t nv, uint64_t seed_bits,
-                         uint64_t *scr) {
+                         uint64_t *scr, PhaseClock &pc) {
     const int tid = threadIdx.x;
+    pc.start();
+    pc.add(GP_N_SEEDS, 1);
     const bool tiny = cnt <= GS_TINY;
     if (tid == 0) L.flag = 0;
     for (uint32_t v = tid; v < nv; v += GS_THREADS) {
@@ -161,6 +183,7 @@ __device__ bool try_seed(SolveLds &L, const ulonglong2 *sig, uint32_t cnt, uint3
         L.round_of[k] = -1;
     }
     __syncthreads();
+    pc.lap(GP_EDGES);
     if (L.flag) return false;
     if (cnt == 1 && nv == 1) {
         if (tid == 0) {
@@ -201,6 +224,7 @@ __device__ bool try_seed(SolveLds &L, const ulonglong2 *sig, uint32_t cnt, uint3
         __syncthreads();
     }
     const int rounds = r;
+    pc.lap(GP_PEEL);
 
     // ---- 2. orientation of the core (lane 0): greedy, then BFS augmenting paths
     if (tid == 0) {
@@ -218,14 +242,20 @@ __device__ bool try_seed(SolveLds &L, const ulonglong2 *sig, uint32_t cnt, uint3
                 }
             }
         }
+        pc.lap(GP_GREEDY);
+        uint32_t nbfs = 0, npops = 0, ncore = 0;
+        if (pc.acc)
+            for (uint32_t k = 0; k < cnt; ++k) ncore += L.round_of[k] < 0;
         for (uint32_t k0 = 0; k0 < cnt && ok; ++k0) {
             if (L.round_of[k0] >= 0 || L.hinge[k0] >= 0) continue;
             for (uint32_t v = 0; v < nv; ++v) seen[v] = 0;
             int qh = 0, qt = 0, found_v = -1, found_e = -1;
             queue[qt++] = (int16_t)k0;
             bfs_prev[k0] = -1;
+            ++nbfs;
             while (qh < qt && found_v < 0) {
                 const int k = queue[qh++];
+                ++npops;
                 for (int i = 0; i < 3; ++i) {
                     const uint32_t v = L.e[3 * k + i];
                     if (seen[v]) continue;
@@ -255,8 +285,12 @@ __device__ bool try_seed(SolveLds &L, const ulonglong2 *sig, uint32_t cnt, uint3
             }
         }
         L.flag = ok;
+        pc.add(GP_N_BFS, nbfs);
+        pc.add(GP_N_BFS_POPS, npops);
+        pc.add(GP_N_CORE, ncore);
     }
     __syncthreads();
+    pc.lap(GP_BFS);
     if (!L.flag) return false;
 
     // ---- tiny buckets: first satisfying assignment in base-3 order (lane 0)
@@ -339,6 +373,7 @@ __device__ bool try_seed(SolveLds &L, const ulonglong2 *sig, uint32_t cnt, uint3
         L.ncomp = (uint32_t)nc;
     }
     __syncthreads();
+    pc.lap(GP_TARJAN);
 
     // ---- 3b. blocks in emission order: singletons on lane 0, blocks with the WG
     const uint32_t ncomp = L.ncomp;
@@ -369,6 +404,7 @@ __device__ bool try_seed(SolveLds &L, const ulonglong2 *sig, uint32_t cnt, uint3
             L.pivot = c;
         }
         __syncthreads();
+        pc.lap(GP_SINGLE);
         c = L.pivot;
         if (c >= ncomp) break;
         // dense block c
@@ -457,6 +493,9 @@ __device__ bool try_seed(SolveLds &L, const ulonglong2 *sig, uint32_t cnt, uint3
         }
         for (uint32_t i = tid; i < sz; i += GS_THREADS) L.col_of[L.members[beg + i]] = -1;
         __syncthreads();
+        pc.lap(GP_DENSE);
+        pc.add(GP_N_DENSE_ROWS, sz);
+        pc.max(GP_N_DENSE_MAX, sz);
         ++c;
     }
     if (!L.flag) return false;
@@ -477,12 +516,14 @@ __device__ bool try_seed(SolveLds &L, const ulonglong2 *sig, uint32_t cnt, uint3
         }
         __syncthreads();
     }
+    pc.lap(GP_BACK);
     return true;
 }
 
 __global__ __launch_bounds__(GS_THREADS) void k_gov_solve(SolveArgs a) {
     __shared__ SolveLds L;
     uint64_t *scr = a.scratch + (size_t)blockIdx.x * 2 * GS_CMAX * GS_WMAX;
+    PhaseClock pc{a.prof ? a.prof + (size_t)blockIdx.x * GP_N : nullptr, 0};
     for (uint64_t b = blockIdx.x; b < a.m; b += gridDim.x) {
         const uint64_t lo = a.E[b] & OFFSET_MASK, hi = a.E[b + 1] & OFFSET_MASK;
         const uint32_t cnt = (uint32_t)(hi - lo);
@@ -496,7 +537,8 @@ __global__ __launch_bounds__(GS_THREADS) void k_gov_solve(SolveArgs a) {
         const ulonglong2 *sig = reinterpret_cast<const ulonglong2 *>(a.sig) + lo;
         uint32_t j = 0;
         for (; j < 256; ++j)
-            if (try_seed(L, sig, cnt, nv, (uint64_t)j << 56, scr)) break;
+            if (try_seed(L, sig, cnt, nv, (uint64_t)j << 56, scr, pc)) break;
+        pc.start();
         if (j == 256) {
             if (threadIdx.x == 0) atomicOr(a.status, (uint32_t)GOV_SEEDS);
             continue;
@@ -519,6 +561,7 @@ __global__ __launch_bounds__(GS_THREADS) void k_gov_solve(SolveArgs a) {
         }
         if (threadIdx.x == 0) a.E[b] |= (uint64_t)j << 56;
         __syncthreads();
+        pc.lap(GP_STORE);
     }
 }
 

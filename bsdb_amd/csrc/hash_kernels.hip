@@ -130,7 +130,7 @@ __device__ __forceinline__ void hash_staged(const uint32_t *stage, uint32_t k, u
         const uint32_t *q = stage + (o >> 2);
         const uint32_t sh = (o & 3) * 8;
         W64 a0, a1;
-        spooky13_w(q[0], q[1], q[2], q[3], sh, w64(seed), a0, a1);
+        spooky13_u(q[0], q[1], q[2], q[3], sh, seed, a0, a1);
         s0 = u64(a0);
         s1 = u64(a1);
     } else {
@@ -240,13 +240,12 @@ __global__ __launch_bounds__(P1_THREADS, 4) void k_pass1(P1Args a) {
                 const uint64_t byte = (tile0 + tid + j * P1_THREADS) * 13;
                 win[j] = __builtin_nontemporal_load(reinterpret_cast<const u32x4a *>(a.keys + (byte & ~3ULL)));
             }
-            const W64 seedw = w64(a.seed);
 #pragma unroll
             for (int j = 0; j < P1_KEYS_PER_THREAD; ++j) {
                 const uint32_t kt = tid + j * P1_THREADS;
                 const uint32_t sh = ((kt * 13u) & 3u) * 8u;  // tile0*13 is a multiple of 4
                 W64 s0, s1;
-                spooky13_w(win[j].x, win[j].y, win[j].z, win[j].w, sh, seedw, s0, s1);
+                spooky13_u(win[j].x, win[j].y, win[j].z, win[j].w, sh, a.seed, s0, s1);
                 emit(kt, tile0 + kt, u64(s0), u64(s1));
             }
         } else {
@@ -418,7 +417,8 @@ constexpr int D13_NQ = P1_KEYS_PER_THREAD / D13_Q;  // quarters per tile
 
 // VARIANT (profiling builds only; 0 in production): 1 = skip the tile
 // epilogue, 3 = no global id stores, 4 = no LDS scatter (stores of stale slots),
-// 5 = scan + barriers only.
+// 5 = scan + barriers only, 6 = adds as v_add_co/v_addc pairs (round-1 form,
+// 3.5 % slower: 1539 vs 1380 VALU per 16 keys).
 template <int VARIANT, int NT>
 __global__ __launch_bounds__(NT, 4) void k_pass1_d13(P1Args a, uint64_t ntiles) {
     constexpr int TILE = NT * P1_KEYS_PER_THREAD;
@@ -463,7 +463,10 @@ __global__ __launch_bounds__(NT, 4) void k_pass1_d13(P1Args a, uint64_t ntiles) 
                 const uint32_t kt = tid + (q * D13_Q + j) * NT;
                 const uint32_t sh = ((kt * 13u) & 3u) * 8u;  // tile0*13 is a multiple of 4
                 W64 s0, s1;
-                spooky13_w(R[j].x, R[j].y, R[j].z, R[j].w, sh, seedw, s0, s1);
+                if (VARIANT == 6)
+                    spooky13_w(R[j].x, R[j].y, R[j].z, R[j].w, sh, seedw, s0, s1);
+                else
+                    spooky13_u(R[j].x, R[j].y, R[j].z, R[j].w, sh, a.seed, s0, s1);
                 const uint32_t b = bucket_of_w(s0, mult);
                 const int jj = q * D13_Q + j;
                 bk[jj] = b;
