@@ -37,6 +37,8 @@ struct bsdb_ctx {
     size_t ids_bytes = 0;
     uint32_t *cursor = nullptr;   // region fills [nregions][P]
     size_t cursor_bytes = 0;
+    uint64_t *p2_pref = nullptr;  // pass-2 plan: prefix of the segment fills
+    size_t p2_pref_bytes = 0;
     uint32_t *overflow = nullptr; // 1 word
     uint64_t *scan_part = nullptr;
     size_t scan_part_n = 0;
@@ -77,7 +79,7 @@ struct ProfScope {
 
 namespace {
 
-constexpr uint64_t DEFAULT_CHUNK_KEYS = 1ULL << 31;
+constexpr uint64_t DEFAULT_CHUNK_KEYS = 1ULL << 32;  // measured: 2^32 286 G keys/s, 2^33 284, one launch (13.2e9) 266
 
 #define HIP_OK(x)                                      \
     do {                                               \
@@ -148,36 +150,60 @@ void launch_pass1(const P1Args &a0, bool var, uint32_t key_len, uint64_t tiles, 
 
 struct PartPlan {
     uint32_t nparts;
-    uint32_t nregions;  // regions per partition in the id buffer (one per XCD)
-    uint32_t region0;   // first region used by k_pass1
+    uint32_t nmain;     // NCOPY regions shared by the workgroups of one XCD
+    uint32_t ntail;     // 13-byte path: NCOPY regions of the bounds-checked tail kernel
     uint32_t grid_d13;  // persistent workgroups of the 13-byte kernel (0 = generic path)
-    uint64_t cap;       // ids per (partition, region), multiple of 8
-    uint32_t rpw;       // pass 2: regions per workgroup
-    uint32_t nslices;   // pass 2: slices per region
-    uint32_t slice;     // pass 2: ids per slice, multiple of 8
+    uint64_t cap;       // ids per (partition, main region), multiple of 64
+    uint64_t cap_tail;  // ids per (partition, tail region), multiple of 64
+    size_t ids_elems() const { return (size_t)nparts * (nmain * cap + ntail * cap_tail); }
 };
 
-uint64_t round8(double x) { return ((uint64_t)x + 7) & ~7ULL; }
+uint64_t round64(double x) { return ((uint64_t)x + 63) & ~63ULL; }
 
-// Region capacities: expected share of a full partition per XCD copy plus 8
-// sigma and slack (a fill beyond cap raises the overflow flag: the chunk is
-// recounted with direct atomics).
+using D13Kernel = void (*)(P1Args, uint64_t);
+D13Kernel d13_kernel(int threads, int variant) {
+#define BSDB_D13_PICK(T)                                  \
+    switch (variant) {                                    \
+        case 1: return k_pass1_d13<1, T>;                 \
+        case 5: return k_pass1_d13<5, T>;                 \
+        case 6: return k_pass1_d13<6, T>;                 \
+        case 7: return k_pass1_d13<7, T>;                 \
+        case 9: return k_pass1_d13b<T, 4, 4>;             \
+        case 10: return k_pass1_d13b<T, 8, T == 256 ? 3 : 2>; \
+        case 11: return k_pass1_d13b<T, 4, 4, 1>;         \
+        default: return k_pass1_d13<0, T>;                \
+    }
+    if (threads == 256) BSDB_D13_PICK(256)
+    BSDB_D13_PICK(512)
+#undef BSDB_D13_PICK
+}
+
+// Region capacities: a partition's expected share per XCD copy plus 8 sigma
+// and two tiles of slack (a fill beyond cap raises the overflow flag: the
+// chunk is recounted with direct atomics).  Layout of the id buffer:
+// [nmain][P][cap] then [ntail][P][cap_tail].
 PartPlan plan_partitions(const bsdb_ctx *c, uint64_t chunk, uint64_t m, bool d13) {
     PartPlan p{};
     p.nparts = (uint32_t)((m + PART_BUCKETS - 1) / PART_BUCKETS);
     const double frac = std::min(1.0, (double)PART_BUCKETS / (double)m);
-    const uint64_t tiles = (chunk + P1_TILE - 1) / P1_TILE;
-    p.grid_d13 = d13 ? (uint32_t)std::min<uint64_t>(tiles, (uint64_t)c->num_cus * 2) : 0;
-    {
-        const double e = (double)chunk * frac / NCOPY;
-        p.cap = round8(e * 1.02 + 8.0 * std::sqrt(e) + 2 * P1_TILE + 64);
-        p.region0 = 0;
-        p.nregions = NCOPY;
-        p.rpw = 1;
-        uint64_t slice = std::max<uint64_t>(65536, (uint64_t)std::ceil(e * p.nparts * NCOPY / 1024.0));
-        slice = std::min<uint64_t>(round8((double)slice), p.cap);
-        p.slice = (uint32_t)slice;
-        p.nslices = (uint32_t)((p.cap + slice - 1) / slice);
+    const double e = (double)chunk * frac / NCOPY;
+    p.nmain = NCOPY;
+    p.cap = round64(e * 1.02 + 8.0 * std::sqrt(e) + 2 * P1_TILE + 64);
+    p.ntail = 0;
+    p.cap_tail = 0;
+    if (d13) {
+        const int nt = c->d13_threads;
+        const uint64_t dtile = (uint64_t)nt * P1_KEYS_PER_THREAD;
+        D13Kernel k = d13_kernel(nt, c->d13_variant);
+        int per_cu = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, nt, 0) != hipSuccess || per_cu < 1) per_cu = 1;
+        per_cu = std::min(per_cu, 2048 / nt);  // 16 waves per CU
+        const uint64_t tiles = (chunk + dtile - 1) / dtile;
+        p.grid_d13 = (uint32_t)std::min<uint64_t>(tiles, (uint64_t)c->num_cus * per_cu);
+        // the tail (< 2 tiles of the persistent kernel) goes to k_pass1 in
+        // blocks of P1_TILE keys, one region each
+        p.ntail = NCOPY;
+        p.cap_tail = round64(P1_TILE + 64);
     }
     return p;
 }
@@ -206,21 +232,44 @@ int histogram_impl(bsdb_ctx *c, const uint8_t *keys, const uint64_t *offsets, ui
     uint64_t chunk = c->chunk_keys ? c->chunk_keys : DEFAULT_CHUNK_KEYS;
     chunk = std::max<uint64_t>(P1_TILE, chunk / P1_TILE * P1_TILE);
     chunk = std::min<uint64_t>(chunk, (n + P1_TILE - 1) / P1_TILE * P1_TILE);
-    bool d13 = !var && key_len == 13 && c->frontend == 0;
+    const bool d13 = !var && key_len == 13 && c->frontend == 0 && nparts <= 2u * c->d13_threads;
     PartPlan pp = plan_partitions(c, chunk, m, d13);
-    // the 13-byte kernel addresses the id buffer with 32-bit element offsets
-    if (d13 && (uint64_t)pp.nparts * pp.nregions * pp.cap >= (1ULL << 32)) d13 = false;
-    int rc = grow(&c->ids, &c->ids_bytes, (size_t)pp.nparts * pp.nregions * pp.cap * sizeof(uint16_t));
+    // the id buffer takes at most half of the device memory left (workspace
+    // included); the 13-byte kernel addresses one region set (P segments)
+    // with 32-bit offsets
+    size_t free_b = 0, total_b = 0;
+    if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) free_b = 0;
+    const size_t budget = (free_b + c->ids_bytes) / 2;
+    while (chunk > 2 * P1_TILE && (pp.ids_elems() * sizeof(uint16_t) > budget ||
+                                   (uint64_t)pp.nparts * pp.cap >= (1ULL << 32))) {
+        chunk = std::max<uint64_t>(P1_TILE, chunk / 2 / P1_TILE * P1_TILE);
+        pp = plan_partitions(c, chunk, m, d13);
+    }
+    const uint32_t R = pp.nmain + pp.ntail;
+    int rc = grow(&c->ids, &c->ids_bytes, pp.ids_elems() * sizeof(uint16_t));
     if (rc) return rc;
-    rc = grow((void **)&c->cursor, &c->cursor_bytes, (size_t)pp.nparts * pp.nregions * sizeof(uint32_t));
+    rc = grow((void **)&c->cursor, &c->cursor_bytes, (size_t)pp.nparts * R * sizeof(uint32_t));
+    if (rc) return rc;
+    rc = grow((void **)&c->p2_pref, &c->p2_pref_bytes, ((size_t)pp.nparts * R + 1) * sizeof(uint64_t));
     if (rc) return rc;
     a.ids = (uint16_t *)c->ids;
     a.cursor = c->cursor;
     a.overflow = c->overflow;
     a.cap = pp.cap;
     a.nparts = pp.nparts;
-    a.nregions = pp.nregions;
-    a.region0 = pp.region0;
+    a.nregions = pp.nmain;
+    a.region0 = 0;
+    P2Layout L{};
+    L.ids = (const uint16_t *)c->ids;
+    L.cursor = c->cursor;
+    L.overflow = c->overflow;
+    L.cap = pp.cap;
+    L.cap_tail = pp.cap_tail;
+    L.nparts = pp.nparts;
+    L.nmain = pp.nmain;
+    L.ntail = pp.ntail;
+    L.num_buckets = m;
+    L.counts = counts;
     for (uint64_t k0 = 0; k0 < n; k0 += chunk) {
         const uint64_t nk = std::min(chunk, n - k0);
         P1Args ac = a;
@@ -231,35 +280,32 @@ int histogram_impl(bsdb_ctx *c, const uint8_t *keys, const uint64_t *offsets, ui
             ac.keys = keys + k0 * key_len;
             ac.blob_bytes = nk * key_len;
         }
-        HIP_OK(hipMemsetAsync(c->cursor, 0, sizeof(uint32_t) * pp.nregions * pp.nparts, s));
+        HIP_OK(hipMemsetAsync(c->cursor, 0, sizeof(uint32_t) * R * pp.nparts, s));
         HIP_OK(hipMemsetAsync(c->overflow, 0, sizeof(uint32_t), s));
         {
             ProfScope ps(c, s, 0, nk);
             const uint64_t tiles = (nk + P1_TILE - 1) / P1_TILE;
             if (d13) {
                 // full tiles whose 16-byte windows stay inside the chunk go to the
-                // pipelined kernel (private regions); the rest (at most two) to the
-                // bounds-checked kernel (shared regions region0..region0+7)
+                // persistent kernel; the rest (< 2 of its tiles) to the
+                // bounds-checked kernel, in the tail regions
                 const uint64_t dtile = (uint64_t)c->d13_threads * P1_KEYS_PER_THREAD;
                 uint64_t nfast = 0;
                 if (ac.blob_bytes >= 3) nfast = std::min(nk / dtile, ((ac.blob_bytes - 3) / 13) / dtile);
                 if (nfast) {
-                    const uint32_t per_cu = 2048 / c->d13_threads;  // 16 waves per CU
-                    const uint32_t grid = (uint32_t)std::min<uint64_t>(nfast, (uint64_t)c->num_cus * per_cu);
-#define BSDB_D13(V, T) k_pass1_d13<V, T><<<grid, T, 0, s>>>(ac, nfast)
-                    if (c->d13_threads == 256) {
-                        if (c->d13_variant == 1) BSDB_D13(1, 256); else if (c->d13_variant == 3) BSDB_D13(3, 256); else if (c->d13_variant == 6) BSDB_D13(6, 256); else BSDB_D13(0, 256);
-                    } else {
-                        if (c->d13_variant == 1) BSDB_D13(1, 512); else if (c->d13_variant == 3) BSDB_D13(3, 512); else if (c->d13_variant == 6) BSDB_D13(6, 512); else BSDB_D13(0, 512);
-                    }
-#undef BSDB_D13
+                    const uint32_t grid = (uint32_t)std::min<uint64_t>(nfast, pp.grid_d13);
+                    d13_kernel(c->d13_threads, c->d13_variant)<<<grid, c->d13_threads, 0, s>>>(ac, nfast);
                 }
                 const uint64_t done = nfast * dtile;
                 if (done < nk) {
-                    P1Args at = ac;  // shares the 8 XCD regions (atomic cursors)
+                    P1Args at = ac;
                     at.keys = ac.keys + done * 13;
                     at.n = nk - done;
                     at.blob_bytes = at.n * 13;
+                    at.ids = a.ids + (size_t)pp.nmain * pp.nparts * pp.cap;
+                    at.cursor = a.cursor + (size_t)pp.nmain * pp.nparts;
+                    at.cap = pp.cap_tail;
+                    at.nregions = pp.ntail;
                     k_pass1<SRC_DIRECT13, EPI_PARTITION, 4, 13><<<(uint32_t)((at.n + P1_TILE - 1) / P1_TILE), P1_THREADS, 0, s>>>(at);
                 }
             } else {
@@ -268,10 +314,8 @@ int histogram_impl(bsdb_ctx *c, const uint8_t *keys, const uint64_t *offsets, ui
         }
         {
             ProfScope ps(c, s, 1, nk);
-            const uint32_t groups = (pp.nregions + pp.rpw - 1) / pp.rpw;
-            k_pass2<<<dim3(groups * pp.nslices, pp.nparts), P2_THREADS, 0, s>>>(
-                (const uint16_t *)c->ids, c->cursor, c->overflow, pp.cap, pp.nparts, pp.nregions, pp.rpw,
-                pp.nslices, pp.slice, m, counts);
+            k_pass2_plan<<<1, SCAN_THREADS, 0, s>>>(L, c->p2_pref);
+            k_pass2b<<<(uint32_t)c->num_cus, P2_THREADS, 0, s>>>(L, c->p2_pref);
         }
         if (var) {
             k_overflow_fallback<SRC_VAR, 0><<<1024, P1_THREADS, 0, s>>>(ac);
@@ -353,6 +397,7 @@ int bsdb_close(bsdb_ctx *c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     (void)hipFree(c->ids);
     (void)hipFree(c->cursor);
+    (void)hipFree(c->p2_pref);
     (void)hipFree(c->overflow);
     (void)hipFree(c->scan_part);
     (void)hipFree(c->d_keys);

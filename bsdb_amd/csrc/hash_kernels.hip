@@ -415,10 +415,13 @@ __global__ __launch_bounds__(P1_THREADS, 4) void k_pass1(P1Args a) {
 constexpr int D13_Q = 4;                          // keys per quarter
 constexpr int D13_NQ = P1_KEYS_PER_THREAD / D13_Q;  // quarters per tile
 
-// VARIANT (profiling builds only; 0 in production): 1 = skip the tile
-// epilogue, 3 = no global id stores, 4 = no LDS scatter (stores of stale slots),
-// 5 = scan + barriers only, 6 = adds as v_add_co/v_addc pairs (round-1 form,
-// 3.5 % slower: 1539 vs 1380 VALU per 16 keys).
+// VARIANT 0 is production.  Profiling variants (results invalid), pass-1 ms
+// per 2^31 keys at the C4 bucket count: 1 = hash only,
+// no tile epilogue (5.0 vs 7.0); 5 = scan + cursor atomics + barriers, no
+// scatter / write-out (6.4); 7 = no write-out (7.07); 6 = adds as
+// v_add_co/v_addc pairs (+3.5 %).  Private per-workgroup regions (no cursor
+// atomics) measured 8.37: a tile leaves ~60 B per partition, so private lines
+// are written partially, while the XCD-shared regions complete lines in L2.
 template <int VARIANT, int NT>
 __global__ __launch_bounds__(NT, 4) void k_pass1_d13(P1Args a, uint64_t ntiles) {
     constexpr int TILE = NT * P1_KEYS_PER_THREAD;
@@ -496,6 +499,9 @@ __global__ __launch_bounds__(NT, 4) void k_pass1_d13(P1Args a, uint64_t ntiles) 
         // consecutive reservations by different workgroups complete 128-byte
         // lines quickly).  The returning cursor atomic overlaps the LDS scatter.
         const uint32_t copy = (uint32_t)(t & (NCOPY - 1));
+        // element offsets below are relative to this tile's region set
+        // (P*cap < 2^32: checked by the host plan)
+        uint16_t *const tile_base = a.ids + (uint64_t)copy * P * a.cap;
         // partitions p = tid and p = tid + NT (P <= 2*NT)
         const uint32_t p0 = tid, p1 = tid + NT;
         const uint32_t c0 = p0 < P ? hist[p0] : 0, c1 = p1 < P ? hist[p1] : 0;
@@ -518,20 +524,21 @@ __global__ __launch_bounds__(NT, 4) void k_pass1_d13(P1Args a, uint64_t ntiles) 
 #pragma unroll
         for (int j = 0; j < P1_KEYS_PER_THREAD; ++j) {
             const uint32_t r = (rk[j >> 1] >> ((j & 1) * 16)) & 0xFFFFu;
-            sorted[run[bk[j] >> PART_SHIFT] + r] = bk[j];
+            if (VARIANT != 5) sorted[run[bk[j] >> PART_SHIFT] + r] = bk[j];
         }
         if (p0 < P) {
             if ((uint64_t)b0 + c0 > a.cap) tile_ovf = 1;
             // element offset of sorted slot 0 for partition p (ids buffer < 2^32
             // elements: checked by the host plan)
-            off32[p0] = (uint32_t)(((uint64_t)copy * P + p0) * a.cap + b0 - e0);
+            off32[p0] = (uint32_t)((uint64_t)p0 * a.cap + b0 - e0);
         }
         if (p1 < P) {
             if ((uint64_t)b1 + c1 > a.cap) tile_ovf = 1;
-            off32[p1] = (uint32_t)(((uint64_t)copy * P + p1) * a.cap + b1 - e1);
+            off32[p1] = (uint32_t)((uint64_t)p1 * a.cap + b1 - e1);
         }
         __syncthreads();
-        if (!tile_ovf) {
+        if (VARIANT == 5 || VARIANT == 7) {
+        } else if (!tile_ovf) {
             // batched: 16 sorted reads, 16 offset reads, 16 two-byte stores
             uint32_t sb[P1_KEYS_PER_THREAD];
 #pragma unroll
@@ -539,20 +546,200 @@ __global__ __launch_bounds__(NT, 4) void k_pass1_d13(P1Args a, uint64_t ntiles) 
             uint32_t so[P1_KEYS_PER_THREAD];
 #pragma unroll
             for (int j = 0; j < P1_KEYS_PER_THREAD; ++j) so[j] = off32[sb[j] >> PART_SHIFT];
-            if (VARIANT == 3) {
-                uint32_t x = 0;
 #pragma unroll
-                for (int j = 0; j < P1_KEYS_PER_THREAD; ++j) x ^= (uint32_t)so[j] ^ sb[j];
-                if (x == 0xFFFFFFFFu) a.overflow[1] = x;
-            } else {
-#pragma unroll
-                for (int j = 0; j < P1_KEYS_PER_THREAD; ++j)
-                    a.ids[(uint64_t)(so[j] + tid + j * NT)] = (uint16_t)(sb[j] & (PART_BUCKETS - 1));
-            }
+            for (int j = 0; j < P1_KEYS_PER_THREAD; ++j)
+                tile_base[(uint64_t)(so[j] + tid + j * NT)] = (uint16_t)(sb[j] & (PART_BUCKETS - 1));
         } else if (tid == 0) {
             atomicOr(a.overflow, 1u);
         }
         __syncthreads();  // sorted / run / off64 reused by the next tile
+    }
+}
+
+// Pass 1, 13-byte keys, two barriers per tile (k_pass1_d13b).  Same front end
+// and XCD-shared regions as k_pass1_d13; the tile epilogue is re-timed so no
+// wave waits on a returning memory operation or on a partner's scan:
+//   A  barrier: hist[cur] complete
+//      every wave scans the (<= 512) partition counts itself into its own
+//      copy runw[w] (no barrier), scatters its keys into `sorted`, and thread
+//      p issues the cursor atomic of partition p;
+//      then the next tile's first quarter is hashed (into hist[nxt]) while
+//      the atomics return; thread p writes off32[p];
+//   C  barrier: sorted / off32 complete
+//      write-out (runs of 2-byte ids into the XCD-shared regions), then
+//      hist[cur] is zeroed for the tile after next.
+// `sorted`, `off32` need no double buffer: the next scatter / off32 write is
+// behind the next A barrier, which every wave reaches after its write-out.
+// hist is double-buffered: the next tile's first quarter counts into hist[nxt]
+// while slower waves may still be scanning hist[cur].
+// STAMP (diagnostic builds only, results invalid): per-wave s_memtime sums of
+// the cycles spent in barrier A, in barrier C and in the whole loop, written
+// over counts[4*wave ..] at exit.
+template <int NT, int KQ, int WPS, int STAMP = 0>
+__global__ __launch_bounds__(NT, WPS) void k_pass1_d13b(P1Args a, uint64_t ntiles) {
+    constexpr int TILE = NT * P1_KEYS_PER_THREAD;
+    constexpr int NQ = P1_KEYS_PER_THREAD / KQ;  // quarters per tile (even)
+    static_assert(NQ % 2 == 0, "two alternating register sets");
+    constexpr int NW = NT / 64;
+    __shared__ uint32_t sorted[TILE];
+    __shared__ __align__(16) uint32_t hist[2][MAX_PARTS];
+    __shared__ __align__(16) uint32_t runw[NW][MAX_PARTS];
+    __shared__ uint32_t off32[MAX_PARTS];
+    __shared__ uint32_t tile_ovf;
+    const int tid = threadIdx.x;
+    const int w = tid >> 6, l = tid & 63;
+    const uint32_t P = a.nparts;
+    const uint32_t mult = (uint32_t)a.multiplier;
+    const uint64_t G = gridDim.x;
+    if (tid == 0) tile_ovf = 0;
+    for (int i = tid; i < 2 * MAX_PARTS; i += NT) (&hist[0][0])[i] = 0;
+
+    uint64_t t = blockIdx.x;
+    if (t >= ntiles) return;
+    // every tile here is full and readable 3 bytes past its last key: the host
+    // sends the ragged end to k_pass1<SRC_DIRECT13> (bounds-checked)
+    u32x4a X[KQ], Y[KQ];
+    auto load_q = [&](u32x4a(&R)[KQ], uint64_t tt, int q) {
+        if (tt < ntiles) {
+#pragma unroll
+            for (int j = 0; j < KQ; ++j) {
+                const uint64_t byte = (tt * TILE + tid + (q * KQ + j) * NT) * 13;
+                R[j] = __builtin_nontemporal_load(reinterpret_cast<const u32x4a *>(a.keys + (byte & ~3ULL)));
+            }
+        }
+    };
+    uint32_t bk[P1_KEYS_PER_THREAD];
+    uint32_t rk[P1_KEYS_PER_THREAD / 2];  // rank within (tile, partition), two u16 per register
+    auto hash_q = [&](const u32x4a(&R)[KQ], int q, uint32_t *h) {
+#pragma unroll
+        for (int j = 0; j < KQ; ++j) {
+            const uint32_t kt = tid + (q * KQ + j) * NT;
+            const uint32_t sh = ((kt * 13u) & 3u) * 8u;  // tile0*13 is a multiple of 4
+            W64 s0, s1;
+            spooky13_u(R[j].x, R[j].y, R[j].z, R[j].w, sh, a.seed, s0, s1);
+            const uint32_t b = bucket_of_w(s0, mult);
+            const int jj = q * KQ + j;
+            bk[jj] = b;
+            // the count's old value is this key's rank in its partition run
+            const uint32_t r = atomicAdd(&h[b >> PART_SHIFT], 1u);
+            if (jj & 1) rk[jj >> 1] |= r << 16; else rk[jj >> 1] = r;
+        }
+    };
+    load_q(X, t, 0);
+    load_q(Y, t, 1);
+    __syncthreads();  // hist zeroed
+    uint32_t cur = 0;
+    uint64_t st_a = 0, st_c = 0;
+    uint32_t st_n = 0;
+    const uint64_t st_t0 = STAMP ? __builtin_amdgcn_s_memtime() : 0;
+    hash_q(X, 0, hist[cur]);
+    if (NQ > 2) load_q(X, t, 2); else load_q(X, t + G, 0);
+
+    for (; t < ntiles; t += G, cur ^= 1) {
+        // quarter q hashes from set q%2, then that set loads quarter q+2
+        // (of this tile, or of the next one)
+#pragma unroll
+        for (int q = 1; q < NQ; ++q) {
+            if (q & 1) {
+                hash_q(Y, q, hist[cur]);
+                if (q + 2 < NQ) load_q(Y, t, q + 2); else load_q(Y, t + G, q + 2 - NQ);
+            } else {
+                hash_q(X, q, hist[cur]);
+                if (q + 2 < NQ) load_q(X, t, q + 2); else load_q(X, t + G, q + 2 - NQ);
+            }
+        }
+        uint64_t ts0 = STAMP ? __builtin_amdgcn_s_memtime() : 0;
+        __syncthreads();  // A: hist[cur] complete
+        if (STAMP) {
+            const uint64_t ts1 = __builtin_amdgcn_s_memtime();
+            st_a += ts1 - ts0;
+        }
+        // per-wave exclusive scan of the partition counts: lane l owns
+        // partitions 8l .. 8l+7 (entries >= P are zero)
+        {
+            const uint4 h0 = *reinterpret_cast<const uint4 *>(&hist[cur][8 * l]);
+            const uint4 h1 = *reinterpret_cast<const uint4 *>(&hist[cur][8 * l + 4]);
+            uint32_t e[8] = {0, h0.x, h0.x + h0.y, h0.x + h0.y + h0.z, 0, 0, 0, 0};
+            e[4] = e[3] + h0.w;
+            e[5] = e[4] + h1.x;
+            e[6] = e[5] + h1.y;
+            e[7] = e[6] + h1.z;
+            const uint32_t tot = e[7] + h1.w;
+            uint32_t x = tot;
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const uint32_t y = __shfl_up(x, d, 64);
+                if (l >= d) x += y;
+            }
+            const uint32_t base = x - tot;
+            *reinterpret_cast<uint4 *>(&runw[w][8 * l]) = make_uint4(base + e[0], base + e[1], base + e[2], base + e[3]);
+            *reinterpret_cast<uint4 *>(&runw[w][8 * l + 4]) = make_uint4(base + e[4], base + e[5], base + e[6], base + e[7]);
+        }
+        // scatter: slot = run[p] + rank (this wave's own copy of run; LDS
+        // operations of one wave complete in order)
+#pragma unroll
+        for (int j = 0; j < P1_KEYS_PER_THREAD; ++j) {
+            const uint32_t r = (rk[j >> 1] >> ((j & 1) * 16)) & 0xFFFFu;
+            sorted[runw[w][bk[j] >> PART_SHIFT] + r] = bk[j];
+        }
+        // cursor reservation of partitions p0 = tid, p1 = tid + NT in the
+        // XCD-shared regions of copy t % 8 (tiles are dealt round-robin, so a
+        // copy is written from one XCD's L2)
+        const uint32_t copy = (uint32_t)(t & (NCOPY - 1));
+        const uint32_t p0 = tid, p1 = tid + NT;
+        uint32_t c0 = 0, c1 = 0, b0 = 0, b1 = 0;
+        if (p0 < P) {
+            c0 = hist[cur][p0];
+            if (c0) b0 = atomicAdd(a.cursor + copy * P + p0, c0);
+        }
+        if (p1 < P) {
+            c1 = hist[cur][p1];
+            if (c1) b1 = atomicAdd(a.cursor + copy * P + p1, c1);
+        }
+        // the next tile's first quarter hashes while the atomics return
+        if (t + G < ntiles) {
+            hash_q(X, 0, hist[cur ^ 1]);
+            if (NQ > 2) load_q(X, t + G, 2); else load_q(X, t + 2 * G, 0);
+        }
+        if (p0 < P) {
+            if ((uint64_t)b0 + c0 > a.cap) tile_ovf = 1;
+            // element offset, relative to this copy's region set, of sorted slot 0
+            off32[p0] = (uint32_t)((uint64_t)p0 * a.cap + b0 - runw[w][p0]);
+        }
+        if (p1 < P) {
+            if ((uint64_t)b1 + c1 > a.cap) tile_ovf = 1;
+            off32[p1] = (uint32_t)((uint64_t)p1 * a.cap + b1 - runw[w][p1]);
+        }
+        ts0 = STAMP ? __builtin_amdgcn_s_memtime() : 0;
+        __syncthreads();  // C: sorted, off32 complete; every scan of hist[cur] done
+        if (STAMP) {
+            const uint64_t ts1 = __builtin_amdgcn_s_memtime();
+            st_c += ts1 - ts0;
+            ++st_n;
+        }
+        if (!tile_ovf) {
+            uint16_t *const tile_base = a.ids + (uint64_t)copy * P * a.cap;  // P*cap < 2^32 (host plan)
+            uint32_t sb[P1_KEYS_PER_THREAD];
+#pragma unroll
+            for (int j = 0; j < P1_KEYS_PER_THREAD; ++j) sb[j] = sorted[tid + j * NT];
+            uint32_t so[P1_KEYS_PER_THREAD];
+#pragma unroll
+            for (int j = 0; j < P1_KEYS_PER_THREAD; ++j) so[j] = off32[sb[j] >> PART_SHIFT];
+#pragma unroll
+            for (int j = 0; j < P1_KEYS_PER_THREAD; ++j)
+                tile_base[(uint64_t)(so[j] + tid + j * NT)] = (uint16_t)(sb[j] & (PART_BUCKETS - 1));
+        } else if (tid == 0) {
+            atomicOr(a.overflow, 1u);
+        }
+        if (p0 < P) hist[cur][p0] = 0;  // for the tile after next
+        if (p1 < P) hist[cur][p1] = 0;
+    }
+    if (STAMP && l == 0) {
+        const uint64_t wg = (uint64_t)blockIdx.x * NW + w;
+        a.counts[4 * wg + 0] = (uint32_t)(st_a >> 4);
+        a.counts[4 * wg + 1] = (uint32_t)(st_c >> 4);
+        a.counts[4 * wg + 2] = (uint32_t)((__builtin_amdgcn_s_memtime() - st_t0) >> 4);
+        a.counts[4 * wg + 3] = st_n;
     }
 }
 
@@ -693,6 +880,132 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan_final(const uint32_t *cou
         run += c[j];
         if (i0 + j < m) E[i0 + j + 1] = run;
     }
+}
+
+// Pass 2, persistent and balanced.  A launch's id stream is the concatenation,
+// partition-major, of its (partition, region) segments: items k = p*R + r,
+// with regions 0..nmain-1 (capacity cap) followed by tail regions
+// (capacity cap_tail).  k_pass2_plan prefix-sums the segment fills; each of
+// the G workgroups of k_pass2b then histograms exactly its share
+// [total*i/G, total*(i+1)/G) of the stream in a 128 KiB LDS table and
+// flushes the table (coalesced atomics) only when its share crosses into the
+// next partition: ~2 flushes per workgroup instead of one per (partition,
+// slice), no tail of idle workgroups, and 4 x 16 B of ids in flight per lane.
+struct P2Layout {
+    const uint16_t *ids;
+    const uint32_t *cursor;    // fills [R][P]
+    const uint32_t *overflow;
+    uint64_t cap, cap_tail;    // ids per segment of a main / tail region
+    uint32_t nparts, nmain, ntail;
+    uint64_t num_buckets;
+    uint32_t *counts;
+};
+
+__device__ __forceinline__ uint64_t p2_seg_base(const P2Layout &L, uint32_t p, uint32_t r) {
+    return r < L.nmain ? ((uint64_t)r * L.nparts + p) * L.cap
+                       : (uint64_t)L.nmain * L.nparts * L.cap + ((uint64_t)(r - L.nmain) * L.nparts + p) * L.cap_tail;
+}
+
+constexpr int P2_ITEMS_PER_THREAD = 8;  // items <= 1024*8: P <= 512, R <= 16
+
+// pref[k] = ids before item k (exclusive), pref[NI] = total.  One workgroup.
+__global__ __launch_bounds__(SCAN_THREADS) void k_pass2_plan(P2Layout L, uint64_t *pref) {
+    __shared__ uint64_t wsum[SCAN_THREADS / 64];
+    const uint32_t R = L.nmain + L.ntail, NI = L.nparts * R;
+    const int tid = threadIdx.x;
+    uint64_t f[P2_ITEMS_PER_THREAD], s = 0;
+#pragma unroll
+    for (int j = 0; j < P2_ITEMS_PER_THREAD; ++j) {
+        const uint32_t k = tid * P2_ITEMS_PER_THREAD + j;
+        f[j] = 0;
+        if (k < NI) {
+            const uint32_t p = k / R, r = k % R;
+            f[j] = min((uint64_t)L.cursor[(uint64_t)r * L.nparts + p], r < L.nmain ? L.cap : L.cap_tail);
+        }
+        s += f[j];
+    }
+    uint64_t tot;
+    uint64_t run = block_excl_scan64(s, wsum, tid, tot);
+#pragma unroll
+    for (int j = 0; j < P2_ITEMS_PER_THREAD; ++j) {
+        const uint32_t k = tid * P2_ITEMS_PER_THREAD + j;
+        if (k < NI) pref[k] = run;
+        run += f[j];
+    }
+    if (tid == 0) pref[NI] = tot;
+}
+
+__global__ __launch_bounds__(P2_THREADS, 1) void k_pass2b(P2Layout L, const uint64_t *pref) {
+    __shared__ uint32_t hist[PART_BUCKETS];
+    __shared__ uint32_t k_start;
+    if (*L.overflow) return;
+    const int tid = threadIdx.x;
+    const uint32_t R = L.nmain + L.ntail, NI = L.nparts * R;
+    const uint64_t G = gridDim.x, total = pref[NI];
+    const uint64_t lo = total * blockIdx.x / G, hi = total * (blockIdx.x + 1) / G;
+    if (lo >= hi) return;
+    if (tid == 0) {
+        // first item with pref[k] <= lo < pref[k+1]
+        uint32_t a = 0, b = NI;  // invariant: pref[a] <= lo < pref[b]
+        while (b - a > 1) {
+            const uint32_t c = (a + b) / 2;
+            if (pref[c] <= lo) a = c; else b = c;
+        }
+        k_start = a;
+    }
+    for (int i = tid; i < PART_BUCKETS; i += P2_THREADS) hist[i] = 0;
+    __syncthreads();
+    auto flush = [&](uint32_t p) {
+        __syncthreads();
+        const uint64_t b0 = (uint64_t)p << PART_SHIFT;
+        const uint32_t nb = (uint32_t)min((uint64_t)PART_BUCKETS, L.num_buckets - b0);
+        for (uint32_t i = tid; i < PART_BUCKETS; i += P2_THREADS) {
+            const uint32_t h = hist[i];
+            if (h && i < nb) atomicAdd(L.counts + b0 + i, h);
+            hist[i] = 0;
+        }
+        __syncthreads();
+    };
+    int64_t cur_p = -1;
+    for (uint32_t k = k_start; k < NI; ++k) {
+        const uint64_t pk = pref[k], pk1 = pref[k + 1];
+        if (pk >= hi) break;
+        const uint64_t a = max(lo, pk) - pk, b = min(hi, pk1) - pk;
+        if (a >= b) continue;
+        const uint32_t p = k / R, r = k % R;
+        if ((int64_t)p != cur_p) {
+            if (cur_p >= 0) flush((uint32_t)cur_p);
+            cur_p = p;
+        }
+        // segment base is a multiple of 64 ids: 16-byte vectors from a8 on
+        const uint16_t *src = L.ids + p2_seg_base(L, p, r);
+        const uint64_t a8 = min(b, (a + 7) & ~7ULL), b8 = max(a8, b & ~7ULL);
+        if (a + tid < a8) atomicAdd(&hist[src[a + tid]], 1u);
+        if (b8 + tid < b) atomicAdd(&hist[src[b8 + tid]], 1u);
+        const uint4 *v = reinterpret_cast<const uint4 *>(src);
+        uint64_t i = a8 / 8 + tid;
+        const uint64_t v1 = b8 / 8;
+        for (; i + 3 * P2_THREADS < v1; i += 4 * P2_THREADS) {
+            uint4 w[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) w[u] = ntload16(v + i + u * P2_THREADS);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                atomicAdd(&hist[w[u].x & 0xFFFF], 1u); atomicAdd(&hist[w[u].x >> 16], 1u);
+                atomicAdd(&hist[w[u].y & 0xFFFF], 1u); atomicAdd(&hist[w[u].y >> 16], 1u);
+                atomicAdd(&hist[w[u].z & 0xFFFF], 1u); atomicAdd(&hist[w[u].z >> 16], 1u);
+                atomicAdd(&hist[w[u].w & 0xFFFF], 1u); atomicAdd(&hist[w[u].w >> 16], 1u);
+            }
+        }
+        for (; i < v1; i += P2_THREADS) {
+            const uint4 w = ntload16(v + i);
+            atomicAdd(&hist[w.x & 0xFFFF], 1u); atomicAdd(&hist[w.x >> 16], 1u);
+            atomicAdd(&hist[w.y & 0xFFFF], 1u); atomicAdd(&hist[w.y >> 16], 1u);
+            atomicAdd(&hist[w.z & 0xFFFF], 1u); atomicAdd(&hist[w.z >> 16], 1u);
+            atomicAdd(&hist[w.w & 0xFFFF], 1u); atomicAdd(&hist[w.w >> 16], 1u);
+        }
+    }
+    if (cur_p >= 0) flush((uint32_t)cur_p);
 }
 
 // key i has length 8 + r, r drawn Zipf(s=1.1)
