@@ -30,6 +30,7 @@ struct bsdb_ctx {
     int num_cus = 256;
     int d13_variant = 0;  // profiling only (BSDB_D13_VARIANT): results are NOT valid when != 0
     int d13_threads = 512;  // workgroup size of the pipelined 13-byte kernel (BSDB_D13_THREADS=256|512)
+    int d13_copies = 8;     // region copies of the binned 13-byte kernel (BSDB_D13_COPIES=8|16|32)
     uint64_t chunk_keys = 0;
     std::mutex mu;
     // workspace
@@ -171,11 +172,42 @@ D13Kernel d13_kernel(int threads, int variant) {
         case 9: return k_pass1_d13b<T, 4, 4>;             \
         case 10: return k_pass1_d13b<T, 8, T == 256 ? 3 : 2>; \
         case 11: return k_pass1_d13b<T, 4, 4, 1>;         \
+        case 12: return k_pass1_d13<12, T>;               \
+        case 13: return k_pass1_d13b<T, 4, 4, 0, 1>;      \
+        case 14: return k_pass1_d13b<T, 4, 4, 1, 1>;      \
+        case 15: return k_pass1_d13c<0>;                  \
+        case 16: return k_pass1_d13c<1>;                  \
+        case 17: return k_pass1_d13d<0>;                  \
+        case 18: return k_pass1_d13d<1>;                  \
+        case 19: return k_pass1_d13<19, T>;               \
+        case 20: return k_pass1_d13<20, T>;               \
+        case 21: return k_pass1_d13c<2>;                  \
+        case 22: return k_pass1_d13e<0>;                  \
+        case 23: return k_pass1_d13e<1>;                  \
+        case 24: return k_pass1_d13e<2>;                  \
+        case 25: return k_pass1_d13e<3>;                  \
+        case 26: return k_pass1_d13e<4>;                  \
+        case 27: return k_pass1_d13e<5>;                  \
+        case 28: return k_pass1_d13e<6>;                  \
         default: return k_pass1_d13<0, T>;                \
     }
     if (threads == 256) BSDB_D13_PICK(256)
     BSDB_D13_PICK(512)
 #undef BSDB_D13_PICK
+}
+
+// workgroup size of the 13-byte kernel a context runs (the binned kernel is
+// fixed at 1024 threads)
+int d13_nt(const bsdb_ctx *c) {
+    if (c->d13_variant == 15 || c->d13_variant == 16 || c->d13_variant == 21) return D13C_NT;
+    if (c->d13_variant >= 22 && c->d13_variant <= 28) return D13E_NT;
+    if (c->d13_variant == 17 || c->d13_variant == 18) return D13D_NT;
+    return c->d13_threads;
+}
+// keys per tile of the 13-byte kernel a context runs
+uint64_t d13_tile(const bsdb_ctx *c) {
+    if (c->d13_variant == 17 || c->d13_variant == 18) return D13D_TILE;
+    return (uint64_t)d13_nt(c) * P1_KEYS_PER_THREAD;
 }
 
 // Region capacities: a partition's expected share per XCD copy plus 8 sigma
@@ -186,24 +218,30 @@ PartPlan plan_partitions(const bsdb_ctx *c, uint64_t chunk, uint64_t m, bool d13
     PartPlan p{};
     p.nparts = (uint32_t)((m + PART_BUCKETS - 1) / PART_BUCKETS);
     const double frac = std::min(1.0, (double)PART_BUCKETS / (double)m);
-    const double e = (double)chunk * frac / NCOPY;
-    p.nmain = NCOPY;
+    const bool d13e = d13 && c->d13_variant >= 22 && c->d13_variant <= 28;
+    p.nmain = d13e ? (uint32_t)c->d13_copies : NCOPY;
+    const double e = (double)chunk * frac / p.nmain;
     p.cap = round64(e * 1.02 + 8.0 * std::sqrt(e) + 2 * P1_TILE + 64);
     p.ntail = 0;
     p.cap_tail = 0;
     if (d13) {
-        const int nt = c->d13_threads;
-        const uint64_t dtile = (uint64_t)nt * P1_KEYS_PER_THREAD;
+        const int nt = d13_nt(c);
+        const uint64_t dtile = d13_tile(c);
         D13Kernel k = d13_kernel(nt, c->d13_variant);
         int per_cu = 0;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, nt, 0) != hipSuccess || per_cu < 1) per_cu = 1;
         per_cu = std::min(per_cu, 2048 / nt);  // 16 waves per CU
         const uint64_t tiles = (chunk + dtile - 1) / dtile;
         p.grid_d13 = (uint32_t)std::min<uint64_t>(tiles, (uint64_t)c->num_cus * per_cu);
+        if (c->d13_variant >= 22 && c->d13_variant <= 28) {
+            // runs are padded to 8 ids: up to 7 pads per (tile, partition)
+            const double tiles_per_copy = (double)tiles / p.nmain + 1;
+            p.cap = round64(e * 1.02 + 8.0 * std::sqrt(e) + 7.0 * tiles_per_copy + 2 * P1_TILE + 64);
+        }
         // the tail (< 2 tiles of the persistent kernel) goes to k_pass1 in
         // blocks of P1_TILE keys, one region each
         p.ntail = NCOPY;
-        p.cap_tail = round64(P1_TILE + 64);
+        p.cap_tail = round64(std::max<uint64_t>(P1_TILE, dtile) + 64);
     }
     return p;
 }
@@ -232,7 +270,8 @@ int histogram_impl(bsdb_ctx *c, const uint8_t *keys, const uint64_t *offsets, ui
     uint64_t chunk = c->chunk_keys ? c->chunk_keys : DEFAULT_CHUNK_KEYS;
     chunk = std::max<uint64_t>(P1_TILE, chunk / P1_TILE * P1_TILE);
     chunk = std::min<uint64_t>(chunk, (n + P1_TILE - 1) / P1_TILE * P1_TILE);
-    const bool d13 = !var && key_len == 13 && c->frontend == 0 && nparts <= 2u * c->d13_threads;
+    const bool d13 = !var && key_len == 13 && c->frontend == 0 && nparts <= 2u * c->d13_threads &&
+                     (d13_nt(c) != 1024 || nparts <= (uint32_t)std::min(std::min(D13C_MAXP, D13D_MAXP), D13E_MAXP));
     PartPlan pp = plan_partitions(c, chunk, m, d13);
     // the id buffer takes at most half of the device memory left (workspace
     // included); the 13-byte kernel addresses one region set (P segments)
@@ -248,17 +287,19 @@ int histogram_impl(bsdb_ctx *c, const uint8_t *keys, const uint64_t *offsets, ui
     const uint32_t R = pp.nmain + pp.ntail;
     int rc = grow(&c->ids, &c->ids_bytes, pp.ids_elems() * sizeof(uint16_t));
     if (rc) return rc;
-    rc = grow((void **)&c->cursor, &c->cursor_bytes, (size_t)pp.nparts * R * sizeof(uint32_t));
+    rc = grow((void **)&c->cursor, &c->cursor_bytes, ((size_t)pp.nparts * R + P1_SCRATCH_WG + (size_t)P1_SCRATCH_MAXWG * 1024) * sizeof(uint32_t));
     if (rc) return rc;
     rc = grow((void **)&c->p2_pref, &c->p2_pref_bytes, ((size_t)pp.nparts * R + 1) * sizeof(uint64_t));
     if (rc) return rc;
     a.ids = (uint16_t *)c->ids;
     a.cursor = c->cursor;
+    a.scratch = c->cursor + (size_t)pp.nparts * R;
     a.overflow = c->overflow;
     a.cap = pp.cap;
     a.nparts = pp.nparts;
     a.nregions = pp.nmain;
     a.region0 = 0;
+    a.ncopy = pp.nmain;
     P2Layout L{};
     L.ids = (const uint16_t *)c->ids;
     L.cursor = c->cursor;
@@ -289,12 +330,12 @@ int histogram_impl(bsdb_ctx *c, const uint8_t *keys, const uint64_t *offsets, ui
                 // full tiles whose 16-byte windows stay inside the chunk go to the
                 // persistent kernel; the rest (< 2 of its tiles) to the
                 // bounds-checked kernel, in the tail regions
-                const uint64_t dtile = (uint64_t)c->d13_threads * P1_KEYS_PER_THREAD;
+                const uint64_t dtile = d13_tile(c);
                 uint64_t nfast = 0;
                 if (ac.blob_bytes >= 3) nfast = std::min(nk / dtile, ((ac.blob_bytes - 3) / 13) / dtile);
                 if (nfast) {
                     const uint32_t grid = (uint32_t)std::min<uint64_t>(nfast, pp.grid_d13);
-                    d13_kernel(c->d13_threads, c->d13_variant)<<<grid, c->d13_threads, 0, s>>>(ac, nfast);
+                    d13_kernel(d13_nt(c), c->d13_variant)<<<grid, d13_nt(c), 0, s>>>(ac, nfast);
                 }
                 const uint64_t done = nfast * dtile;
                 if (done < nk) {
@@ -376,6 +417,10 @@ int bsdb_open(int device, bsdb_ctx **out) {
     c->device = device;
     if (const char *v = std::getenv("BSDB_D13_VARIANT")) c->d13_variant = std::atoi(v);
     if (const char *v = std::getenv("BSDB_D13_THREADS")) c->d13_threads = std::atoi(v) == 256 ? 256 : 512;
+    if (const char *v = std::getenv("BSDB_D13_COPIES")) {
+        const int k = std::atoi(v);
+        c->d13_copies = (k == 16 || k == 32 || k == 64) ? k : 8;
+    }
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0)
         c->num_cus = cus;

@@ -4,7 +4,7 @@ import os, sys
 import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from bsdb_amd import Context  # noqa: E402
-os.environ["BSDB_D13_VARIANT"] = "11"
+os.environ.setdefault("BSDB_D13_VARIANT", "11")
 n = 2147483648
 m = 8795859
 ctx = Context(0)
