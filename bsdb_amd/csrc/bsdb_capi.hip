@@ -150,98 +150,87 @@ void launch_pass1(const P1Args &a0, bool var, uint32_t key_len, uint64_t tiles, 
 }
 
 struct PartPlan {
-    uint32_t nparts;
-    uint32_t nmain;     // NCOPY regions shared by the workgroups of one XCD
-    uint32_t ntail;     // 13-byte path: NCOPY regions of the bounds-checked tail kernel
-    uint32_t grid_d13;  // persistent workgroups of the 13-byte kernel (0 = generic path)
-    uint64_t cap;       // ids per (partition, main region), multiple of 64
-    uint64_t cap_tail;  // ids per (partition, tail region), multiple of 64
+    uint32_t nparts;     // region bins: bucket >> bin_shift
+    uint32_t bin_shift;  // <= PART_SHIFT; bins nest in the 32768-bucket pass-2 partitions
+    uint32_t capb;       // k_pass1_d13e: ids per LDS bin
+    uint32_t nmain;      // region copies shared by the workgroups of one XCD
+    uint32_t ntail;      // 13-byte path: NCOPY regions of the bounds-checked tail kernel
+    uint32_t grid_d13;   // persistent workgroups of the 13-byte kernel (0 = generic path)
+    uint64_t cap;        // ids per (bin, main region), multiple of 64
+    uint64_t cap_tail;   // ids per (bin, tail region), multiple of 64
     size_t ids_elems() const { return (size_t)nparts * (nmain * cap + ntail * cap_tail); }
 };
 
 uint64_t round64(double x) { return ((uint64_t)x + 63) & ~63ULL; }
 
 using D13Kernel = void (*)(P1Args, uint64_t);
-D13Kernel d13_kernel(int threads, int variant) {
-#define BSDB_D13_PICK(T)                                  \
-    switch (variant) {                                    \
-        case 1: return k_pass1_d13<1, T>;                 \
-        case 5: return k_pass1_d13<5, T>;                 \
-        case 6: return k_pass1_d13<6, T>;                 \
-        case 7: return k_pass1_d13<7, T>;                 \
-        case 9: return k_pass1_d13b<T, 4, 4>;             \
-        case 10: return k_pass1_d13b<T, 8, T == 256 ? 3 : 2>; \
-        case 11: return k_pass1_d13b<T, 4, 4, 1>;         \
-        case 12: return k_pass1_d13<12, T>;               \
-        case 13: return k_pass1_d13b<T, 4, 4, 0, 1>;      \
-        case 14: return k_pass1_d13b<T, 4, 4, 1, 1>;      \
-        case 15: return k_pass1_d13c<0>;                  \
-        case 16: return k_pass1_d13c<1>;                  \
-        case 17: return k_pass1_d13d<0>;                  \
-        case 18: return k_pass1_d13d<1>;                  \
-        case 19: return k_pass1_d13<19, T>;               \
-        case 20: return k_pass1_d13<20, T>;               \
-        case 21: return k_pass1_d13c<2>;                  \
-        case 22: return k_pass1_d13e<0>;                  \
-        case 23: return k_pass1_d13e<1>;                  \
-        case 24: return k_pass1_d13e<2>;                  \
-        case 25: return k_pass1_d13e<3>;                  \
-        case 26: return k_pass1_d13e<4>;                  \
-        case 27: return k_pass1_d13e<5>;                  \
-        case 28: return k_pass1_d13e<6>;                  \
-        default: return k_pass1_d13<0, T>;                \
+
+// The 13-byte pass-1 kernel a context runs (BSDB_D13_VARIANT):
+//   0 k_pass1_d13e (production), 1 its hash-and-bins-only profile (results
+//   invalid), 2 the round-1 sort kernel k_pass1_d13, 4 k_pass1_d13e with
+//   phase stamps over counts[] (results invalid).
+struct D13Sel {
+    D13Kernel k;
+    int nt;             // workgroup size
+    uint64_t tile;      // keys per tile
+    uint32_t maxp;      // partitions supported
+    bool binned;        // runs padded to 8 ids, region copies = d13_copies
+};
+D13Sel d13_select(const bsdb_ctx *c) {
+    switch (c->d13_variant) {
+        case 1: return {k_pass1_d13e<1>, D13E_NT, D13E_TILE, D13E_MAXP, true};
+        case 4: return {k_pass1_d13e<4>, D13E_NT, D13E_TILE, D13E_MAXP, true};
+        case 2:
+            if (c->d13_threads == 256) return {k_pass1_d13<256>, 256, 256 * P1_KEYS_PER_THREAD, 512, false};
+            return {k_pass1_d13<512>, 512, 512 * P1_KEYS_PER_THREAD, 1024, false};
+        default: return {k_pass1_d13e<0>, D13E_NT, D13E_TILE, D13E_MAXP, true};
     }
-    if (threads == 256) BSDB_D13_PICK(256)
-    BSDB_D13_PICK(512)
-#undef BSDB_D13_PICK
 }
 
-// workgroup size of the 13-byte kernel a context runs (the binned kernel is
-// fixed at 1024 threads)
-int d13_nt(const bsdb_ctx *c) {
-    if (c->d13_variant == 15 || c->d13_variant == 16 || c->d13_variant == 21) return D13C_NT;
-    if (c->d13_variant >= 22 && c->d13_variant <= 28) return D13E_NT;
-    if (c->d13_variant == 17 || c->d13_variant == 18) return D13D_NT;
-    return c->d13_threads;
-}
-// keys per tile of the 13-byte kernel a context runs
-uint64_t d13_tile(const bsdb_ctx *c) {
-    if (c->d13_variant == 17 || c->d13_variant == 18) return D13D_TILE;
-    return (uint64_t)d13_nt(c) * P1_KEYS_PER_THREAD;
+// Bins of the binned kernel: the smallest bin_shift with ceil(m >> shift)
+// <= D13E_MAXP, so a tile (16384 keys) fills each LDS bin to 16384/P on
+// average while a bin holds D13E_BIN_IDS/P >= 2.25x that (>= 8 sigma).
+bool binned_layout(uint64_t m, uint32_t &shift, uint32_t &nbins, uint32_t &capb) {
+    shift = 0;
+    while (shift <= (uint32_t)PART_SHIFT && ((m + (1ULL << shift) - 1) >> shift) > (uint64_t)D13E_MAXP) ++shift;
+    if (shift > (uint32_t)PART_SHIFT) return false;
+    nbins = (uint32_t)((m + (1ULL << shift) - 1) >> shift);
+    capb = std::min<uint32_t>(((uint32_t)D13E_BIN_IDS / nbins) & ~7u, D13E_TILE + 8);
+    return true;
 }
 
-// Region capacities: a partition's expected share per XCD copy plus 8 sigma
-// and two tiles of slack (a fill beyond cap raises the overflow flag: the
-// chunk is recounted with direct atomics).  Layout of the id buffer:
-// [nmain][P][cap] then [ntail][P][cap_tail].
+// Region capacities: a bin's expected share per region copy plus 8 sigma and
+// two tiles of slack (and, for padded runs, 7 pads per tile); a fill beyond
+// cap raises the overflow flag and the chunk is recounted with direct
+// atomics.  Layout of the id buffer: [nmain][P][cap], then the tail kernel's
+// [ntail][P][cap_tail].
 PartPlan plan_partitions(const bsdb_ctx *c, uint64_t chunk, uint64_t m, bool d13) {
     PartPlan p{};
+    const D13Sel sel = d13_select(c);
+    const bool binned = d13 && sel.binned;
+    p.bin_shift = PART_SHIFT;
     p.nparts = (uint32_t)((m + PART_BUCKETS - 1) / PART_BUCKETS);
-    const double frac = std::min(1.0, (double)PART_BUCKETS / (double)m);
-    const bool d13e = d13 && c->d13_variant >= 22 && c->d13_variant <= 28;
-    p.nmain = d13e ? (uint32_t)c->d13_copies : NCOPY;
+    if (binned) binned_layout(m, p.bin_shift, p.nparts, p.capb);
+    const double frac = std::min(1.0, (double)(1ULL << p.bin_shift) / (double)m);
+    p.nmain = binned ? (uint32_t)c->d13_copies : NCOPY;
     const double e = (double)chunk * frac / p.nmain;
     p.cap = round64(e * 1.02 + 8.0 * std::sqrt(e) + 2 * P1_TILE + 64);
     p.ntail = 0;
     p.cap_tail = 0;
     if (d13) {
-        const int nt = d13_nt(c);
-        const uint64_t dtile = d13_tile(c);
-        D13Kernel k = d13_kernel(nt, c->d13_variant);
         int per_cu = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, nt, 0) != hipSuccess || per_cu < 1) per_cu = 1;
-        per_cu = std::min(per_cu, 2048 / nt);  // 16 waves per CU
-        const uint64_t tiles = (chunk + dtile - 1) / dtile;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, sel.k, sel.nt, 0) != hipSuccess || per_cu < 1) per_cu = 1;
+        per_cu = std::min(per_cu, 2048 / sel.nt);  // at most 32 waves per CU
+        const uint64_t tiles = (chunk + sel.tile - 1) / sel.tile;
         p.grid_d13 = (uint32_t)std::min<uint64_t>(tiles, (uint64_t)c->num_cus * per_cu);
-        if (c->d13_variant >= 22 && c->d13_variant <= 28) {
-            // runs are padded to 8 ids: up to 7 pads per (tile, partition)
+        if (binned) {
             const double tiles_per_copy = (double)tiles / p.nmain + 1;
             p.cap = round64(e * 1.02 + 8.0 * std::sqrt(e) + 7.0 * tiles_per_copy + 2 * P1_TILE + 64);
         }
         // the tail (< 2 tiles of the persistent kernel) goes to k_pass1 in
         // blocks of P1_TILE keys, one region each
         p.ntail = NCOPY;
-        p.cap_tail = round64(std::max<uint64_t>(P1_TILE, dtile) + 64);
+        p.cap_tail = round64(std::max<uint64_t>(P1_TILE, sel.tile) + 64);
     }
     return p;
 }
@@ -270,8 +259,10 @@ int histogram_impl(bsdb_ctx *c, const uint8_t *keys, const uint64_t *offsets, ui
     uint64_t chunk = c->chunk_keys ? c->chunk_keys : DEFAULT_CHUNK_KEYS;
     chunk = std::max<uint64_t>(P1_TILE, chunk / P1_TILE * P1_TILE);
     chunk = std::min<uint64_t>(chunk, (n + P1_TILE - 1) / P1_TILE * P1_TILE);
-    const bool d13 = !var && key_len == 13 && c->frontend == 0 && nparts <= 2u * c->d13_threads &&
-                     (d13_nt(c) != 1024 || nparts <= (uint32_t)std::min(std::min(D13C_MAXP, D13D_MAXP), D13E_MAXP));
+    const D13Sel sel = d13_select(c);
+    uint32_t bsh = 0, nb = 0, cb = 0;
+    const bool d13 = !var && key_len == 13 && c->frontend == 0 &&
+                     (sel.binned ? binned_layout(m, bsh, nb, cb) : nparts <= sel.maxp);
     PartPlan pp = plan_partitions(c, chunk, m, d13);
     // the id buffer takes at most half of the device memory left (workspace
     // included); the 13-byte kernel addresses one region set (P segments)
@@ -300,6 +291,8 @@ int histogram_impl(bsdb_ctx *c, const uint8_t *keys, const uint64_t *offsets, ui
     a.nregions = pp.nmain;
     a.region0 = 0;
     a.ncopy = pp.nmain;
+    a.bin_shift = pp.bin_shift;
+    a.capb = pp.capb;
     P2Layout L{};
     L.ids = (const uint16_t *)c->ids;
     L.cursor = c->cursor;
@@ -309,6 +302,7 @@ int histogram_impl(bsdb_ctx *c, const uint8_t *keys, const uint64_t *offsets, ui
     L.nparts = pp.nparts;
     L.nmain = pp.nmain;
     L.ntail = pp.ntail;
+    L.bshift = PART_SHIFT - pp.bin_shift;
     L.num_buckets = m;
     L.counts = counts;
     for (uint64_t k0 = 0; k0 < n; k0 += chunk) {
@@ -330,12 +324,12 @@ int histogram_impl(bsdb_ctx *c, const uint8_t *keys, const uint64_t *offsets, ui
                 // full tiles whose 16-byte windows stay inside the chunk go to the
                 // persistent kernel; the rest (< 2 of its tiles) to the
                 // bounds-checked kernel, in the tail regions
-                const uint64_t dtile = d13_tile(c);
+                const uint64_t dtile = sel.tile;
                 uint64_t nfast = 0;
                 if (ac.blob_bytes >= 3) nfast = std::min(nk / dtile, ((ac.blob_bytes - 3) / 13) / dtile);
                 if (nfast) {
                     const uint32_t grid = (uint32_t)std::min<uint64_t>(nfast, pp.grid_d13);
-                    d13_kernel(d13_nt(c), c->d13_variant)<<<grid, d13_nt(c), 0, s>>>(ac, nfast);
+                    sel.k<<<grid, sel.nt, 0, s>>>(ac, nfast);
                 }
                 const uint64_t done = nfast * dtile;
                 if (done < nk) {
@@ -428,7 +422,8 @@ int bsdb_open(int device, bsdb_ctx **out) {
         delete c;
         return BSDB_EIO;
     }
-    if (hipMalloc(&c->overflow, sizeof(uint32_t) * 4) != hipSuccess) {
+    if (hipMalloc(&c->overflow, sizeof(uint32_t) * 4) != hipSuccess ||
+        hipMemset(c->overflow, 0, sizeof(uint32_t) * 4) != hipSuccess) {
         bsdb_close(c);
         return BSDB_ENOMEM;
     }
@@ -470,6 +465,17 @@ int bsdb_set_frontend(bsdb_ctx *c, int frontend) {
     if (!c || frontend < 0 || frontend > 2) return BSDB_EINVAL;
     std::lock_guard<std::mutex> g(c->mu);
     c->frontend = frontend;
+    return BSDB_OK;
+}
+
+int bsdb_fallback_count(bsdb_ctx *c, uint64_t *out) {
+    if (!c || !out) return BSDB_EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    HIP_OK(hipSetDevice(c->device));
+    HIP_OK(hipDeviceSynchronize());
+    uint32_t v = 0;
+    HIP_OK(hipMemcpy(&v, c->overflow + 2, sizeof(v), hipMemcpyDeviceToHost));
+    *out = v;
     return BSDB_OK;
 }
 

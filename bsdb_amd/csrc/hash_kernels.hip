@@ -50,6 +50,9 @@ struct P1Args {
     uint32_t nregions;        // regions per partition in the id buffer
     uint32_t region0;         // first region used by k_pass1's NCOPY shared regions
     uint32_t ncopy;           // k_pass1_d13e: region copies (power of 2), copy = tile % ncopy
+    uint32_t bin_shift;       // EPI_PARTITION: a key's region bin is bucket >> bin_shift (<= PART_SHIFT);
+                              // its 2-byte id stays bucket % 32768 (local to its pass-2 partition)
+    uint32_t capb;            // k_pass1_d13e: ids per LDS bin (multiple of 8), nparts*capb <= D13E_BIN_IDS
     // EPI_ATOMIC
     uint32_t *counts;
     // EPI_SIG
@@ -227,7 +230,7 @@ __global__ __launch_bounds__(P1_THREADS, 4) void k_pass1(P1Args a) {
                 atomicAdd(a.counts + b, 1u);
             } else {
                 bkl[kt] = b;
-                atomicAdd(&hist[b >> PART_SHIFT], 1u);
+                atomicAdd(&hist[b >> a.bin_shift], 1u);
             }
         }
     };
@@ -390,14 +393,14 @@ __global__ __launch_bounds__(P1_THREADS, 4) void k_pass1(P1Args a) {
     __syncthreads();
     for (uint32_t kt = tid; kt < tile_n; kt += P1_THREADS) {
         const uint32_t b = bkl[kt];
-        const uint32_t pos = atomicAdd(&run[b >> PART_SHIFT], 1u);
+        const uint32_t pos = atomicAdd(&run[b >> a.bin_shift], 1u);
         sorted[pos] = b;
     }
     __syncthreads();
     bool ovf = false;
     for (uint32_t j = tid; j < tile_n; j += P1_THREADS) {
         const uint32_t b = sorted[j];
-        const uint32_t p = b >> PART_SHIFT;
+        const uint32_t p = b >> a.bin_shift;
         const uint64_t idx = (uint64_t)base[p] + (j - start[p]);
         if (idx < a.cap) {
             a.ids[((uint64_t)copy * a.nparts + p) * a.cap + idx] = (uint16_t)(b & (PART_BUCKETS - 1));
@@ -422,14 +425,10 @@ __global__ __launch_bounds__(P1_THREADS, 4) void k_pass1(P1Args a) {
 constexpr int D13_Q = 4;                          // keys per quarter
 constexpr int D13_NQ = P1_KEYS_PER_THREAD / D13_Q;  // quarters per tile
 
-// VARIANT 0 is production.  Profiling variants (results invalid), pass-1 ms
-// per 2^31 keys at the C4 bucket count: 1 = hash only,
-// no tile epilogue (5.0 vs 7.0); 5 = scan + cursor atomics + barriers, no
-// scatter / write-out (6.4); 7 = no write-out (7.07); 6 = adds as
-// v_add_co/v_addc pairs (+3.5 %).  Private per-workgroup regions (no cursor
-// atomics) measured 8.37: a tile leaves ~60 B per partition, so private lines
-// are written partially, while the XCD-shared regions complete lines in L2.
-template <int VARIANT, int NT>
+// Kept as the reference point for k_pass1_d13e (BSDB_D13_VARIANT=2): the
+// round-1 epilogue, with its loads made unconditional and the epilogue run at
+// raised wave priority (the workgroup's critical path).
+template <int NT>
 __global__ __launch_bounds__(NT, 4) void k_pass1_d13(P1Args a, uint64_t ntiles) {
     constexpr int TILE = NT * P1_KEYS_PER_THREAD;
     __shared__ uint32_t sorted[TILE];
@@ -441,16 +440,7 @@ __global__ __launch_bounds__(NT, 4) void k_pass1_d13(P1Args a, uint64_t ntiles) 
     const uint32_t P = a.nparts;
     if (tid == 0) tile_ovf = 0;
     const uint32_t mult = (uint32_t)a.multiplier;
-    const W64 seedw = w64(a.seed);
     const uint64_t G = gridDim.x;
-    // EXACT (VARIANT >= 19): every vector-memory operation of the loop is
-    // unconditional and each wave only ever waits for its OLDEST outstanding
-    // operations (s_waitcnt vmcnt counts loads, stores and atomics together,
-    // in issue order): the cursor atomics are issued before the next tile's
-    // prefetch, the id stores before the loop head's wait for it.
-    constexpr bool EXACT = VARIANT >= 19;
-    constexpr bool PRIO = VARIANT == 12 || VARIANT == 19;
-    bool ovf_any = false;
     for (int i = tid; i < MAX_PARTS; i += NT) hist[i] = 0;
 
     uint64_t t = blockIdx.x;
@@ -459,9 +449,8 @@ __global__ __launch_bounds__(NT, 4) void k_pass1_d13(P1Args a, uint64_t ntiles) 
     // sends the ragged last tile to k_pass1<SRC_DIRECT13> (bounds-checked)
     // two register sets of D13_Q windows, alternating over the quarters
     u32x4a X[D13_Q], Y[D13_Q];
-    // Past the last tile the loads re-read tile blockIdx.x instead of being
-    // skipped: a conditional load would make the waitcnt pass merge the two
-    // paths and wait for the fresh prefetch before hashing the current quarter.
+    // past the last tile the loads re-read tile blockIdx.x (unconditional
+    // loads keep the compiler's waitcnt bookkeeping exact)
     const uint64_t t_first = blockIdx.x;
     auto load_q = [&](u32x4a(&R)[D13_Q], uint64_t tt, int q) {
         const uint64_t ts = tt < ntiles ? tt : t_first;
@@ -473,14 +462,6 @@ __global__ __launch_bounds__(NT, 4) void k_pass1_d13(P1Args a, uint64_t ntiles) 
     };
     load_q(X, t, 0);
     load_q(Y, t, 1);
-    if (EXACT) {
-        // the loop head is entered with the previous tile's 16 id stores
-        // behind the prefetch; give the first entry the same shape so the
-        // waitcnt pass needs no conservative merge there
-        uint16_t *const dummy = reinterpret_cast<uint16_t *>(a.scratch + 2048);
-#pragma unroll
-        for (int j = 0; j < P1_KEYS_PER_THREAD; ++j) dummy[j * NT + tid] = 0;
-    }
     __syncthreads();  // hist zeroed
 
     for (; t < ntiles; t += G) {
@@ -492,15 +473,12 @@ __global__ __launch_bounds__(NT, 4) void k_pass1_d13(P1Args a, uint64_t ntiles) 
                 const uint32_t kt = tid + (q * D13_Q + j) * NT;
                 const uint32_t sh = ((kt * 13u) & 3u) * 8u;  // tile0*13 is a multiple of 4
                 W64 s0, s1;
-                if (VARIANT == 6)
-                    spooky13_w(R[j].x, R[j].y, R[j].z, R[j].w, sh, seedw, s0, s1);
-                else
-                    spooky13_u(R[j].x, R[j].y, R[j].z, R[j].w, sh, a.seed, s0, s1);
+                spooky13_u(R[j].x, R[j].y, R[j].z, R[j].w, sh, a.seed, s0, s1);
                 const uint32_t b = bucket_of_w(s0, mult);
                 const int jj = q * D13_Q + j;
                 bk[jj] = b;
                 // the count's old value is this key's rank in its partition run
-                const uint32_t r = atomicAdd(&hist[b >> PART_SHIFT], 1u);
+                const uint32_t r = atomicAdd(&hist[b >> a.bin_shift], 1u);
                 if (jj & 1) rk[jj >> 1] |= r << 16; else rk[jj >> 1] = r;
             }
         };
@@ -509,25 +487,17 @@ __global__ __launch_bounds__(NT, 4) void k_pass1_d13(P1Args a, uint64_t ntiles) 
         hash_q(Y, 1);
         load_q(Y, t, 3);
         hash_q(X, 2);
-        if (!EXACT) load_q(X, t + G, 0);
+        load_q(X, t + G, 0);
         hash_q(Y, 3);
-        if (!EXACT) load_q(Y, t + G, 1);
-        if (VARIANT == 1) {
-            uint32_t x = 0;
-#pragma unroll
-            for (int j = 0; j < P1_KEYS_PER_THREAD; ++j) x ^= bk[j];
-            if (x == 0xFFFFFFFFu) a.overflow[1] = x;  // keep the hashes live
-            continue;
-        }
-        if (PRIO) __builtin_amdgcn_s_setprio(2);  // epilogue = the workgroup's critical path
+        load_q(Y, t + G, 1);
+        __builtin_amdgcn_s_setprio(2);  // the epilogue is the workgroup's critical path
         __syncthreads();  // all hist adds of this tile done
         // Regions are shared by the workgroups of one XCD (copy = t % 8: tiles
         // are dealt round-robin, so copy c is written from one XCD's L2, where
         // consecutive reservations by different workgroups complete 128-byte
         // lines quickly).  The returning cursor atomic overlaps the LDS scatter.
         const uint32_t copy = (uint32_t)(t & (NCOPY - 1));
-        // element offsets below are relative to this tile's region set
-        // (P*cap < 2^32: checked by the host plan)
+        // element offsets below are relative to this tile's region set (P*cap < 2^32)
         uint16_t *const tile_base = a.ids + (uint64_t)copy * P * a.cap;
         // partitions p = tid and p = tid + NT (P <= 2*NT)
         const uint32_t p0 = tid, p1 = tid + NT;
@@ -536,30 +506,22 @@ __global__ __launch_bounds__(NT, 4) void k_pass1_d13(P1Args a, uint64_t ntiles) 
         const uint32_t e0 = block_excl_scan_n<NT>(c0 + c1, wsum, tid, total);
         const uint32_t e1 = e0 + c0;
         uint32_t b0 = 0, b1 = 0;
-        if (EXACT) {
-            // every lane adds (0 to a scratch word when it has no partition)
-            uint32_t *const wgs = a.scratch + P1_SCRATCH_WG + blockIdx.x * 1024;  // this workgroup's own words
-            b0 = atomicAdd(p0 < P ? a.cursor + copy * P + p0 : wgs + p0, c0);
-            b1 = atomicAdd(p1 < P ? a.cursor + copy * P + p1 : wgs + (p1 & 1023), c1);
-            load_q(X, t + G, 0);
-            load_q(Y, t + G, 1);
-        }
         if (p0 < P) {
             run[p0] = e0;  // partition start in the sorted tile (read-only below)
             hist[p0] = 0;  // ready for the next tile
-            if (!EXACT && c0) b0 = atomicAdd(a.cursor + copy * P + p0, c0);
+            if (c0) b0 = atomicAdd(a.cursor + copy * P + p0, c0);
         }
         if (p1 < P) {
             run[p1] = e1;
             hist[p1] = 0;
-            if (!EXACT && c1) b1 = atomicAdd(a.cursor + copy * P + p1, c1);
+            if (c1) b1 = atomicAdd(a.cursor + copy * P + p1, c1);
         }
         __syncthreads();
         // scatter: slot = start[p] + rank (plain LDS reads, broadcast on equal p)
 #pragma unroll
         for (int j = 0; j < P1_KEYS_PER_THREAD; ++j) {
             const uint32_t r = (rk[j >> 1] >> ((j & 1) * 16)) & 0xFFFFu;
-            if (VARIANT != 5) sorted[run[bk[j] >> PART_SHIFT] + r] = bk[j];
+            sorted[run[bk[j] >> a.bin_shift] + r] = bk[j];
         }
         if (p0 < P) {
             if ((uint64_t)b0 + c0 > a.cap) tile_ovf = 1;
@@ -572,29 +534,14 @@ __global__ __launch_bounds__(NT, 4) void k_pass1_d13(P1Args a, uint64_t ntiles) 
             off32[p1] = (uint32_t)((uint64_t)p1 * a.cap + b1 - e1);
         }
         __syncthreads();
-        if (EXACT) {
-            // unconditional stores: an overflowing tile writes element 0 of its
-            // region set (garbage, the chunk is recounted) instead of past cap
-            const bool ovf = tile_ovf;
-            ovf_any |= ovf;
-            uint32_t sb[P1_KEYS_PER_THREAD];
-#pragma unroll
-            for (int j = 0; j < P1_KEYS_PER_THREAD; ++j) sb[j] = sorted[tid + j * NT];
-            uint32_t so[P1_KEYS_PER_THREAD];
-#pragma unroll
-            for (int j = 0; j < P1_KEYS_PER_THREAD; ++j) so[j] = off32[sb[j] >> PART_SHIFT];
-#pragma unroll
-            for (int j = 0; j < P1_KEYS_PER_THREAD; ++j)
-                tile_base[ovf ? 0 : (uint64_t)(so[j] + tid + j * NT)] = (uint16_t)(sb[j] & (PART_BUCKETS - 1));
-        } else if (VARIANT == 5 || VARIANT == 7) {
-        } else if (!tile_ovf) {
+        if (!tile_ovf) {
             // batched: 16 sorted reads, 16 offset reads, 16 two-byte stores
             uint32_t sb[P1_KEYS_PER_THREAD];
 #pragma unroll
             for (int j = 0; j < P1_KEYS_PER_THREAD; ++j) sb[j] = sorted[tid + j * NT];
             uint32_t so[P1_KEYS_PER_THREAD];
 #pragma unroll
-            for (int j = 0; j < P1_KEYS_PER_THREAD; ++j) so[j] = off32[sb[j] >> PART_SHIFT];
+            for (int j = 0; j < P1_KEYS_PER_THREAD; ++j) so[j] = off32[sb[j] >> a.bin_shift];
 #pragma unroll
             for (int j = 0; j < P1_KEYS_PER_THREAD; ++j)
                 tile_base[(uint64_t)(so[j] + tid + j * NT)] = (uint16_t)(sb[j] & (PART_BUCKETS - 1));
@@ -602,489 +549,13 @@ __global__ __launch_bounds__(NT, 4) void k_pass1_d13(P1Args a, uint64_t ntiles) 
             atomicOr(a.overflow, 1u);
         }
         __syncthreads();  // sorted / run / off64 reused by the next tile
-        if (PRIO) __builtin_amdgcn_s_setprio(0);
-    }
-    if (EXACT && ovf_any && tid == 0) atomicOr(a.overflow, 1u);
-}
-
-// Pass 1, 13-byte keys, two barriers per tile (k_pass1_d13b).  Same front end
-// and XCD-shared regions as k_pass1_d13; the tile epilogue is re-timed so no
-// wave waits on a returning memory operation or on a partner's scan:
-//   A  barrier: hist[cur] complete
-//      every wave scans the (<= 512) partition counts itself into its own
-//      copy runw[w] (no barrier), scatters its keys into `sorted`, and thread
-//      p issues the cursor atomic of partition p;
-//      then the next tile's first quarter is hashed (into hist[nxt]) while
-//      the atomics return; thread p writes off32[p];
-//   C  barrier: sorted / off32 complete
-//      write-out (runs of 2-byte ids into the XCD-shared regions), then
-//      hist[cur] is zeroed for the tile after next.
-// `sorted`, `off32` need no double buffer: the next scatter / off32 write is
-// behind the next A barrier, which every wave reaches after its write-out.
-// hist is double-buffered: the next tile's first quarter counts into hist[nxt]
-// while slower waves may still be scanning hist[cur].
-// STAMP (diagnostic builds only, results invalid): per-wave s_memtime sums of
-// the cycles spent in barrier A, in barrier C and in the whole loop, written
-// over counts[4*wave ..] at exit.
-template <int NT, int KQ, int WPS, int STAMP = 0, int PRIO = 0>
-__global__ __launch_bounds__(NT, WPS) void k_pass1_d13b(P1Args a, uint64_t ntiles) {
-    constexpr int TILE = NT * P1_KEYS_PER_THREAD;
-    constexpr int NQ = P1_KEYS_PER_THREAD / KQ;  // quarters per tile (even)
-    static_assert(NQ % 2 == 0, "two alternating register sets");
-    constexpr int NW = NT / 64;
-    __shared__ uint32_t sorted[TILE];
-    __shared__ __align__(16) uint32_t hist[2][MAX_PARTS];
-    __shared__ __align__(16) uint32_t runw[NW][MAX_PARTS];
-    __shared__ uint32_t off32[MAX_PARTS];
-    __shared__ uint32_t tile_ovf;
-    const int tid = threadIdx.x;
-    const int w = tid >> 6, l = tid & 63;
-    const uint32_t P = a.nparts;
-    const uint32_t mult = (uint32_t)a.multiplier;
-    const uint64_t G = gridDim.x;
-    if (tid == 0) tile_ovf = 0;
-    for (int i = tid; i < 2 * MAX_PARTS; i += NT) (&hist[0][0])[i] = 0;
-
-    uint64_t t = blockIdx.x;
-    if (t >= ntiles) return;
-    // every tile here is full and readable 3 bytes past its last key: the host
-    // sends the ragged end to k_pass1<SRC_DIRECT13> (bounds-checked)
-    u32x4a X[KQ], Y[KQ];
-    const uint64_t t_first = blockIdx.x;  // see k_pass1_d13c: unconditional loads
-    auto load_q = [&](u32x4a(&R)[KQ], uint64_t tt, int q) {
-        const uint64_t ts = tt < ntiles ? tt : t_first;
-#pragma unroll
-        for (int j = 0; j < KQ; ++j) {
-            const uint64_t byte = (ts * TILE + tid + (q * KQ + j) * NT) * 13;
-            R[j] = __builtin_nontemporal_load(reinterpret_cast<const u32x4a *>(a.keys + (byte & ~3ULL)));
-        }
-    };
-    uint32_t bk[P1_KEYS_PER_THREAD];
-    uint32_t rk[P1_KEYS_PER_THREAD / 2];  // rank within (tile, partition), two u16 per register
-    auto hash_q = [&](const u32x4a(&R)[KQ], int q, uint32_t *h) {
-#pragma unroll
-        for (int j = 0; j < KQ; ++j) {
-            const uint32_t kt = tid + (q * KQ + j) * NT;
-            const uint32_t sh = ((kt * 13u) & 3u) * 8u;  // tile0*13 is a multiple of 4
-            W64 s0, s1;
-            spooky13_u(R[j].x, R[j].y, R[j].z, R[j].w, sh, a.seed, s0, s1);
-            const uint32_t b = bucket_of_w(s0, mult);
-            const int jj = q * KQ + j;
-            bk[jj] = b;
-            // the count's old value is this key's rank in its partition run
-            const uint32_t r = atomicAdd(&h[b >> PART_SHIFT], 1u);
-            if (jj & 1) rk[jj >> 1] |= r << 16; else rk[jj >> 1] = r;
-        }
-    };
-    load_q(X, t, 0);
-    load_q(Y, t, 1);
-    __syncthreads();  // hist zeroed
-    uint32_t cur = 0;
-    uint64_t st_a = 0, st_c = 0;
-    uint32_t st_n = 0;
-    const uint64_t st_t0 = STAMP ? __builtin_amdgcn_s_memtime() : 0;
-    hash_q(X, 0, hist[cur]);
-    if (NQ > 2) load_q(X, t, 2); else load_q(X, t + G, 0);
-
-    for (; t < ntiles; t += G, cur ^= 1) {
-        // quarter q hashes from set q%2, then that set loads quarter q+2
-        // (of this tile, or of the next one)
-#pragma unroll
-        for (int q = 1; q < NQ; ++q) {
-            if (q & 1) {
-                hash_q(Y, q, hist[cur]);
-                if (q + 2 < NQ) load_q(Y, t, q + 2); else load_q(Y, t + G, q + 2 - NQ);
-            } else {
-                hash_q(X, q, hist[cur]);
-                if (q + 2 < NQ) load_q(X, t, q + 2); else load_q(X, t + G, q + 2 - NQ);
-            }
-        }
-        uint64_t ts0 = STAMP ? __builtin_amdgcn_s_memtime() : 0;
-        __syncthreads();  // A: hist[cur] complete
-        if (STAMP) {
-            const uint64_t ts1 = __builtin_amdgcn_s_memtime();
-            st_a += ts1 - ts0;
-        }
-        if (PRIO) __builtin_amdgcn_s_setprio(2);
-        // cursor reservation of partitions p0 = tid, p1 = tid + NT in the
-        // XCD-shared regions of copy t % 8 (tiles are dealt round-robin, so a
-        // copy is written from one XCD's L2), issued first to give the
-        // atomics the most time
-        const uint32_t copy = (uint32_t)(t & (NCOPY - 1));
-        const uint32_t p0 = tid, p1 = tid + NT;
-        uint32_t c0 = 0, c1 = 0, b0 = 0, b1 = 0;
-        if (p0 < P) {
-            c0 = hist[cur][p0];
-            if (c0) b0 = atomicAdd(a.cursor + copy * P + p0, c0);
-        }
-        if (p1 < P) {
-            c1 = hist[cur][p1];
-            if (c1) b1 = atomicAdd(a.cursor + copy * P + p1, c1);
-        }
-        // per-wave exclusive scan of the partition counts: lane l owns
-        // partitions 8l .. 8l+7 (entries >= P are zero)
-        {
-            const uint4 h0 = *reinterpret_cast<const uint4 *>(&hist[cur][8 * l]);
-            const uint4 h1 = *reinterpret_cast<const uint4 *>(&hist[cur][8 * l + 4]);
-            uint32_t e[8] = {0, h0.x, h0.x + h0.y, h0.x + h0.y + h0.z, 0, 0, 0, 0};
-            e[4] = e[3] + h0.w;
-            e[5] = e[4] + h1.x;
-            e[6] = e[5] + h1.y;
-            e[7] = e[6] + h1.z;
-            const uint32_t tot = e[7] + h1.w;
-            uint32_t x = tot;
-#pragma unroll
-            for (int d = 1; d < 64; d <<= 1) {
-                const uint32_t y = __shfl_up(x, d, 64);
-                if (l >= d) x += y;
-            }
-            const uint32_t base = x - tot;
-            *reinterpret_cast<uint4 *>(&runw[w][8 * l]) = make_uint4(base + e[0], base + e[1], base + e[2], base + e[3]);
-            *reinterpret_cast<uint4 *>(&runw[w][8 * l + 4]) = make_uint4(base + e[4], base + e[5], base + e[6], base + e[7]);
-        }
-        // scatter: slot = run[p] + rank (this wave's own copy of run; LDS
-        // operations of one wave complete in order)
-#pragma unroll
-        for (int j = 0; j < P1_KEYS_PER_THREAD; ++j) {
-            const uint32_t r = (rk[j >> 1] >> ((j & 1) * 16)) & 0xFFFFu;
-            sorted[runw[w][bk[j] >> PART_SHIFT] + r] = bk[j];
-        }
-        // the next tile's first quarter hashes while the atomics return
-        if (PRIO) __builtin_amdgcn_s_setprio(0);
-        if (t + G < ntiles) {
-            hash_q(X, 0, hist[cur ^ 1]);
-            if (NQ > 2) load_q(X, t + G, 2); else load_q(X, t + 2 * G, 0);
-        }
-        if (p0 < P) {
-            if ((uint64_t)b0 + c0 > a.cap) tile_ovf = 1;
-            // element offset, relative to this copy's region set, of sorted slot 0
-            off32[p0] = (uint32_t)((uint64_t)p0 * a.cap + b0 - runw[w][p0]);
-        }
-        if (p1 < P) {
-            if ((uint64_t)b1 + c1 > a.cap) tile_ovf = 1;
-            off32[p1] = (uint32_t)((uint64_t)p1 * a.cap + b1 - runw[w][p1]);
-        }
-        ts0 = STAMP ? __builtin_amdgcn_s_memtime() : 0;
-        if (PRIO) __builtin_amdgcn_s_setprio(2);
-        __syncthreads();  // C: sorted, off32 complete; every scan of hist[cur] done
-        if (STAMP) {
-            const uint64_t ts1 = __builtin_amdgcn_s_memtime();
-            st_c += ts1 - ts0;
-            ++st_n;
-        }
-        if (!tile_ovf) {
-            uint16_t *const tile_base = a.ids + (uint64_t)copy * P * a.cap;  // P*cap < 2^32 (host plan)
-            uint32_t sb[P1_KEYS_PER_THREAD];
-#pragma unroll
-            for (int j = 0; j < P1_KEYS_PER_THREAD; ++j) sb[j] = sorted[tid + j * NT];
-            uint32_t so[P1_KEYS_PER_THREAD];
-#pragma unroll
-            for (int j = 0; j < P1_KEYS_PER_THREAD; ++j) so[j] = off32[sb[j] >> PART_SHIFT];
-#pragma unroll
-            for (int j = 0; j < P1_KEYS_PER_THREAD; ++j)
-                tile_base[(uint64_t)(so[j] + tid + j * NT)] = (uint16_t)(sb[j] & (PART_BUCKETS - 1));
-        } else if (tid == 0) {
-            atomicOr(a.overflow, 1u);
-        }
-        if (p0 < P) hist[cur][p0] = 0;  // for the tile after next
-        if (p1 < P) hist[cur][p1] = 0;
-        if (PRIO) __builtin_amdgcn_s_setprio(0);
-    }
-    if (STAMP && l == 0) {
-        const uint64_t wg = (uint64_t)blockIdx.x * NW + w;
-        a.counts[4 * wg + 0] = (uint32_t)(st_a >> 4);
-        a.counts[4 * wg + 1] = (uint32_t)(st_c >> 4);
-        a.counts[4 * wg + 2] = (uint32_t)((__builtin_amdgcn_s_memtime() - st_t0) >> 4);
-        a.counts[4 * wg + 3] = st_n;
+        __builtin_amdgcn_s_setprio(0);
     }
 }
 
-// Pass 1, 13-byte keys, binned (k_pass1_d13c): ONE barrier per 16384-key tile.
-// A key's 2-byte local id goes straight from the hash into its partition's
-// LDS bin (rank from the bin counter, ds_add_rtn), so no bucket id or rank is
-// kept in registers and there is no scan, no scatter pass and no sorted copy.
-// Bins are double-buffered: while tile t hashes into bins[cur], the bins of
-// tile t-1 are written out; partition p is owned by lane p / 16 of wave
-// p % 16, which reserved p's run in the XCD-shared region with a cursor
-// atomic right after tile t-1's barrier -- a whole tile earlier -- so the
-// write-out reads the count and base with readlane and never waits on memory.
-// A bin holds 128 ids (tile share 61 +- 8, i.e. 8.6 sigma); an overflowing bin
-// raises the overflow flag and the chunk is recounted with direct atomics.
-constexpr int D13C_NT = 1024;
-constexpr int D13C_NW = D13C_NT / 64;
-constexpr int D13C_TILE = D13C_NT * P1_KEYS_PER_THREAD;  // 16384
-constexpr int D13C_CAPB = 128;                            // ids per bin
-constexpr int D13C_MAXP = 288;                            // 2 x 288 x 256 B of bins = 144 KiB
-
-template <int VARIANT>
-__global__ __launch_bounds__(D13C_NT, 1) void k_pass1_d13c(P1Args a, uint64_t ntiles) {
-    constexpr int NT = D13C_NT, NW = D13C_NW, TILE = D13C_TILE, CAPB = D13C_CAPB;
-    __shared__ __align__(16) uint16_t bins[2][D13C_MAXP * CAPB];
-    __shared__ uint32_t cnt[2][D13C_MAXP];
-    const int tid = threadIdx.x;
-    const int w = __builtin_amdgcn_readfirstlane(tid >> 6), l = tid & 63;
-    const uint32_t P = a.nparts;
-    const uint32_t mult = (uint32_t)a.multiplier;
-    const uint64_t G = gridDim.x;
-    for (int i = tid; i < 2 * D13C_MAXP; i += NT) (&cnt[0][0])[i] = 0;
-    uint64_t t = blockIdx.x;
-    if (t >= ntiles) return;
-    // partition owned by this lane (valid when < P)
-    const uint32_t my_p = (uint32_t)l * NW + w;
-    const uint32_t nj = (P + NW - 1) / NW;  // partitions per wave (upper bound)
-
-    u32x4a X[D13_Q], Y[D13_Q];
-    // Past the last tile the loads re-read tile blockIdx.x instead of being
-    // skipped: a conditional load would make the waitcnt pass merge the two
-    // paths and wait for the fresh prefetch before hashing the current quarter.
-    const uint64_t t_first = blockIdx.x;
-    auto load_q = [&](u32x4a(&R)[D13_Q], uint64_t tt, int q) {
-        const uint64_t ts = tt < ntiles ? tt : t_first;
-#pragma unroll
-        for (int j = 0; j < D13_Q; ++j) {
-            const uint64_t byte = (ts * TILE + tid + (q * D13_Q + j) * NT) * 13;
-            R[j] = __builtin_nontemporal_load(reinterpret_cast<const u32x4a *>(a.keys + (byte & ~3ULL)));
-        }
-    };
-    bool bin_ovf = false;
-    auto hash_q = [&](const u32x4a(&R)[D13_Q], int q, uint32_t cur) {
-#pragma unroll
-        for (int j = 0; j < D13_Q; ++j) {
-            const uint32_t kt = tid + (q * D13_Q + j) * NT;
-            const uint32_t sh = ((kt * 13u) & 3u) * 8u;  // tile0*13 is a multiple of 4
-            W64 s0, s1;
-            spooky13_u(R[j].x, R[j].y, R[j].z, R[j].w, sh, a.seed, s0, s1);
-            const uint32_t b = bucket_of_w(s0, mult);
-            const uint32_t p = b >> PART_SHIFT;
-            const uint32_t r = atomicAdd(&cnt[cur][p], 1u);
-            // branch-free: an overflowing bin (flagged; the chunk is
-            // recounted) keeps overwriting its last slot
-            bins[cur][p * CAPB + (r < CAPB ? r : CAPB - 1)] = (uint16_t)(b & (PART_BUCKETS - 1));
-            bin_ovf |= r >= CAPB;
-        }
-    };
-    // owner state of the previous tile: count and cursor base of partition my_p
-    uint32_t c_prev = 0, b_prev = 0, copy_prev = 0;
-    bool have_prev = false, cap_ovf = false;
-    // EXACT (VARIANT 2): a fixed number of unconditional stores / atomics
-    // per tile (lanes with nothing to write store to a scratch word), so the
-    // waitcnt pass counts the loop head exactly and no wave waits for its
-    // own id stores before hashing.
-    constexpr bool EXACT = VARIANT == 2;
-    constexpr uint32_t MAXJ = (D13C_MAXP + NW - 1) / NW;
-    uint16_t *const dummy = reinterpret_cast<uint16_t *>(a.scratch + 2048);
-    auto write_out_exact = [&](uint32_t prev) {
-        uint16_t *const rbase = a.ids + (uint64_t)copy_prev * P * a.cap;  // P*cap < 2^32 (host plan)
-        const uint16_t *const bp = bins[prev];
-        if (my_p < P && (uint64_t)b_prev + c_prev > a.cap) cap_ovf = true;
-#pragma unroll
-        for (uint32_t j = 0; j < MAXJ; ++j) {
-            const uint32_t p = j * NW + w;
-            uint32_t c = (uint32_t)__builtin_amdgcn_readlane(c_prev, j);
-            const uint32_t b = (uint32_t)__builtin_amdgcn_readlane(b_prev, j);
-            c = c < (uint32_t)CAPB ? c : (uint32_t)CAPB;
-            if (p >= P || (uint64_t)b + c > a.cap) c = 0;
-            const uint32_t ps = p < P ? p : 0;
-            const uint16_t v0 = bp[ps * CAPB + l], v1 = bp[ps * CAPB + 64 + l];
-            const uint32_t base = ps * (uint32_t)a.cap + b;
-            uint16_t *const d0 = (uint32_t)l < c ? rbase + base + l : dummy + tid;
-            uint16_t *const d1 = (uint32_t)l + 64 < c ? rbase + base + 64 + l : dummy + tid;
-            *d0 = v0;
-            *d1 = v1;
-        }
-    };
-    auto write_out = [&](uint32_t prev) {
-        uint16_t *const rbase = a.ids + (uint64_t)copy_prev * P * a.cap;  // P*cap < 2^32 (host plan)
-        const uint16_t *const bp = bins[prev];
-        if (my_p < P && (uint64_t)b_prev + c_prev > a.cap) cap_ovf = true;
-        for (uint32_t j = 0; j < nj; ++j) {
-            const uint32_t p = j * NW + w;
-            if (p >= P) break;
-            uint32_t c = (uint32_t)__builtin_amdgcn_readlane(c_prev, j);
-            c = c < (uint32_t)CAPB ? c : (uint32_t)CAPB;
-            const uint32_t b = (uint32_t)__builtin_amdgcn_readlane(b_prev, j);
-            if ((uint64_t)b + c > a.cap) continue;  // region full: flagged above, never written past
-            const uint32_t base = p * (uint32_t)a.cap + b;
-            const uint16_t v0 = (uint32_t)l < c ? bp[p * CAPB + l] : 0;
-            const uint16_t v1 = (uint32_t)l + 64 < c ? bp[p * CAPB + 64 + l] : 0;
-            if ((uint32_t)l < c) rbase[base + l] = v0;
-            if ((uint32_t)l + 64 < c) rbase[base + 64 + l] = v1;
-        }
-    };
-
-    load_q(X, t, 0);
-    load_q(Y, t, 1);
-    if (EXACT) {
-        // same shape as the loop head: 2*MAXJ stores and one atomic behind the prefetch
-#pragma unroll
-        for (uint32_t j = 0; j < 2 * MAXJ; ++j) *(volatile uint16_t *)(dummy + tid) = 0;
-        (void)atomicAdd(a.scratch + tid, 0u);
-    }
-    __syncthreads();  // cnt zeroed
-    uint32_t cur = 0;
-    for (; t < ntiles; t += G, cur ^= 1) {
-        hash_q(X, 0, cur);
-        load_q(X, t, 2);
-        hash_q(Y, 1, cur);
-        load_q(Y, t, 3);
-        hash_q(X, 2, cur);
-        load_q(X, t + G, 0);
-        hash_q(Y, 3, cur);
-        load_q(Y, t + G, 1);
-        if (EXACT) write_out_exact(cur ^ 1);  // first tile: c_prev = 0, all to scratch
-        else if (have_prev && VARIANT != 1) write_out(cur ^ 1);
-        __syncthreads();  // bins[cur] complete; bins[cur ^ 1] written out
-        // owners: take partition my_p's count, re-arm its counter for the
-        // tile after next, reserve its run (returns during the next tile)
-        const uint32_t copy = (uint32_t)(t & (NCOPY - 1));
-        c_prev = 0;
-        b_prev = 0;
-        if (my_p < P) {
-            c_prev = cnt[cur][my_p];
-            cnt[cur][my_p] = 0;
-            if (!EXACT && c_prev && VARIANT != 1) b_prev = atomicAdd(a.cursor + copy * P + my_p, c_prev);
-        }
-        if (EXACT) b_prev = atomicAdd(my_p < P ? a.cursor + copy * P + my_p : a.scratch + tid, c_prev);
-        copy_prev = copy;
-        have_prev = true;
-    }
-    if (EXACT) write_out_exact(cur ^ 1);
-    else if (have_prev && VARIANT != 1) write_out(cur ^ 1);
-    if (bin_ovf || cap_ovf) atomicOr(a.overflow, 1u);
-}
-
-// Pass 1, 13-byte keys, warp-specialised (k_pass1_d13d) -- the production
-// kernel.  One 1024-thread workgroup per CU:
-//  * waves 0..11 hash.  A key's 2-byte partition-local id goes straight from
-//    the hash into its partition's LDS bin (rank from the bin counter), so a
-//    hashing wave keeps no bucket ids, issues no store and no global atomic:
-//    its only vector-memory operations are its key loads, four quarters deep
-//    (set q holds quarter q; the next tile's quarter q is loaded as soon as
-//    this tile's is hashed), so every s_waitcnt the compiler emits is exact.
-//  * waves 12..15 write.  After the tile's barrier a writer takes the counts
-//    of its partitions (p = w' + 4k), re-arms their bin counters, reserves
-//    each run in the XCD-shared region of copy t % 8 with one cursor atomic,
-//    and streams the bins out while the hashers fill the other bin buffer.
-// One barrier per 12288-key tile.  A bin holds 128 ids (tile share 46 +- 7,
-// 12 sigma); an overflowing bin or region raises the overflow flag and the
-// chunk is recounted with direct atomics.
-constexpr int D13D_NT = 1024;
-constexpr int D13D_HW = 12;                                   // hashing waves
-constexpr int D13D_WW = 4;                                    // writing waves
-constexpr int D13D_HT = D13D_HW * 64;                         // hashing threads
-constexpr int D13D_TILE = D13D_HT * P1_KEYS_PER_THREAD;       // 12288
-constexpr int D13D_CAPB = 128;
-constexpr int D13D_MAXP = 288;
-
-template <int VARIANT>
-__global__ __launch_bounds__(D13D_NT, 1) void k_pass1_d13d(P1Args a, uint64_t ntiles) {
-    constexpr int CAPB = D13D_CAPB, HT = D13D_HT, TILE = D13D_TILE;
-    __shared__ __align__(16) uint16_t bins[2][D13D_MAXP * CAPB];
-    __shared__ uint32_t cnt[2][D13D_MAXP];
-    const int tid = threadIdx.x;
-    const int w = __builtin_amdgcn_readfirstlane(tid >> 6), l = tid & 63;  // wave index in an SGPR
-    const uint32_t P = a.nparts;
-    const uint64_t G = gridDim.x;
-    for (int i = tid; i < 2 * D13D_MAXP; i += D13D_NT) (&cnt[0][0])[i] = 0;
-    const uint64_t t0 = blockIdx.x;
-    if (t0 >= ntiles) return;
-    bool ovf = false;
-    uint32_t cur = 0;
-    if (w < D13D_HW) {
-        // ---------------- hashing waves ----------------
-        const uint32_t mult = (uint32_t)a.multiplier;
-        u32x4a S[4][D13_Q];
-        // past the last tile the loads re-read tile t0 (unconditional: keeps
-        // the compiler's waitcnt bookkeeping exact)
-        auto load_q = [&](int q, uint64_t tt) {
-            const uint64_t ts = tt < ntiles ? tt : t0;
-#pragma unroll
-            for (int j = 0; j < D13_Q; ++j) {
-                const uint64_t byte = (ts * TILE + tid + (q * D13_Q + j) * HT) * 13;
-                S[q][j] = __builtin_nontemporal_load(reinterpret_cast<const u32x4a *>(a.keys + (byte & ~3ULL)));
-            }
-        };
-#pragma unroll
-        for (int q = 0; q < 4; ++q) load_q(q, t0);
-        __syncthreads();  // cnt zeroed
-        for (uint64_t t = t0; t < ntiles; t += G, cur ^= 1) {
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-#pragma unroll
-                for (int j = 0; j < D13_Q; ++j) {
-                    const uint32_t kt = tid + (q * D13_Q + j) * HT;
-                    const uint32_t sh = ((kt * 13u) & 3u) * 8u;  // tile0*13 is a multiple of 4
-                    W64 s0, s1;
-                    spooky13_u(S[q][j].x, S[q][j].y, S[q][j].z, S[q][j].w, sh, a.seed, s0, s1);
-                    const uint32_t b = bucket_of_w(s0, mult);
-                    const uint32_t p = b >> PART_SHIFT;
-                    const uint32_t r = atomicAdd(&cnt[cur][p], 1u);
-                    if (r < CAPB) bins[cur][p * CAPB + r] = (uint16_t)(b & (PART_BUCKETS - 1));
-                    else ovf = true;
-                }
-                load_q(q, t + G);
-            }
-            __syncthreads();  // bins[cur] complete; bins[cur ^ 1] written out
-        }
-    } else {
-        // ---------------- writing waves ----------------
-        const uint32_t ww = (uint32_t)(w - D13D_HW);
-        __syncthreads();  // cnt zeroed
-        for (uint64_t t = t0; t < ntiles; t += G, cur ^= 1) {
-            __syncthreads();  // bins[cur] complete
-            // partitions p = ww + 4*(64*i + lane), i = 0, 1
-            const uint32_t copy = (uint32_t)(t & (NCOPY - 1));
-            uint32_t c[2], b[2];
-#pragma unroll
-            for (int i = 0; i < 2; ++i) {
-                const uint32_t p = ww + D13D_WW * (64 * i + l);
-                c[i] = 0;
-                b[i] = 0;
-                if (p < P) {
-                    c[i] = cnt[cur][p];
-                    cnt[cur][p] = 0;  // re-armed for the tile after next
-                    if (c[i] && VARIANT != 1) b[i] = atomicAdd(a.cursor + copy * P + p, c[i]);
-                }
-            }
-            if (VARIANT == 1) continue;
-            uint16_t *const rbase = a.ids + (uint64_t)copy * P * a.cap;  // P*cap < 2^32 (host plan)
-            const uint16_t *const bp = bins[cur];
-            // batches of 4 partitions: 8 LDS reads in flight, then 8 stores
-            constexpr int BATCH = 4;
-#pragma unroll
-            for (int i = 0; i < 2; ++i) {
-                if ((uint64_t)b[i] + c[i] > a.cap) ovf = true;
-                for (uint32_t j0 = 0; j0 < 64; j0 += BATCH) {
-                    if (ww + D13D_WW * (64 * i + j0) >= P) break;
-                    uint32_t cj[BATCH], base[BATCH];
-                    uint16_t v0[BATCH], v1[BATCH];
-#pragma unroll
-                    for (int u = 0; u < BATCH; ++u) {
-                        const uint32_t p = ww + D13D_WW * (64 * i + j0 + u);
-                        uint32_t cc = p < P ? (uint32_t)__builtin_amdgcn_readlane(c[i], j0 + u) : 0;
-                        cc = cc < (uint32_t)CAPB ? cc : (uint32_t)CAPB;
-                        const uint32_t bb = (uint32_t)__builtin_amdgcn_readlane(b[i], j0 + u);
-                        if ((uint64_t)bb + cc > a.cap) cc = 0;  // full region: flagged, never written past
-                        cj[u] = cc;
-                        base[u] = p * (uint32_t)a.cap + bb;
-                        const uint32_t ps = p < P ? p : 0;  // reads stay inside the bins
-                        v0[u] = bp[ps * CAPB + l];
-                        v1[u] = bp[ps * CAPB + 64 + l];
-                    }
-#pragma unroll
-                    for (int u = 0; u < BATCH; ++u) {
-                        if ((uint32_t)l < cj[u]) rbase[base[u] + l] = v0[u];
-                        if ((uint32_t)l + 64 < cj[u]) rbase[base[u] + 64 + l] = v1[u];
-                    }
-                }
-            }
-        }
-    }
-    if (ovf) atomicOr(a.overflow, 1u);
-}
-
-// Pass 1, 13-byte keys, binned with 16-byte write-out (k_pass1_d13e).
-// One 1024-thread workgroup per CU, 16384-key tiles, ONE barrier per tile.
+// Pass 1, 13-byte keys -- the production kernel (k_pass1_d13e): binned, with
+// a 16-byte write-out.  One 1024-thread workgroup per CU, 16384-key tiles,
+// ONE barrier per tile.
 //  * Hash: a key's 2-byte partition-local id goes from the hash straight into
 //    its partition's LDS bin (rank = the bin counter's old value); no bucket
 //    id or rank is held in registers, so the four quarters of a tile live in
@@ -1105,18 +576,23 @@ __global__ __launch_bounds__(D13D_NT, 1) void k_pass1_d13d(P1Args a, uint64_t nt
 constexpr int D13E_NT = 1024;
 constexpr int D13E_NW = D13E_NT / 64;
 constexpr int D13E_TILE = D13E_NT * P1_KEYS_PER_THREAD;  // 16384
-constexpr int D13E_CAPB = 128;
-constexpr int D13E_MAXP = 288;
+constexpr int D13E_BIN_IDS = 36864;  // ids per bin buffer: nparts * capb (72 KiB, two buffers)
+constexpr int D13E_MAXP = 288;       // bins (capb >= 128 ids: tile share 57 +- 7.5 at 288 bins)
 constexpr uint16_t ID_PAD = 0xFFFF;                       // not a local id (ids are < 2^15)
 
+// VARIANT 0 is production.  Profiling only (results invalid): 1 = hash and
+// bins, no cursor atomics and no write-out; 4 = per-wave phase cycles
+// (s_memtime) written over counts[8*wave ..] (tools/stamp_probe_e.py).
 template <int VARIANT>
 __global__ __launch_bounds__(D13E_NT, 1) void k_pass1_d13e(P1Args a, uint64_t ntiles) {
-    constexpr int NT = D13E_NT, NW = D13E_NW, TILE = D13E_TILE, CAPB = D13E_CAPB;
-    __shared__ __align__(16) uint16_t bins[2][D13E_MAXP * CAPB];
+    constexpr int NT = D13E_NT, NW = D13E_NW, TILE = D13E_TILE;
+    __shared__ __align__(16) uint16_t bins[2][D13E_BIN_IDS];
     __shared__ uint32_t cnt[2][D13E_MAXP];
     const int tid = threadIdx.x;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6), l = tid & 63;
-    const uint32_t P = a.nparts;
+    const uint32_t P = a.nparts;  // bins: bucket >> bin_shift
+    const uint32_t CAPB = a.capb;  // P * CAPB <= D13E_BIN_IDS (host plan); mean fill 16384/P, CAPB >= 2.25x that
+    const uint32_t bsh = a.bin_shift;
     const uint32_t mult = (uint32_t)a.multiplier;
     const uint64_t G = gridDim.x;
     for (int i = tid; i < 2 * D13E_MAXP; i += NT) (&cnt[0][0])[i] = 0;
@@ -1148,7 +624,7 @@ __global__ __launch_bounds__(D13E_NT, 1) void k_pass1_d13e(P1Args a, uint64_t nt
             W64 s0, s1;
             spooky13_u(S[q][j].x, S[q][j].y, S[q][j].z, S[q][j].w, sh, a.seed, s0, s1);
             const uint32_t b = bucket_of_w(s0, mult);
-            const uint32_t p = b >> PART_SHIFT;
+            const uint32_t p = b >> bsh;
             const uint32_t r = atomicAdd(&cnt[cur][p], 1u);
             // branch-free: an overflowing bin (flagged below) reuses its last slot
             bins[cur][p * CAPB + (r < CAPB ? r : CAPB - 1)] = (uint16_t)(b & (PART_BUCKETS - 1));
@@ -1159,11 +635,8 @@ __global__ __launch_bounds__(D13E_NT, 1) void k_pass1_d13e(P1Args a, uint64_t nt
     auto write_out = [&](uint32_t prev) {
         // chunks (8 ids) of this wave's partitions, packed across lanes:
         // owner lane j covers chunk indices [st_j, st_j + nch_j)
-        // b_prev is first touched here, a whole tile after its atomic: a
-        // use right after the atomic would wait for the prefetch behind it.
-        // Outstanding now, oldest first: the atomic, then this tile's
-        // prefetch of quarters 0..2 (12 loads).
-        if (VARIANT != 1 && VARIANT != 6) asm volatile("s_waitcnt vmcnt(12)" : "+v"(b_prev)::"memory");
+        // b_prev is first touched here, a whole tile after its atomic (a use
+        // right after the atomic would also wait for the prefetch behind it)
         const bool fits = (uint64_t)b_prev + c8_prev <= a.cap;
         ovf |= my_p < P && !fits;
         const uint32_t nch = (my_p < P && fits) ? c8_prev / 8 : 0;
@@ -1190,13 +663,7 @@ __global__ __launch_bounds__(D13E_NT, 1) void k_pass1_d13e(P1Args a, uint64_t nt
             const uint32_t p = (uint32_t)w * PPW + j;
             if (i < total) {
                 const uint4 v = *reinterpret_cast<const uint4 *>(&bins[prev][p * CAPB + 8 * k]);
-                if (VARIANT == 2) {
-                    if (v.x == 0x12345678u) a.overflow[1] = v.y;  // keep the read live
-                } else if (VARIANT == 3) {
-                    *reinterpret_cast<uint4 *>(a.ids + ((uint64_t)blockIdx.x * NT + tid) * 8) = v;
-                } else {
-                    *reinterpret_cast<uint4 *>(rbase + (uint64_t)p * a.cap + bj + 8 * k) = v;
-                }
+                *reinterpret_cast<uint4 *>(rbase + (uint64_t)p * a.cap + bj + 8 * k) = v;
             }
         }
     };
@@ -1226,7 +693,7 @@ __global__ __launch_bounds__(D13E_NT, 1) void k_pass1_d13e(P1Args a, uint64_t nt
         load_q(2, t + G);
         hash_q(3, cur);
         stamp(st_h);
-        if (have_prev && VARIANT != 1 && VARIANT != 5) write_out(cur ^ 1);
+        if (have_prev && VARIANT != 1) write_out(cur ^ 1);
         load_q(3, t + G);
         stamp(st_w);
         __syncthreads();  // bins[cur] complete; bins[cur ^ 1] written out
@@ -1239,22 +706,20 @@ __global__ __launch_bounds__(D13E_NT, 1) void k_pass1_d13e(P1Args a, uint64_t nt
         if (my_p < P) {
             const uint32_t c = cnt[cur][my_p];
             cnt[cur][my_p] = 0;  // the tile after next counts into it again
-            ovf |= c > CAPB - 8;
-            const uint32_t c8 = c > CAPB - 8 ? 0 : (c + 7) & ~7u;
+            ovf |= c > CAPB;
+            const uint32_t c8 = c > CAPB ? 0 : (c + 7) & ~7u;
             for (uint32_t e = c; e < c8; ++e) bins[cur][my_p * CAPB + e] = ID_PAD;
             c8_prev = c8;
         }
-        // every lane issues the atomic (0 to a scratch word without a
-        // partition): an unconditional instruction keeps the waitcnt pass
-        // exact, so the write-out's wait for it never covers the prefetch
-        // The atomic is inline asm, issued by the owner lanes only: hipcc
-        // does not count it, so no waitcnt anywhere is widened by the
-        // conditional issue; its one consumer (the write-out a tile later)
-        // waits for it with an explicit, exact vmcnt.
-        if (VARIANT != 1 && VARIANT != 6 && my_p < P) {
-            uint32_t *const addr = a.cursor + copy * P + my_p;
-            asm volatile("global_atomic_add %0, %1, %2, off sc0" : "=v"(b_prev) : "v"(addr), "v"(c8_prev) : "memory");
-        }
+        // Every lane issues the atomic -- a lane without a partition adds 0
+        // to a word of this workgroup's own scratch -- so the instruction is
+        // unconditional and the waitcnt pass counts it exactly (the
+        // write-out's wait for it then covers nothing younger).  Lanes of one
+        // instruction must not share a word: same-word lanes are serialised
+        // at the memory side (measured 6x slower).
+        if (VARIANT != 1)
+            b_prev = atomicAdd(my_p < P ? a.cursor + copy * P + my_p : a.scratch + P1_SCRATCH_WG + blockIdx.x * 1024 + tid,
+                               c8_prev);
         copy_prev = copy;
         have_prev = true;
         stamp(st_o);
@@ -1268,55 +733,8 @@ __global__ __launch_bounds__(D13E_NT, 1) void k_pass1_d13e(P1Args a, uint64_t nt
         a.counts[8 * wg + 4] = (uint32_t)((__builtin_amdgcn_s_memtime() - st_t0) >> 4);
         a.counts[8 * wg + 5] = st_n;
     }
-    if (VARIANT != 1 && VARIANT != 6) asm volatile("s_waitcnt vmcnt(0)" : "+v"(b_prev)::"memory");
     if (have_prev && VARIANT != 1) write_out(cur ^ 1);
     if (ovf) atomicOr(a.overflow, 1u);
-}
-
-// Pass 2: LDS histogram of partition p = blockIdx.y over a group of regions
-// (x / nslices) and one slice of each region (x % nslices), then one coalesced
-// atomic flush of the 32768-bucket table into counts.
-__global__ __launch_bounds__(P2_THREADS, 4) void k_pass2(const uint16_t *ids, const uint32_t *cursor,
-                                                         const uint32_t *overflow, uint64_t cap,
-                                                         uint32_t nparts, uint32_t nregions, uint32_t rpw,
-                                                         uint32_t nslices, uint32_t slice,
-                                                         uint64_t num_buckets, uint32_t *counts) {
-    __shared__ uint32_t hist[PART_BUCKETS];
-    if (*overflow) return;
-    const int tid = threadIdx.x;
-    const uint32_t p = blockIdx.y;
-    const uint32_t grp = blockIdx.x / nslices, sl = blockIdx.x % nslices;
-    const uint32_t r0 = grp * rpw, r1 = min(nregions, r0 + rpw);
-    const uint64_t lo = (uint64_t)sl * slice;
-    bool any = false;
-    for (uint32_t r = r0; r < r1; ++r) any |= min((uint64_t)cursor[(uint64_t)r * nparts + p], cap) > lo;
-    if (!any) return;
-    for (int i = tid; i < PART_BUCKETS; i += P2_THREADS) hist[i] = 0;
-    __syncthreads();
-    for (uint32_t r = r0; r < r1; ++r) {
-        const uint64_t fill = min((uint64_t)cursor[(uint64_t)r * nparts + p], cap);
-        if (fill <= lo) continue;
-        const uint64_t hi = min(fill, lo + slice);
-        const uint16_t *src = ids + ((uint64_t)r * nparts + p) * cap;
-        // lo and cap are multiples of 8: 16-B aligned vectors
-        const uint64_t nvec = (hi - lo) >> 3;
-        const uint4 *v = reinterpret_cast<const uint4 *>(src + lo);
-        for (uint64_t i = tid; i < nvec; i += P2_THREADS) {
-            const uint4 w = ntload16(v + i);
-            atomicAdd(&hist[w.x & 0xFFFF], 1u); atomicAdd(&hist[w.x >> 16], 1u);
-            atomicAdd(&hist[w.y & 0xFFFF], 1u); atomicAdd(&hist[w.y >> 16], 1u);
-            atomicAdd(&hist[w.z & 0xFFFF], 1u); atomicAdd(&hist[w.z >> 16], 1u);
-            atomicAdd(&hist[w.w & 0xFFFF], 1u); atomicAdd(&hist[w.w >> 16], 1u);
-        }
-        for (uint64_t i = lo + nvec * 8 + tid; i < hi; i += P2_THREADS) atomicAdd(&hist[src[i]], 1u);
-    }
-    __syncthreads();
-    const uint64_t b0 = (uint64_t)p << PART_SHIFT;
-    const uint32_t nb = (uint32_t)min((uint64_t)PART_BUCKETS, num_buckets - b0);
-    for (uint32_t i = tid; i < nb; i += P2_THREADS) {
-        const uint32_t h = hist[i];
-        if (h) atomicAdd(counts + b0 + i, h);
-    }
 }
 
 // Fallback when pass 1 overflowed a region (adversarial key sets): recount the
@@ -1324,6 +742,7 @@ __global__ __launch_bounds__(P2_THREADS, 4) void k_pass2(const uint16_t *ids, co
 template <int SRC, int LFIX>
 __global__ __launch_bounds__(P1_THREADS) void k_overflow_fallback(P1Args a) {
     if (*a.overflow == 0) return;
+    if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(a.overflow + 2, 1u);  // bsdb_fallback_count
     const uint64_t stride = (uint64_t)gridDim.x * P1_THREADS;
     for (uint64_t gk = (uint64_t)blockIdx.x * P1_THREADS + threadIdx.x; gk < a.n; gk += stride) {
         uint64_t pos, len;
@@ -1423,10 +842,11 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan_final(const uint32_t *cou
 // slice), no tail of idle workgroups, and 4 x 16 B of ids in flight per lane.
 struct P2Layout {
     const uint16_t *ids;
-    const uint32_t *cursor;    // fills [R][P]
+    const uint32_t *cursor;    // fills [R][P] (P = region bins)
     const uint32_t *overflow;
     uint64_t cap, cap_tail;    // ids per segment of a main / tail region
     uint32_t nparts, nmain, ntail;
+    uint32_t bshift;           // bins per pass-2 partition = 2^bshift (bin = bucket >> (15 - bshift))
     uint64_t num_buckets;
     uint32_t *counts;
 };
@@ -1436,37 +856,42 @@ __device__ __forceinline__ uint64_t p2_seg_base(const P2Layout &L, uint32_t p, u
                        : (uint64_t)L.nmain * L.nparts * L.cap + ((uint64_t)(r - L.nmain) * L.nparts + p) * L.cap_tail;
 }
 
-constexpr int P2_ITEMS_PER_THREAD = 16;  // items <= 1024*16: P*R <= 16384
+constexpr int P2_ITEMS_PER_THREAD = 8;
 
-// pref[k] = ids before item k (exclusive), pref[NI] = total.  One workgroup.
+// pref[k] = ids before item k (exclusive), pref[NI] = total.  One workgroup,
+// items in rounds of SCAN_THREADS * P2_ITEMS_PER_THREAD.
 __global__ __launch_bounds__(SCAN_THREADS) void k_pass2_plan(P2Layout L, uint64_t *pref) {
     __shared__ uint64_t wsum[SCAN_THREADS / 64];
     const uint32_t R = L.nmain + L.ntail, NI = L.nparts * R;
     const int tid = threadIdx.x;
-    uint64_t f[P2_ITEMS_PER_THREAD], s = 0;
+    uint64_t carry = 0;
+    for (uint32_t base = 0; base < NI; base += SCAN_THREADS * P2_ITEMS_PER_THREAD) {
+        uint64_t f[P2_ITEMS_PER_THREAD], s = 0;
 #pragma unroll
-    for (int j = 0; j < P2_ITEMS_PER_THREAD; ++j) {
-        const uint32_t k = tid * P2_ITEMS_PER_THREAD + j;
-        f[j] = 0;
-        if (k < NI) {
-            const uint32_t p = k / R, r = k % R;
-            f[j] = min((uint64_t)L.cursor[(uint64_t)r * L.nparts + p], r < L.nmain ? L.cap : L.cap_tail);
+        for (int j = 0; j < P2_ITEMS_PER_THREAD; ++j) {
+            const uint32_t k = base + tid * P2_ITEMS_PER_THREAD + j;
+            f[j] = 0;
+            if (k < NI) {
+                const uint32_t p = k / R, r = k % R;
+                f[j] = min((uint64_t)L.cursor[(uint64_t)r * L.nparts + p], r < L.nmain ? L.cap : L.cap_tail);
+            }
+            s += f[j];
         }
-        s += f[j];
-    }
-    uint64_t tot;
-    uint64_t run = block_excl_scan64(s, wsum, tid, tot);
+        uint64_t tot;
+        uint64_t run = carry + block_excl_scan64(s, wsum, tid, tot);  // ends with a barrier
 #pragma unroll
-    for (int j = 0; j < P2_ITEMS_PER_THREAD; ++j) {
-        const uint32_t k = tid * P2_ITEMS_PER_THREAD + j;
-        if (k < NI) pref[k] = run;
-        run += f[j];
+        for (int j = 0; j < P2_ITEMS_PER_THREAD; ++j) {
+            const uint32_t k = base + tid * P2_ITEMS_PER_THREAD + j;
+            if (k < NI) pref[k] = run;
+            run += f[j];
+        }
+        carry += tot;
     }
-    if (tid == 0) pref[NI] = tot;
+    if (tid == 0) pref[NI] = carry;
 }
 
 __global__ __launch_bounds__(P2_THREADS, 1) void k_pass2b(P2Layout L, const uint64_t *pref) {
-    __shared__ uint32_t hist[PART_BUCKETS];
+    __shared__ uint32_t hist[PART_BUCKETS + 64];  // + per-lane sinks for pads
     __shared__ uint32_t k_start;
     if (*L.overflow) return;
     const int tid = threadIdx.x;
@@ -1502,16 +927,17 @@ __global__ __launch_bounds__(P2_THREADS, 1) void k_pass2b(P2Layout L, const uint
         if (pk >= hi) break;
         const uint64_t a = max(lo, pk) - pk, b = min(hi, pk1) - pk;
         if (a >= b) continue;
-        const uint32_t p = k / R, r = k % R;
-        if ((int64_t)p != cur_p) {
+        const uint32_t p = k / R, r = k % R;  // bin p of pass-2 partition p >> bshift
+        if ((int64_t)(p >> L.bshift) != cur_p) {
             if (cur_p >= 0) flush((uint32_t)cur_p);
-            cur_p = p;
+            cur_p = p >> L.bshift;
         }
         // segment base is a multiple of 64 ids: 16-byte vectors from a8 on
         const uint16_t *src = L.ids + p2_seg_base(L, p, r);
         const uint64_t a8 = min(b, (a + 7) & ~7ULL), b8 = max(a8, b & ~7ULL);
-        // an id with the top bit set is a pad (ID_PAD): it adds 0
-        auto add_id = [&](uint32_t id) { atomicAdd(&hist[id & 0x7FFF], 1u - (id >> 15)); };
+        // an id with the top bit set is a pad (ID_PAD): it goes to a per-lane
+        // sink word (pads of one wave on one word would serialise)
+        auto add_id = [&](uint32_t id) { atomicAdd(&hist[id < 0x8000u ? id : PART_BUCKETS + (tid & 63)], 1u); };
         if (a + tid < a8) add_id(src[a + tid]);
         if (b8 + tid < b) add_id(src[b8 + tid]);
         const uint4 *v = reinterpret_cast<const uint4 *>(src);

@@ -42,6 +42,7 @@ SIGNATURES = [
     ("bsdb_set_histogram_mode", _i, [_vp, _i]),
     ("bsdb_set_frontend", _i, [_vp, _i]),
     ("bsdb_set_chunk_keys", _i, [_vp, _u64]),
+    ("bsdb_fallback_count", _i, [_vp, C.POINTER(_u64)]),
     ("bsdb_set_profiling", _i, [_vp, _i]),
     ("bsdb_profile_read", _i, [_vp, _i, C.POINTER(C.c_double), C.POINTER(_u64), C.POINTER(_u64)]),
     ("bsdb_histogram_fixed", _i, [_vp, _vp, _u32, _u64, _u64, _u64, _vp]),
@@ -136,6 +137,12 @@ class Context:
 
     def set_chunk_keys(self, n: int):
         _check("bsdb_set_chunk_keys", lib().bsdb_set_chunk_keys(self._h, n))
+
+    def fallback_count(self) -> int:
+        """Chunks recounted by the overflow fallback since open (synchronises)."""
+        v = C.c_uint64()
+        _check("bsdb_fallback_count", lib().bsdb_fallback_count(self._h, C.byref(v)))
+        return v.value
 
     # ---- live per-kernel timing (HIP events on the launch stream)
     PASS1, PASS2, SCAN = 0, 1, 2

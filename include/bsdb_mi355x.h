@@ -139,6 +139,10 @@ int bsdb_set_histogram_mode(bsdb_ctx *ctx, int mode);
 int bsdb_set_frontend(bsdb_ctx *ctx, int frontend);
 /* Per-chunk key count of the partitioned path (0 = default). */
 int bsdb_set_chunk_keys(bsdb_ctx *ctx, uint64_t chunk_keys);
+/* Chunks the partitioned path recounted with direct atomics since open
+ * because a partition region or LDS bin overflowed (adversarial key sets,
+ * e.g. many duplicates).  Synchronises the device.  0 for normal inputs. */
+int bsdb_fallback_count(bsdb_ctx *ctx, uint64_t *out);
 
 /* Live per-kernel timing with HIP events recorded on the launch stream around
  * every pass-1 (hash+partition) and pass-2 (partition histogram) launch.

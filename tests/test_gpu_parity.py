@@ -143,9 +143,23 @@ def test_histogram_overflow_fallback(ctx):
     n = 1_000_000
     keys = np.tile(np.frombuffer(b"abcdefghijklm", np.uint8), n)
     m = 8_795_859
+    before = ctx.fallback_count()
     counts = ctx.histogram_fixed(dev(keys), 13, m).cpu().numpy().view(np.uint32)
     b = O.bucket(O.spooky_short(b"abcdefghijklm")[0], m)
     assert counts[b] == n and counts.sum() == n
+    assert ctx.fallback_count() > before  # the LDS bin / region overflow was detected
+
+
+@pytest.mark.parametrize("m", [1, 2, 300, 667, 66_667, 666_667, 8_795_859, 9_437_185, 20_000_000])
+def test_binned_layouts_no_fallback(ctx, m):
+    # every bucket count m maps to a bin layout (bucket >> shift, <= 288 bins)
+    # or to the sort kernel; random distinct keys never take the fallback
+    n = 3 * 16384 + 1234
+    keys = O.gen_keys13(4242, n)
+    before = ctx.fallback_count()
+    counts = ctx.histogram_fixed(dev(keys), 13, m).cpu().numpy().view(np.uint32)
+    np.testing.assert_array_equal(counts, O.histogram_fixed(keys, 13, m))
+    assert ctx.fallback_count() == before
 
 
 def test_empty_and_tiny(ctx):
@@ -192,7 +206,9 @@ def test_full_size_properties(ctx):
     n = 400_000_000
     keys = ctx.gen_keys13(0, n)
     m = O.num_buckets(n)
+    f0 = ctx.fallback_count()
     c_part = ctx.histogram_fixed(keys, 13, m, n=n)
+    assert ctx.fallback_count() == f0  # the fast path, not the overflow recount
     ctx.set_histogram_mode(2)
     try:
         c_atom = ctx.histogram_fixed(keys, 13, m, n=n)
