@@ -165,37 +165,45 @@ uint64_t round64(double x) { return ((uint64_t)x + 63) & ~63ULL; }
 
 using D13Kernel = void (*)(P1Args, uint64_t);
 
-// The 13-byte pass-1 kernel a context runs (BSDB_D13_VARIANT):
-//   0 k_pass1_d13e (production), 1 its hash-and-bins-only profile (results
-//   invalid), 2 the round-1 sort kernel k_pass1_d13, 4 k_pass1_d13e with
-//   phase stamps over counts[] (results invalid).
+// The persistent pass-1 kernel a context runs.  Variable-length keys:
+// k_pass1_vare (BSDB_D13_VARIANT 1, 3: its profiling variants).  13-byte keys (BSDB_D13_VARIANT): 0 k_pass1_d13e
+// (production), 1 its hash-and-bins-only profile (results invalid), 2 the
+// round-1 sort kernel k_pass1_d13, 4 k_pass1_d13e with phase stamps over
+// counts[] (results invalid).
 struct D13Sel {
     D13Kernel k;
     int nt;             // workgroup size
     uint64_t tile;      // keys per tile
-    uint32_t maxp;      // partitions supported
+    uint32_t maxp;      // partitions (bins) supported
     bool binned;        // runs padded to 8 ids, region copies = d13_copies
+    uint32_t bin_ids;   // binned: ids per LDS bin buffer
 };
-D13Sel d13_select(const bsdb_ctx *c) {
+D13Sel d13_select(const bsdb_ctx *c, bool var = false) {
+    if (var) {
+        D13Kernel k = k_pass1_vare<0>;
+        if (c->d13_variant == 1) k = k_pass1_vare<1>;
+        if (c->d13_variant == 3) k = k_pass1_vare<3>;
+        return {k, VARE_NT, VARE_TILE, VARE_MAXP, true, VARE_BIN_IDS};
+    }
     switch (c->d13_variant) {
-        case 1: return {k_pass1_d13e<1>, D13E_NT, D13E_TILE, D13E_MAXP, true};
-        case 4: return {k_pass1_d13e<4>, D13E_NT, D13E_TILE, D13E_MAXP, true};
+        case 1: return {k_pass1_d13e<1>, D13E_NT, D13E_TILE, D13E_MAXP, true, D13E_BIN_IDS};
+        case 4: return {k_pass1_d13e<4>, D13E_NT, D13E_TILE, D13E_MAXP, true, D13E_BIN_IDS};
         case 2:
-            if (c->d13_threads == 256) return {k_pass1_d13<256>, 256, 256 * P1_KEYS_PER_THREAD, 512, false};
-            return {k_pass1_d13<512>, 512, 512 * P1_KEYS_PER_THREAD, 1024, false};
-        default: return {k_pass1_d13e<0>, D13E_NT, D13E_TILE, D13E_MAXP, true};
+            if (c->d13_threads == 256) return {k_pass1_d13<256>, 256, 256 * P1_KEYS_PER_THREAD, 512, false, 0};
+            return {k_pass1_d13<512>, 512, 512 * P1_KEYS_PER_THREAD, 1024, false, 0};
+        default: return {k_pass1_d13e<0>, D13E_NT, D13E_TILE, D13E_MAXP, true, D13E_BIN_IDS};
     }
 }
 
-// Bins of the binned kernel: the smallest bin_shift with ceil(m >> shift)
-// <= D13E_MAXP, so a tile (16384 keys) fills each LDS bin to 16384/P on
-// average while a bin holds D13E_BIN_IDS/P >= 2.25x that (>= 8 sigma).
-bool binned_layout(uint64_t m, uint32_t &shift, uint32_t &nbins, uint32_t &capb) {
+// Bins of a binned kernel: the smallest bin_shift with ceil(m >> shift) <=
+// sel.maxp, so a tile fills each LDS bin to tile/P on average while a bin
+// holds bin_ids/P >= 2.25x that (>= 8 sigma).
+bool binned_layout(const D13Sel &sel, uint64_t m, uint32_t &shift, uint32_t &nbins, uint32_t &capb) {
     shift = 0;
-    while (shift <= (uint32_t)PART_SHIFT && ((m + (1ULL << shift) - 1) >> shift) > (uint64_t)D13E_MAXP) ++shift;
+    while (shift <= (uint32_t)PART_SHIFT && ((m + (1ULL << shift) - 1) >> shift) > (uint64_t)sel.maxp) ++shift;
     if (shift > (uint32_t)PART_SHIFT) return false;
     nbins = (uint32_t)((m + (1ULL << shift) - 1) >> shift);
-    capb = std::min<uint32_t>(((uint32_t)D13E_BIN_IDS / nbins) & ~7u, D13E_TILE + 8);
+    capb = std::min<uint32_t>((sel.bin_ids / nbins) & ~7u, (uint32_t)sel.tile + 8);
     return true;
 }
 
@@ -204,13 +212,12 @@ bool binned_layout(uint64_t m, uint32_t &shift, uint32_t &nbins, uint32_t &capb)
 // cap raises the overflow flag and the chunk is recounted with direct
 // atomics.  Layout of the id buffer: [nmain][P][cap], then the tail kernel's
 // [ntail][P][cap_tail].
-PartPlan plan_partitions(const bsdb_ctx *c, uint64_t chunk, uint64_t m, bool d13) {
+PartPlan plan_partitions(const bsdb_ctx *c, uint64_t chunk, uint64_t m, bool d13, const D13Sel &sel) {
     PartPlan p{};
-    const D13Sel sel = d13_select(c);
     const bool binned = d13 && sel.binned;
     p.bin_shift = PART_SHIFT;
     p.nparts = (uint32_t)((m + PART_BUCKETS - 1) / PART_BUCKETS);
-    if (binned) binned_layout(m, p.bin_shift, p.nparts, p.capb);
+    if (binned) binned_layout(sel, m, p.bin_shift, p.nparts, p.capb);
     const double frac = std::min(1.0, (double)(1ULL << p.bin_shift) / (double)m);
     p.nmain = binned ? (uint32_t)c->d13_copies : NCOPY;
     const double e = (double)chunk * frac / p.nmain;
@@ -259,11 +266,12 @@ int histogram_impl(bsdb_ctx *c, const uint8_t *keys, const uint64_t *offsets, ui
     uint64_t chunk = c->chunk_keys ? c->chunk_keys : DEFAULT_CHUNK_KEYS;
     chunk = std::max<uint64_t>(P1_TILE, chunk / P1_TILE * P1_TILE);
     chunk = std::min<uint64_t>(chunk, (n + P1_TILE - 1) / P1_TILE * P1_TILE);
-    const D13Sel sel = d13_select(c);
+    // the persistent kernels: 13-byte keys and variable-length keys
+    const D13Sel sel = d13_select(c, var);
     uint32_t bsh = 0, nb = 0, cb = 0;
-    const bool d13 = !var && key_len == 13 && c->frontend == 0 &&
-                     (sel.binned ? binned_layout(m, bsh, nb, cb) : nparts <= sel.maxp);
-    PartPlan pp = plan_partitions(c, chunk, m, d13);
+    const bool d13 = (var || key_len == 13) && c->frontend == 0 &&
+                     (sel.binned ? binned_layout(sel, m, bsh, nb, cb) : nparts <= sel.maxp);
+    PartPlan pp = plan_partitions(c, chunk, m, d13, sel);
     // the id buffer takes at most half of the device memory left (workspace
     // included); the 13-byte kernel addresses one region set (P segments)
     // with 32-bit offsets
@@ -273,7 +281,7 @@ int histogram_impl(bsdb_ctx *c, const uint8_t *keys, const uint64_t *offsets, ui
     while (chunk > 2 * P1_TILE && (pp.ids_elems() * sizeof(uint16_t) > budget ||
                                    (uint64_t)pp.nparts * pp.cap >= (1ULL << 32))) {
         chunk = std::max<uint64_t>(P1_TILE, chunk / 2 / P1_TILE * P1_TILE);
-        pp = plan_partitions(c, chunk, m, d13);
+        pp = plan_partitions(c, chunk, m, d13, sel);
     }
     const uint32_t R = pp.nmain + pp.ntail;
     int rc = grow(&c->ids, &c->ids_bytes, pp.ids_elems() * sizeof(uint16_t));
@@ -320,7 +328,26 @@ int histogram_impl(bsdb_ctx *c, const uint8_t *keys, const uint64_t *offsets, ui
         {
             ProfScope ps(c, s, 0, nk);
             const uint64_t tiles = (nk + P1_TILE - 1) / P1_TILE;
-            if (d13) {
+            if (d13 && var) {
+                // full tiles to the persistent kernel, the rest (< 1 of its
+                // tiles) to the generic kernel, in the tail regions
+                const uint64_t nfast = nk / sel.tile;
+                if (nfast) {
+                    const uint32_t grid = (uint32_t)std::min<uint64_t>(nfast, pp.grid_d13);
+                    sel.k<<<grid, sel.nt, 0, s>>>(ac, nfast);
+                }
+                const uint64_t done = nfast * sel.tile;
+                if (done < nk) {
+                    P1Args at = ac;
+                    at.offsets = ac.offsets + done;
+                    at.n = nk - done;
+                    at.ids = a.ids + (size_t)pp.nmain * pp.nparts * pp.cap;
+                    at.cursor = a.cursor + (size_t)pp.nmain * pp.nparts;
+                    at.cap = pp.cap_tail;
+                    at.nregions = pp.ntail;
+                    k_pass1<SRC_VAR, EPI_PARTITION, 1, 0><<<(uint32_t)((at.n + P1_TILE - 1) / P1_TILE), P1_THREADS, 0, s>>>(at);
+                }
+            } else if (d13) {
                 // full tiles whose 16-byte windows stay inside the chunk go to the
                 // persistent kernel; the rest (< 2 of its tiles) to the
                 // bounds-checked kernel, in the tail regions

@@ -16,6 +16,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "spooky_dev.hpp"
 
 namespace bsdb {
@@ -66,6 +68,7 @@ constexpr uint32_t P1_SCRATCH_WG = 10240;
 constexpr uint32_t P1_SCRATCH_MAXWG = 2048;
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned long long u64x2 __attribute__((ext_vector_type(2), aligned(8)));
 // 16-byte vector with 4-byte alignment: global_load_dwordx4 at a dword-aligned
 // address (the 13-byte-key windows of the direct front end).
 typedef unsigned int u32x4a __attribute__((ext_vector_type(4), aligned(4)));
@@ -734,6 +737,266 @@ __global__ __launch_bounds__(D13E_NT, 1) void k_pass1_d13e(P1Args a, uint64_t nt
         a.counts[8 * wg + 5] = st_n;
     }
     if (have_prev && VARIANT != 1) write_out(cur ^ 1);
+    if (ovf) atomicOr(a.overflow, 1u);
+}
+
+// Pass 1, variable-length keys -- k_pass1_vare: the binned design of
+// k_pass1_d13e behind a per-wave LDS-staged front end.  One 1024-thread
+// workgroup per CU, 8192-key tiles, ONE barrier per tile.
+//  * A wave takes its keys in groups of 128 consecutive keys, two adjacent
+//    keys per lane (group j of tile t: keys t*8192 + j*2048 + w*128 + 2*lane
+//    + {0, 1}); hashing two keys at once gives the hash chains ILP.
+//  * A group's bytes are one contiguous range of the blob (~2.3 KiB at the C5
+//    mean of 17.7 B): the wave copies it with 16-byte loads, 3 per lane, into
+//    its own LDS stage (no workgroup barrier), and each lane then reads the
+//    17 dwords a key of <= 64 B can touch and hashes on registers.  Offsets
+//    are loaded three groups ahead and the range two groups ahead, so HBM
+//    reads run under the hashing.
+//  * A range over 3 KiB is completed with synchronous loads; one over the
+//    5 KiB stage (mean key > 39 B) is hashed straight from global memory, as
+//    are keys over 64 B from the stage.
+//  * Bins, pads, cursor reservation and the 16-byte write-out are
+//    k_pass1_d13e's, at half its tile (so <= 144 bins of >= 2.25x their mean
+//    fill).
+constexpr int VARE_NT = 1024;
+constexpr int VARE_NW = VARE_NT / 64;
+constexpr int VARE_NG = 4;                         // groups of 128 keys per wave per tile
+constexpr int VARE_TILE = VARE_NT * 2 * VARE_NG;   // 8192 keys
+constexpr int VARE_BIN_IDS = 18432;                // ids per bin buffer (36 KiB, two buffers)
+constexpr int VARE_MAXP = 144;
+constexpr uint32_t VARE_PRE_VECS = 192;            // 16-B vectors per group prefetched (3 per lane)
+constexpr uint32_t VARE_STAGE_VECS = 320;          // 16-B vectors per wave stage (5 KiB)
+constexpr int VARE_STAGE_WORDS = VARE_STAGE_VECS * 4 + 20;  // + slack for the 17-dword key reads
+
+__device__ __forceinline__ uint64_t readfirstlane64(uint64_t x) {
+    return ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(x >> 32)) << 32) |
+           (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)x);
+}
+__device__ __forceinline__ uint64_t readlane64(uint64_t x, int l) {
+    return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(x >> 32), l) << 32) |
+           (uint32_t)__builtin_amdgcn_readlane((uint32_t)x, l);
+}
+
+// VARIANT 0 is production.  Profiling only (results invalid): 1 = no cursor
+// atomics and no write-out; 3 = also no bin inserts (front end + hash only).
+template <int VARIANT>
+__global__ __launch_bounds__(VARE_NT, 1) void k_pass1_vare(P1Args a, uint64_t ntiles) {
+    constexpr int NT = VARE_NT, NW = VARE_NW, TILE = VARE_TILE, NG = VARE_NG;
+    __shared__ __align__(16) uint16_t bins[2][VARE_BIN_IDS];
+    __shared__ uint32_t cnt[2][VARE_MAXP];
+    __shared__ __align__(16) uint32_t stage_all[NW * VARE_STAGE_WORDS];
+    const int tid = threadIdx.x;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6), l = tid & 63;
+    uint32_t *const stage = stage_all + w * VARE_STAGE_WORDS;
+    const uint32_t P = a.nparts;
+    const uint32_t CAPB = a.capb;
+    const uint32_t bsh = a.bin_shift;
+    const uint32_t mult = (uint32_t)a.multiplier;
+    const uint64_t G = gridDim.x;
+    const uintptr_t blob = (uintptr_t)a.keys;
+    for (int i = tid; i < 2 * VARE_MAXP; i += NT) (&cnt[0][0])[i] = 0;
+    const uint64_t t0 = blockIdx.x;
+    if (t0 >= ntiles) return;
+    const uint32_t PPW = (P + NW - 1) / NW;
+    const bool owner = (uint32_t)l < PPW && (uint32_t)w * PPW + l < P;
+    const uint32_t my_p = owner ? (uint32_t)w * PPW + l : P;
+
+    // A: a lane's three offsets off[k], off[k+1], off[k+2] (k = its first
+    // key), ring of 2; past the last tile, tile t0 again (unconditional loads
+    // keep the waitcnt pass exact)
+    u64x2 A01[2];
+    uint64_t A2[2];
+    uint64_t a_tile = t0;  // the tile issue_A counts groups from
+    auto issue_A = [&](int r, int g) __attribute__((always_inline)) {
+        // group g counts from group 0 of the current tile (t) onwards
+        const uint64_t tt = a_tile + (uint64_t)(g / NG) * G;
+        const uint64_t ts = tt < ntiles ? tt : t0;
+        const uint64_t k = ts * TILE + (uint64_t)(g % NG) * (NT * 2) + (uint64_t)w * 128 + 2 * l;
+        A01[r] = __builtin_nontemporal_load(reinterpret_cast<const u64x2 *>(a.offsets + k));
+        A2[r] = __builtin_nontemporal_load(a.offsets + k + 2);
+    };
+    // B: a group's byte range, 3 vectors per lane, and its keys (ring of 2)
+    u32x4 V[2][3];
+    uint64_t Bpos[2], Blo[2];
+    uint32_t Bla[2], Blb[2], Bn[2];
+    auto issue_B = [&](int r, int ra) __attribute__((always_inline)) {
+        const uint64_t first = readfirstlane64(A01[ra].x);
+        const uint64_t last = readlane64(A2[ra], 63);
+        const uintptr_t lo = (blob + first) & ~(uintptr_t)15;
+        const uint64_t nv = (blob + last - lo + 15) >> 4;  // 0: an all-empty group
+        const uint32_t nvec = nv > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)nv;
+        // an empty group reads the offsets array instead (always readable);
+        // pointers derived from the kernel arguments, not from integers, so
+        // the loads stay global_load (a flat load makes every wait a full drain)
+        const uint8_t *src = nvec ? a.keys + (lo - blob) : reinterpret_cast<const uint8_t *>(a.offsets);
+        const uint32_t nl = nvec ? nvec - 1 : 0;
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+            V[r][i] = __builtin_nontemporal_load(
+                reinterpret_cast<const u32x4 *>(src + 16 * (uint64_t)min((uint32_t)(64 * i + l), nl)));
+        Bpos[r] = A01[ra].x;
+        Bla[r] = (uint32_t)(A01[ra].y - A01[ra].x);
+        Blb[r] = (uint32_t)(A2[ra] - A01[ra].y);
+        Blo[r] = lo;
+        Bn[r] = nvec;
+    };
+    // the group's range -> this wave's stage (lanes past the range store
+    // copies of its last vector into slots no key reads)
+    auto stage_group = [&](int r) __attribute__((always_inline)) {
+#pragma unroll
+        for (int i = 0; i < 3; ++i) reinterpret_cast<u32x4 *>(stage)[64 * i + l] = V[r][i];
+        const uint32_t nvec = Bn[r];
+        if (nvec > VARE_PRE_VECS && nvec <= VARE_STAGE_VECS) {
+            for (uint32_t v = VARE_PRE_VECS + l; v < nvec; v += 64)
+                reinterpret_cast<u32x4 *>(stage)[v] =
+                    __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(a.keys + (Blo[r] - blob) + 16 * (uint64_t)v));
+        }
+    };
+    // signature word 0 of the key at blob offset pos
+    auto sig0_of = [&](uint64_t pos, uint32_t len, uintptr_t lo, uint32_t nvec, bool staged) __attribute__((always_inline)) {
+        // the key starts at byte o of the range; its dwords are read at
+        // dword-aligned offsets and funnel-shifted (bytes past the key end are
+        // masked by the hash)
+        const uint64_t o = blob + pos - lo;
+        const uint32_t sh = (uint32_t)(o & 3) * 8;
+        if (staged) {
+            const uint32_t b = (uint32_t)(o >> 2);
+            auto rd = [&](uint32_t off) -> uint64_t {
+                const uint32_t i = b + (off >> 2);
+                return funnel64(stage[i], stage[i + 1], stage[i + 2], sh);
+            };
+            return spooky_short_sig0_u(rd, len, a.seed);
+        }
+        // a range over the stage: dword loads from global memory, clamped to
+        // the range's last dword (the range's lines are readable)
+        const uint32_t *src = reinterpret_cast<const uint32_t *>(a.keys + (lo - blob));
+        const uint64_t last = 4 * (uint64_t)nvec - 1, b = o >> 2;
+        auto rd = [&](uint32_t off) -> uint64_t {
+            const uint64_t i = b + (off >> 2);
+            return funnel64(src[min(i, last)], src[min(i + 1, last)], src[min(i + 2, last)], sh);
+        };
+        return spooky_short_sig0_u(rd, len, a.seed);
+    };
+    auto insert = [&](uint64_t s0, uint32_t cur) __attribute__((always_inline)) {
+        const uint32_t bk = bucket_of_w(w64(s0), mult);
+        const uint32_t p = bk >> bsh;
+        if (VARIANT == 3) {
+            if (bk == 0xFFFFFFFFu) a.overflow[3] = 1;  // keeps the hash live
+            return;
+        }
+        const uint32_t rk = atomicAdd(&cnt[cur][p], 1u);
+        bins[cur][p * CAPB + (rk < CAPB ? rk : CAPB - 1)] = (uint16_t)(bk & (PART_BUCKETS - 1));
+    };
+    auto hash_group = [&](uint64_t pos, uint32_t la, uint32_t lb, uintptr_t lo, uint32_t nvec, uint32_t cur)
+                          __attribute__((always_inline)) {
+        const uint64_t pb = pos + la;
+        const bool staged = nvec <= VARE_STAGE_VECS;  // wave-uniform
+        uint64_t sa, sb;
+        if (staged && la <= 64 && lb <= 64) {
+            // the common case: both keys' 17 dwords read at once, then two
+            // independent hash chains on registers
+            const uint32_t oa = (uint32_t)(blob + pos - lo), ob = oa + la;
+            uint32_t da[17], db[17];
+#pragma unroll
+            for (int i = 0; i < 17; ++i) da[i] = stage[(oa >> 2) + i];
+#pragma unroll
+            for (int i = 0; i < 17; ++i) db[i] = stage[(ob >> 2) + i];
+            sa = spooky_le64_sig0(da, (oa & 3) * 8, la, a.seed);
+            sb = spooky_le64_sig0(db, (ob & 3) * 8, lb, a.seed);
+        } else {
+            sa = sig0_of(pos, la, lo, nvec, staged);
+            sb = sig0_of(pb, lb, lo, nvec, staged);
+        }
+        insert(sa, cur);
+        insert(sb, cur);
+    };
+
+    bool ovf = false;
+    uint32_t c8_prev = 0, b_prev = 0, copy_prev = 0;
+    // k_pass1_d13e's write-out: chunks of 8 ids of this wave's bins packed
+    // across lanes, one 16-byte store each
+    auto write_out = [&](uint32_t prev) __attribute__((always_inline)) {
+        const bool fits = (uint64_t)b_prev + c8_prev <= a.cap;
+        ovf |= my_p < P && !fits;
+        const uint32_t nch = (my_p < P && fits) ? c8_prev / 8 : 0;
+        uint32_t x = nch;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t y = __shfl_up(x, d, 64);
+            if (l >= d) x += y;
+        }
+        const uint32_t st = x - nch;
+        const uint32_t total = __builtin_amdgcn_readlane(x, 63);
+        uint16_t *const rbase = a.ids + (uint64_t)copy_prev * P * a.cap;
+        for (uint32_t i0 = 0; i0 < total; i0 += 64) {
+            const uint32_t i = i0 + l;
+            int j = 0;
+#pragma unroll
+            for (int step = 8; step >= 1; step >>= 1) {  // PPW <= 9 < 16
+                const uint32_t s_try = __shfl(st, j + step, 64);
+                if (s_try <= i) j += step;
+            }
+            const uint32_t bj = __shfl(b_prev, j, 64), sj = __shfl(st, j, 64);
+            const uint32_t k = i - sj;
+            const uint32_t p = (uint32_t)w * PPW + j;
+            if (i < total) {
+                const uint4 v = *reinterpret_cast<const uint4 *>(&bins[prev][p * CAPB + 8 * k]);
+                *reinterpret_cast<uint4 *>(rbase + (uint64_t)p * a.cap + bj + 8 * k) = v;
+            }
+        }
+    };
+
+    issue_A(0, 0);
+    issue_A(1, 1);
+    issue_B(0, 0);
+    issue_B(1, 1);
+    issue_A(0, 2);
+    __syncthreads();  // cnt zeroed
+    uint32_t cur = 0;
+    bool have_prev = false;
+    for (uint64_t t = t0; t < ntiles; t += G, cur ^= 1) {
+        a_tile = t;
+        // the groups unrolled by construction (a rolled loop rotates the rings
+        // with register moves, which wait for the loads in flight).  Step j:
+        // stage group j, issue group j+2's range (offsets in A slot j&1) and
+        // group j+3's offsets (into A slot (j+1)&1, freed at step j-1), hash.
+        auto group = [&](auto jc) __attribute__((always_inline)) {
+            constexpr int j = decltype(jc)::value;
+            constexpr int r = j & 1;
+            stage_group(r);
+            const uint64_t pos = Bpos[r], lo = Blo[r];
+            const uint32_t la = Bla[r], lb = Blb[r], nvec = Bn[r];
+            issue_B(r, j & 1);
+            issue_A((j + 1) & 1, j + 3);
+            __builtin_amdgcn_wave_barrier();
+            hash_group(pos, la, lb, lo, nvec, cur);
+            __builtin_amdgcn_wave_barrier();  // this stage is refilled by the next group
+        };
+        group(std::integral_constant<int, 0>{});
+        group(std::integral_constant<int, 1>{});
+        group(std::integral_constant<int, 2>{});
+        group(std::integral_constant<int, 3>{});
+        static_assert(NG == 4, "group calls above");
+        if (have_prev && VARIANT == 0) write_out(cur ^ 1);
+        __syncthreads();  // bins[cur] complete; bins[cur ^ 1] written out
+        const uint32_t copy = (uint32_t)(t & (a.ncopy - 1));
+        c8_prev = 0;
+        b_prev = 0;
+        if (my_p < P) {
+            const uint32_t c = cnt[cur][my_p];
+            cnt[cur][my_p] = 0;
+            ovf |= c > CAPB;
+            const uint32_t c8 = c > CAPB ? 0 : (c + 7) & ~7u;
+            for (uint32_t e = c; e < c8; ++e) bins[cur][my_p * CAPB + e] = ID_PAD;
+            c8_prev = c8;
+        }
+        if (VARIANT == 0)
+            b_prev = atomicAdd(my_p < P ? a.cursor + copy * P + my_p : a.scratch + P1_SCRATCH_WG + blockIdx.x * 1024 + tid,
+                               c8_prev);
+        copy_prev = copy;
+        have_prev = true;
+    }
+    if (have_prev && VARIANT == 0) write_out(cur ^ 1);
     if (ovf) atomicOr(a.overflow, 1u);
 }
 

@@ -193,6 +193,102 @@ __device__ __forceinline__ void short_end_u(uint64_t &h0, uint64_t &h1, uint64_t
 }
 #undef BSDB_END_STEP_U
 
+// spooky.c:55-68 with the adds as v_lshl_add_u64.
+#define BSDB_MIX_STEP_U(A, K, B, C) A = rotl_u<K>(A); A = add_u(A, B); C ^= A;
+__device__ __forceinline__ void short_mix_u(uint64_t &h0, uint64_t &h1, uint64_t &h2, uint64_t &h3) {
+    BSDB_MIX_STEP_U(h2, 50, h3, h0) BSDB_MIX_STEP_U(h3, 52, h0, h1) BSDB_MIX_STEP_U(h0, 30, h1, h2)
+    BSDB_MIX_STEP_U(h1, 41, h2, h3) BSDB_MIX_STEP_U(h2, 54, h3, h0) BSDB_MIX_STEP_U(h3, 48, h0, h1)
+    BSDB_MIX_STEP_U(h0, 38, h1, h2) BSDB_MIX_STEP_U(h1, 37, h2, h3) BSDB_MIX_STEP_U(h2, 62, h3, h0)
+    BSDB_MIX_STEP_U(h3, 34, h0, h1) BSDB_MIX_STEP_U(h0, 5, h1, h2)  BSDB_MIX_STEP_U(h1, 36, h2, h3)
+}
+#undef BSDB_MIX_STEP_U
+
+// spooky_short (spooky.c:94-175) in the v_lshl_add_u64 formulation, sig0 only
+// (the bucket needs nothing else).
+template <class Reader>
+__device__ __forceinline__ uint64_t spooky_short_sig0_u(const Reader &rd, uint32_t len, uint64_t seed) {
+    uint64_t h0 = seed, h1 = seed, h2 = SC, h3 = SC;
+    uint32_t rem = len & 31, off = 0;
+    if (len > 15) {
+        const uint32_t nblk = len >> 5;
+        for (uint32_t b = 0; b < nblk; ++b, off += 32) {
+            h2 = add_u(h2, rd(off));
+            h3 = add_u(h3, rd(off + 8));
+            short_mix_u(h0, h1, h2, h3);
+            h0 = add_u(h0, rd(off + 16));
+            h1 = add_u(h1, rd(off + 24));
+        }
+        if (rem >= 16) {
+            h2 = add_u(h2, rd(off));
+            h3 = add_u(h3, rd(off + 8));
+            short_mix_u(h0, h1, h2, h3);
+            off += 16;
+            rem -= 16;
+        }
+    }
+    if (rem == 0) {
+        h2 = add_u(h2, SC);
+        h3 = add_u(h3, SC);
+    } else if (rem >= 8) {
+        h2 = add_u(h2, rd(off));
+        h3 = add_u(h3, rd(off + 8) & low_bytes_mask(rem - 8));
+    } else {
+        h2 = add_u(h2, rd(off) & low_bytes_mask(rem));
+    }
+    h0 = add_u(h0, (uint64_t)len * 8);
+    short_end_u(h0, h1, h2, h3);
+    return h0;
+}
+
+// spooky_short (spooky.c:94-175) of a key of len <= 64 bytes held in
+// registers: d[0..16] are the dwords from the key's first byte rounded down
+// to 4, sh = 8 * (that byte's offset in d[0]).  With c_k = bytes [16k, 16k+16):
+//   len >= 16: h2 += c0, mix          len >= 32: h0,h1 += c1 (block 0 done)
+//   len >= 48: h2 += c2, mix          len == 64: h0,h1 += c3 (block 1 done)
+// then the tail is c_{len/16} masked to len % 16 bytes (SC twice when empty).
+__device__ __forceinline__ uint64_t spooky_le64_sig0(const uint32_t (&d)[17], uint32_t sh, uint32_t len,
+                                                     uint64_t seed) {
+    auto W = [&](int k) -> uint64_t { return funnel64(d[2 * k], d[2 * k + 1], d[2 * k + 2], sh); };
+    uint64_t h0 = seed, h1 = seed, h2 = SC, h3 = SC;
+    if (len >= 16) {
+        h2 = add_u(h2, W(0));
+        h3 = add_u(h3, W(1));
+        short_mix_u(h0, h1, h2, h3);
+        if (len >= 32) {
+            h0 = add_u(h0, W(2));
+            h1 = add_u(h1, W(3));
+        }
+        if (len >= 48) {
+            h2 = add_u(h2, W(4));
+            h3 = add_u(h3, W(5));
+            short_mix_u(h0, h1, h2, h3);
+            if (len >= 64) {
+                h0 = add_u(h0, W(6));
+                h1 = add_u(h1, W(7));
+            }
+        }
+    }
+    const uint32_t ci = len >> 4, r = len & 15;  // tail chunk (ci = 4: len 64, r = 0)
+    const uint64_t t0 = ci == 0 ? W(0) : ci == 1 ? W(2) : ci == 2 ? W(4) : W(6);
+    const uint64_t t1 = ci == 0 ? W(1) : ci == 1 ? W(3) : ci == 2 ? W(5) : W(7);
+    uint64_t x0, x1;
+    if (r == 0) {
+        x0 = SC;
+        x1 = SC;
+    } else if (r >= 8) {
+        x0 = t0;
+        x1 = t1 & low_bytes_mask(r - 8);
+    } else {
+        x0 = t0 & low_bytes_mask(r);
+        x1 = 0;
+    }
+    h2 = add_u(h2, x0);
+    h3 = add_u(h3, x1);
+    h0 = add_u(h0, (uint64_t)len * 8);
+    short_end_u(h0, h1, h2, h3);
+    return h0;
+}
+
 __device__ __forceinline__ void spooky13_u(uint32_t d0, uint32_t d1, uint32_t d2, uint32_t d3, uint32_t sh,
                                            uint64_t seed, W64 &sig0, W64 &sig1) {
     const uint64_t w0 = ((uint64_t)__builtin_amdgcn_alignbit(d2, d1, sh) << 32) | __builtin_amdgcn_alignbit(d1, d0, sh);

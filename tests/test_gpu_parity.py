@@ -437,3 +437,40 @@ def test_var_staged_long_subtiles_fall_back(ctx):
     blob = rng.integers(0, 256, int(off[-1]), dtype=np.uint8)
     sig = u64(ctx.hash_var(dev(blob), dev(off.view(np.int64))))
     np.testing.assert_array_equal(sig, O.hash_var(blob, off))
+
+
+@pytest.mark.parametrize("m", [1, 2, 5_000, 66_667, 2_666_667, 144 * 32768, 144 * 32768 + 1])
+def test_var_binned_bucket_counts(ctx, m):
+    """Persistent binned var-len kernel (k_pass1_vare) over bin layouts from 1
+    bin to its 144-bin limit (and just past it: the generic kernel) == oracle,
+    with no overflow fallback; n leaves a ragged tail for the generic kernel."""
+    n = 300_001
+    blob, off = ctx.gen_keys_var(11, n)
+    hb, ho = blob.cpu().numpy(), u64(off)
+    before = ctx.fallback_count()
+    got = ctx.histogram_var(blob, off, m).cpu().numpy().view(np.uint32)
+    np.testing.assert_array_equal(got, O.histogram_var(hb[: int(ho[-1])], ho, m))
+    assert ctx.fallback_count() == before
+
+
+def test_var_binned_ragged_groups(ctx):
+    """Groups of 64 keys whose byte range is empty, over the 2 KiB prefetch
+    (synchronous loads), or over the 4352-byte stage (hashed from global
+    memory), and keys of 0..255 bytes, at tile and group boundaries."""
+    rng = np.random.default_rng(23)
+    n = 3 * 8192 + 777
+    lens = rng.integers(8, 30, n)
+    lens[0:64] = 0                                    # an all-empty group at the start
+    lens[8192 - 32:8192 + 64] = 0                     # across a tile boundary
+    lens[9000:9640] = rng.integers(40, 65, 640)       # 2.5-4 KiB groups
+    lens[12000:12700] = rng.integers(70, 256, 700)    # > 4352-byte groups
+    lens[20000:20064] = 64                            # exactly 64 x 64 B
+    lens[-50:] = rng.integers(0, 256, 50)             # ragged tail
+    off = np.zeros(n + 1, np.uint64)
+    off[1:] = np.cumsum(lens)
+    blob = rng.integers(0, 256, int(off[-1]), dtype=np.uint8)
+    before = ctx.fallback_count()
+    for m in (3, 40_000):
+        got = ctx.histogram_var(dev(blob), dev(off.view(np.int64)), m).cpu().numpy().view(np.uint32)
+        np.testing.assert_array_equal(got, O.histogram_var(blob, off, m))
+    assert ctx.fallback_count() == before

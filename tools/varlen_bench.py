@@ -30,6 +30,7 @@ def main():
     ap.add_argument("--n", type=int, default=500_000_000)
     ap.add_argument("--total", type=int, default=4_000_000_000, help="key-set size that sets m")
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--fe", type=int, default=None, help="time only this front end (0 binned, 1 staged, 2 direct)")
     args = ap.parse_args()
     n = args.n
     m = args.total // 1500 + 1
@@ -40,7 +41,9 @@ def main():
     mean_len = total_bytes / n
     res = {"n": n, "m": m, "mean_len": mean_len, "bytes_per_key": mean_len + 8}
     counts = torch.zeros(m, dtype=torch.int32, device="cuda")
-    for fe, name in ((0, "staged"), (2, "direct")):
+    for fe, name in ((0, "binned"), (1, "staged"), (2, "direct")):
+        if args.fe is not None and fe != args.fe:
+            continue
         ctx.set_frontend(fe)
         ms = timed(lambda: ctx.histogram_var(blob, off, m, counts=counts), args.reps)
         res[f"{name}_ms"] = ms
@@ -50,7 +53,8 @@ def main():
     ctx.set_frontend(0)
     counts.zero_()
     ctx.histogram_var(blob, off, m, counts=counts)
-    assert int(counts.sum(dtype=torch.int64)) == n
+    if os.environ.get("BSDB_D13_VARIANT", "0") == "0":  # profiling variants give invalid counts
+        assert int(counts.sum(dtype=torch.int64)) == n
     print(json.dumps(res))
 
 
