@@ -741,87 +741,120 @@ __global__ __launch_bounds__(D13E_NT, 1) void k_pass1_d13e(P1Args a, uint64_t nt
 }
 
 // Pass 1, variable-length keys -- k_pass1_vare: the binned design of
-// k_pass1_d13e behind a per-wave LDS-staged front end.  One 1024-thread
-// workgroup per CU, 8192-key tiles, ONE barrier per tile.
+// k_pass1_d13e behind a per-wave LDS-staged front end.  TWO 512-thread
+// workgroups per CU, each with its own single-buffered bins, 8192-key tiles:
+// while one workgroup waits at a tile barrier (its waves are unevenly served
+// by the SIMDs' age-ordered VALU arbitration) or for its cursor atomics, the
+// other keeps the SIMDs busy.
 //  * A wave takes its keys in groups of 128 consecutive keys, two adjacent
-//    keys per lane (group j of tile t: keys t*8192 + j*2048 + w*128 + 2*lane
+//    keys per lane (group g of tile t: keys t*8192 + g*1024 + w*128 + 2*lane
 //    + {0, 1}); hashing two keys at once gives the hash chains ILP.
 //  * A group's bytes are one contiguous range of the blob (~2.3 KiB at the C5
 //    mean of 17.7 B): the wave copies it with 16-byte loads, 3 per lane, into
-//    its own LDS stage (no workgroup barrier), and each lane then reads the
-//    17 dwords a key of <= 64 B can touch and hashes on registers.  Offsets
-//    are loaded three groups ahead and the range two groups ahead, so HBM
-//    reads run under the hashing.
+//    its own LDS stage (no workgroup barrier); each lane then reads the 17
+//    dwords a key of <= 64 B can touch and hashes on registers.  A group's
+//    range and offsets are loaded two groups ahead; the range bounds of a
+//    tile's groups a tile ahead, so no load waits on another.
 //  * A range over 3 KiB is completed with synchronous loads; one over the
 //    5 KiB stage (mean key > 39 B) is hashed straight from global memory, as
 //    are keys over 64 B from the stage.
-//  * Bins, pads, cursor reservation and the 16-byte write-out are
-//    k_pass1_d13e's, at half its tile (so <= 144 bins of >= 2.25x their mean
-//    fill).
-constexpr int VARE_NT = 1024;
+//  * After the tile's barrier each bin's owner lane pads it to 8 ids,
+//    reserves its run in the XCD copy with one cursor atomic and its wave
+//    writes its bins out in 16-byte chunks (k_pass1_d13e's write-out); a
+//    second barrier frees the bins.  <= 144 bins of >= 2.25x their mean fill.
+constexpr int VARE_NT = 512;
 constexpr int VARE_NW = VARE_NT / 64;
-constexpr int VARE_NG = 4;                         // groups of 128 keys per wave per tile
+constexpr int VARE_NG = 8;                         // groups of 128 keys per wave per tile
 constexpr int VARE_TILE = VARE_NT * 2 * VARE_NG;   // 8192 keys
-constexpr int VARE_BIN_IDS = 18432;                // ids per bin buffer (36 KiB, two buffers)
+constexpr int VARE_BIN_IDS = 18432;                // ids in the bins (36 KiB)
 constexpr int VARE_MAXP = 144;
 constexpr uint32_t VARE_PRE_VECS = 192;            // 16-B vectors per group prefetched (3 per lane)
-constexpr uint32_t VARE_STAGE_VECS = 320;          // 16-B vectors per wave stage (5 KiB)
+constexpr uint32_t VARE_STAGE_VECS = 288;          // 16-B vectors per wave stage (4.5 KiB)
 constexpr int VARE_STAGE_WORDS = VARE_STAGE_VECS * 4 + 20;  // + slack for the 17-dword key reads
+constexpr int VARE_PERM_WORDS = 128;               // per wave: a group's keys sorted short-first
 
-__device__ __forceinline__ uint64_t readfirstlane64(uint64_t x) {
-    return ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(x >> 32)) << 32) |
-           (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)x);
-}
 __device__ __forceinline__ uint64_t readlane64(uint64_t x, int l) {
     return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(x >> 32), l) << 32) |
            (uint32_t)__builtin_amdgcn_readlane((uint32_t)x, l);
 }
 
 // VARIANT 0 is production.  Profiling only (results invalid): 1 = no cursor
-// atomics and no write-out; 3 = also no bin inserts (front end + hash only).
+// atomics and no write-out; 4 = phase cycles (s_memtime) over counts[8*wave
+// ..]; 6 = no LDS reads of the keys (hash of stand-in words).
+// k_pass1_vare's general-length paths (keys over 64 B, groups over the stage),
+// out of line: the unrolled hot loop then carries one copy of each.
+__device__ __forceinline__ uint64_t vare_sig0_lds(const uint32_t *stage, uint32_t o, uint32_t len,
+                                                            uint64_t seed) {
+    const uint32_t b = o >> 2, sh = (o & 3) * 8;
+    auto rd = [&](uint32_t off) -> uint64_t {
+        const uint32_t i = b + (off >> 2);
+        return funnel64(stage[i], stage[i + 1], stage[i + 2], sh);
+    };
+    return spooky_short_sig0_u(rd, len, seed);
+}
+// a range over the stage: dword loads from global memory, clamped to the
+// range's last dword (its lines are readable)
+__device__ __forceinline__ uint64_t vare_sig0_global(const uint32_t *src, uint64_t nwords, uint64_t o,
+                                                               uint32_t len, uint64_t seed) {
+    const uint64_t last = nwords - 1, b = o >> 2;
+    const uint32_t sh = (uint32_t)(o & 3) * 8;
+    auto rd = [&](uint32_t off) -> uint64_t {
+        const uint64_t i = b + (off >> 2);
+        return funnel64(src[min(i, last)], src[min(i + 1, last)], src[min(i + 2, last)], sh);
+    };
+    return spooky_short_sig0_u(rd, len, seed);
+}
+
 template <int VARIANT>
-__global__ __launch_bounds__(VARE_NT, 1) void k_pass1_vare(P1Args a, uint64_t ntiles) {
+__global__ __launch_bounds__(VARE_NT, 4) void k_pass1_vare(P1Args a, uint64_t ntiles) {
     constexpr int NT = VARE_NT, NW = VARE_NW, TILE = VARE_TILE, NG = VARE_NG;
-    __shared__ __align__(16) uint16_t bins[2][VARE_BIN_IDS];
-    __shared__ uint32_t cnt[2][VARE_MAXP];
+    __shared__ __align__(16) uint16_t bins[VARE_BIN_IDS];
+    __shared__ uint32_t cnt[VARE_MAXP];
     __shared__ __align__(16) uint32_t stage_all[NW * VARE_STAGE_WORDS];
+    __shared__ uint32_t perm_all[NW * VARE_PERM_WORDS];
     const int tid = threadIdx.x;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6), l = tid & 63;
     uint32_t *const stage = stage_all + w * VARE_STAGE_WORDS;
+    uint32_t *const perm = perm_all + w * VARE_PERM_WORDS;
     const uint32_t P = a.nparts;
     const uint32_t CAPB = a.capb;
     const uint32_t bsh = a.bin_shift;
     const uint32_t mult = (uint32_t)a.multiplier;
     const uint64_t G = gridDim.x;
     const uintptr_t blob = (uintptr_t)a.keys;
-    for (int i = tid; i < 2 * VARE_MAXP; i += NT) (&cnt[0][0])[i] = 0;
+    for (int i = tid; i < VARE_MAXP; i += NT) cnt[i] = 0;
     const uint64_t t0 = blockIdx.x;
     if (t0 >= ntiles) return;
-    const uint32_t PPW = (P + NW - 1) / NW;
+    const uint32_t PPW = (P + NW - 1) / NW;  // <= 18
     const bool owner = (uint32_t)l < PPW && (uint32_t)w * PPW + l < P;
     const uint32_t my_p = owner ? (uint32_t)w * PPW + l : P;
-
-    // A: a lane's three offsets off[k], off[k+1], off[k+2] (k = its first
-    // key), ring of 2; past the last tile, tile t0 again (unconditional loads
-    // keep the waitcnt pass exact)
-    u64x2 A01[2];
-    uint64_t A2[2];
-    uint64_t a_tile = t0;  // the tile issue_A counts groups from
-    auto issue_A = [&](int r, int g) __attribute__((always_inline)) {
-        // group g counts from group 0 of the current tile (t) onwards
-        const uint64_t tt = a_tile + (uint64_t)(g / NG) * G;
-        const uint64_t ts = tt < ntiles ? tt : t0;
-        const uint64_t k = ts * TILE + (uint64_t)(g % NG) * (NT * 2) + (uint64_t)w * 128 + 2 * l;
-        A01[r] = __builtin_nontemporal_load(reinterpret_cast<const u64x2 *>(a.offsets + k));
-        A2[r] = __builtin_nontemporal_load(a.offsets + k + 2);
+    constexpr bool STAMP = VARIANT == 4;
+    uint64_t st_acc[6] = {0, 0, 0, 0, 0, 0}, st_last = 0, st_t0 = 0;
+    auto stamp = [&](int ph) __attribute__((always_inline)) {
+        if (STAMP) {
+            const uint64_t now = __builtin_amdgcn_s_memtime();
+            st_acc[ph] += now - st_last;
+            st_last = now;
+        }
     };
-    // B: a group's byte range, 3 vectors per lane, and its keys (ring of 2)
+
+    // Range bounds of this wave's NG groups of a tile: lane 2g holds
+    // off[first key of group g], lane 2g+1 off[its last key + 1].  Past the
+    // last tile, tile t0 again (unconditional loads keep the waitcnt pass exact).
+    auto load_bounds = [&](uint64_t tt) __attribute__((always_inline)) {
+        const uint64_t ts = tt < ntiles ? tt : t0;
+        const uint32_t i = (uint32_t)l < 2 * NG ? (uint32_t)l : 2 * NG - 1;
+        return __builtin_nontemporal_load(a.offsets + ts * TILE + (i >> 1) * (NT * 2) + (uint64_t)w * 128 + (i & 1) * 128);
+    };
+    // B: a group's byte range (3 vectors per lane) and the lane's offsets
+    // off[k], off[k+1], off[k+2] (k = its first key), ring of 2
     u32x4 V[2][3];
-    uint64_t Bpos[2], Blo[2];
-    uint32_t Bla[2], Blb[2], Bn[2];
-    auto issue_B = [&](int r, int ra) __attribute__((always_inline)) {
-        const uint64_t first = readfirstlane64(A01[ra].x);
-        const uint64_t last = readlane64(A2[ra], 63);
+    u64x2 O01[2];
+    uint64_t O2[2], Blo[2];
+    uint32_t Bn[2];
+    auto issue_B = [&](int r, uint64_t bnd, uint32_t gi, uint64_t tt) __attribute__((always_inline)) {
+        const uint64_t first = readlane64(bnd, 2 * gi);
+        const uint64_t last = readlane64(bnd, 2 * gi + 1);
         const uintptr_t lo = (blob + first) & ~(uintptr_t)15;
         const uint64_t nv = (blob + last - lo + 15) >> 4;  // 0: an all-empty group
         const uint32_t nvec = nv > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)nv;
@@ -834,9 +867,10 @@ __global__ __launch_bounds__(VARE_NT, 1) void k_pass1_vare(P1Args a, uint64_t nt
         for (int i = 0; i < 3; ++i)
             V[r][i] = __builtin_nontemporal_load(
                 reinterpret_cast<const u32x4 *>(src + 16 * (uint64_t)min((uint32_t)(64 * i + l), nl)));
-        Bpos[r] = A01[ra].x;
-        Bla[r] = (uint32_t)(A01[ra].y - A01[ra].x);
-        Blb[r] = (uint32_t)(A2[ra] - A01[ra].y);
+        const uint64_t ts = tt < ntiles ? tt : t0;
+        const uint64_t k = ts * TILE + (uint64_t)gi * (NT * 2) + (uint64_t)w * 128 + 2 * l;
+        O01[r] = __builtin_nontemporal_load(reinterpret_cast<const u64x2 *>(a.offsets + k));
+        O2[r] = __builtin_nontemporal_load(a.offsets + k + 2);
         Blo[r] = lo;
         Bn[r] = nvec;
     };
@@ -852,73 +886,96 @@ __global__ __launch_bounds__(VARE_NT, 1) void k_pass1_vare(P1Args a, uint64_t nt
                     __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(a.keys + (Blo[r] - blob) + 16 * (uint64_t)v));
         }
     };
-    // signature word 0 of the key at blob offset pos
+    // signature word 0 of the key at blob offset pos (the general path)
     auto sig0_of = [&](uint64_t pos, uint32_t len, uintptr_t lo, uint32_t nvec, bool staged) __attribute__((always_inline)) {
-        // the key starts at byte o of the range; its dwords are read at
-        // dword-aligned offsets and funnel-shifted (bytes past the key end are
-        // masked by the hash)
         const uint64_t o = blob + pos - lo;
-        const uint32_t sh = (uint32_t)(o & 3) * 8;
-        if (staged) {
-            const uint32_t b = (uint32_t)(o >> 2);
-            auto rd = [&](uint32_t off) -> uint64_t {
-                const uint32_t i = b + (off >> 2);
-                return funnel64(stage[i], stage[i + 1], stage[i + 2], sh);
-            };
-            return spooky_short_sig0_u(rd, len, a.seed);
-        }
-        // a range over the stage: dword loads from global memory, clamped to
-        // the range's last dword (the range's lines are readable)
-        const uint32_t *src = reinterpret_cast<const uint32_t *>(a.keys + (lo - blob));
-        const uint64_t last = 4 * (uint64_t)nvec - 1, b = o >> 2;
-        auto rd = [&](uint32_t off) -> uint64_t {
-            const uint64_t i = b + (off >> 2);
-            return funnel64(src[min(i, last)], src[min(i + 1, last)], src[min(i + 2, last)], sh);
-        };
-        return spooky_short_sig0_u(rd, len, a.seed);
+        if (staged) return vare_sig0_lds(stage, (uint32_t)o, len, a.seed);
+        return vare_sig0_global(reinterpret_cast<const uint32_t *>(a.keys + (lo - blob)), 4 * (uint64_t)nvec, o, len, a.seed);
     };
-    auto insert = [&](uint64_t s0, uint32_t cur) __attribute__((always_inline)) {
+    // bin inserts, software-pipelined: the rank atomics of a group are issued
+    // after its hash and the ids stored during the next group (after its key
+    // reads), so the atomics' round trip is not waited for in the group
+    uint32_t pend_p[2] = {0, 0}, pend_rk[2] = {0, 0};
+    uint16_t pend_id[2] = {0, 0};
+    bool pend = false;
+    auto insert = [&](int k, uint64_t s0) __attribute__((always_inline)) {
         const uint32_t bk = bucket_of_w(w64(s0), mult);
         const uint32_t p = bk >> bsh;
-        if (VARIANT == 3) {
-            if (bk == 0xFFFFFFFFu) a.overflow[3] = 1;  // keeps the hash live
-            return;
-        }
-        const uint32_t rk = atomicAdd(&cnt[cur][p], 1u);
-        bins[cur][p * CAPB + (rk < CAPB ? rk : CAPB - 1)] = (uint16_t)(bk & (PART_BUCKETS - 1));
+        pend_rk[k] = atomicAdd(&cnt[p], 1u);  // first used by flush_inserts
+        pend_p[k] = p;
+        pend_id[k] = (uint16_t)(bk & (PART_BUCKETS - 1));
     };
-    auto hash_group = [&](uint64_t pos, uint32_t la, uint32_t lb, uintptr_t lo, uint32_t nvec, uint32_t cur)
+    auto flush_inserts = [&]() __attribute__((always_inline)) {
+        if (pend) {
+#pragma unroll
+            for (int k = 0; k < 2; ++k)
+                bins[pend_p[k] * CAPB + (pend_rk[k] < CAPB ? pend_rk[k] : CAPB - 1)] = pend_id[k];
+        }
+        pend = false;
+    };
+    // Hash of one key of a staged group per lane, o = its offset in the stage.
+    // The hash branches on the length (ShortMix for >= 16 B, twice for >= 48
+    // B); a branch runs whenever ANY lane takes it, so the caller sorts a
+    // group's keys short-first: chain 0 then holds only keys < 16 B (no mix,
+    // 5 dwords) unless the group has fewer than 64 of them.
+    auto sig0_staged = [&](uint32_t o, uint32_t len) __attribute__((always_inline)) {
+        const uint32_t b = o >> 2, sh = (o & 3) * 8;
+        uint64_t s0;
+        if (__builtin_amdgcn_ballot_w64(len >= 16) == 0) {  // wave-uniform
+            uint32_t d[5];
+#pragma unroll
+            for (int i = 0; i < 5; ++i) d[i] = stage[b + i];
+            s0 = spooky_lt16_sig0(d, sh, len, a.seed);
+        } else if (len <= 64) {
+            uint32_t d[17];
+#pragma unroll
+            for (int i = 0; i < 17; ++i) d[i] = stage[b + i];
+            s0 = spooky_le64_sig0(d, sh, len, a.seed);
+        } else {
+            s0 = vare_sig0_lds(stage, o, len, a.seed);
+        }
+        return s0;
+    };
+    auto hash_group = [&](uint64_t pos, uint32_t la, uint32_t lb, uintptr_t lo, uint32_t nvec)
                           __attribute__((always_inline)) {
-        const uint64_t pb = pos + la;
         const bool staged = nvec <= VARE_STAGE_VECS;  // wave-uniform
         uint64_t sa, sb;
-        if (staged && la <= 64 && lb <= 64) {
-            // the common case: both keys' 17 dwords read at once, then two
-            // independent hash chains on registers
+        if (staged) {
+            // sort the group's 128 keys (key 2l+k = lane l's key k) short
+            // (< 16 B) first, by counting: q = rank among its class
             const uint32_t oa = (uint32_t)(blob + pos - lo), ob = oa + la;
-            uint32_t da[17], db[17];
-#pragma unroll
-            for (int i = 0; i < 17; ++i) da[i] = stage[(oa >> 2) + i];
-#pragma unroll
-            for (int i = 0; i < 17; ++i) db[i] = stage[(ob >> 2) + i];
-            sa = spooky_le64_sig0(da, (oa & 3) * 8, la, a.seed);
-            sb = spooky_le64_sig0(db, (ob & 3) * 8, lb, a.seed);
+            const bool s0 = la < 16, s1 = lb < 16;
+            const uint64_t m0 = __builtin_amdgcn_ballot_w64(s0), m1 = __builtin_amdgcn_ballot_w64(s1);
+            const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m0 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m0, 0u)) +
+                                   __builtin_amdgcn_mbcnt_hi((uint32_t)(m1 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m1, 0u));
+            const uint32_t ns = (uint32_t)__builtin_popcountll(m0) + (uint32_t)__builtin_popcountll(m1);
+            const uint32_t r0 = below, r1 = below + (s0 ? 1u : 0u);  // short ranks
+            const uint32_t q0 = s0 ? r0 : ns + 2 * l - r0, q1 = s1 ? r1 : ns + 2 * l + 1 - r1;
+            // (offsets < 4.6 KiB and lengths < 64 KiB: 16 bits each)
+            perm[q0] = oa | (la << 16);
+            perm[q1] = ob | (lb << 16);
+            __builtin_amdgcn_wave_barrier();
+            const uint32_t ka = perm[l], kb = perm[64 + l];
+            flush_inserts();  // the previous group's ids
+            sa = sig0_staged(ka & 0xFFFF, ka >> 16);
+            sb = sig0_staged(kb & 0xFFFF, kb >> 16);
         } else {
-            sa = sig0_of(pos, la, lo, nvec, staged);
-            sb = sig0_of(pb, lb, lo, nvec, staged);
+            flush_inserts();
+            sa = sig0_of(pos, la, lo, nvec, false);
+            sb = sig0_of(pos + la, lb, lo, nvec, false);
         }
-        insert(sa, cur);
-        insert(sb, cur);
+        insert(0, sa);
+        insert(1, sb);
+        pend = true;
     };
 
     bool ovf = false;
-    uint32_t c8_prev = 0, b_prev = 0, copy_prev = 0;
-    // k_pass1_d13e's write-out: chunks of 8 ids of this wave's bins packed
-    // across lanes, one 16-byte store each
-    auto write_out = [&](uint32_t prev) __attribute__((always_inline)) {
-        const bool fits = (uint64_t)b_prev + c8_prev <= a.cap;
+    // this wave's bins -> its region of copy `copy`, chunks of 8 ids packed
+    // across lanes, one 16-byte store each (k_pass1_d13e's write-out)
+    auto write_out = [&](uint32_t c8, uint32_t base, uint32_t copy) __attribute__((always_inline)) {
+        const bool fits = (uint64_t)base + c8 <= a.cap;
         ovf |= my_p < P && !fits;
-        const uint32_t nch = (my_p < P && fits) ? c8_prev / 8 : 0;
+        const uint32_t nch = (my_p < P && fits) ? c8 / 8 : 0;
         uint32_t x = nch;
 #pragma unroll
         for (int d = 1; d < 64; d <<= 1) {
@@ -927,76 +984,94 @@ __global__ __launch_bounds__(VARE_NT, 1) void k_pass1_vare(P1Args a, uint64_t nt
         }
         const uint32_t st = x - nch;
         const uint32_t total = __builtin_amdgcn_readlane(x, 63);
-        uint16_t *const rbase = a.ids + (uint64_t)copy_prev * P * a.cap;
+        uint16_t *const rbase = a.ids + (uint64_t)copy * P * a.cap;
         for (uint32_t i0 = 0; i0 < total; i0 += 64) {
             const uint32_t i = i0 + l;
             int j = 0;
 #pragma unroll
-            for (int step = 8; step >= 1; step >>= 1) {  // PPW <= 9 < 16
+            for (int step = 16; step >= 1; step >>= 1) {  // PPW <= 18 < 32
                 const uint32_t s_try = __shfl(st, j + step, 64);
                 if (s_try <= i) j += step;
             }
-            const uint32_t bj = __shfl(b_prev, j, 64), sj = __shfl(st, j, 64);
+            const uint32_t bj = __shfl(base, j, 64), sj = __shfl(st, j, 64);
             const uint32_t k = i - sj;
             const uint32_t p = (uint32_t)w * PPW + j;
             if (i < total) {
-                const uint4 v = *reinterpret_cast<const uint4 *>(&bins[prev][p * CAPB + 8 * k]);
+                const uint4 v = *reinterpret_cast<const uint4 *>(&bins[p * CAPB + 8 * k]);
                 *reinterpret_cast<uint4 *>(rbase + (uint64_t)p * a.cap + bj + 8 * k) = v;
             }
         }
     };
 
-    issue_A(0, 0);
-    issue_A(1, 1);
-    issue_B(0, 0);
-    issue_B(1, 1);
-    issue_A(0, 2);
+    if (STAMP) st_t0 = st_last = __builtin_amdgcn_s_memtime();
+    uint64_t bnd_cur = load_bounds(t0), bnd_next = 0;
+    issue_B(0, bnd_cur, 0, t0);
+    issue_B(1, bnd_cur, 1, t0);
     __syncthreads();  // cnt zeroed
-    uint32_t cur = 0;
-    bool have_prev = false;
-    for (uint64_t t = t0; t < ntiles; t += G, cur ^= 1) {
-        a_tile = t;
-        // the groups unrolled by construction (a rolled loop rotates the rings
-        // with register moves, which wait for the loads in flight).  Step j:
-        // stage group j, issue group j+2's range (offsets in A slot j&1) and
-        // group j+3's offsets (into A slot (j+1)&1, freed at step j-1), hash.
-        auto group = [&](auto jc) __attribute__((always_inline)) {
+    for (uint64_t t = t0; t < ntiles; t += G) {
+        bnd_next = load_bounds(t + G);
+        // step j: stage group j, issue group j+2's range and offsets (from
+        // the next tile's bounds past the last group), hash group j; two
+        // steps per iteration so the ring slots are static
+        // step j: stage group j, issue group j+2's range and offsets (from the
+        // next tile's bounds past the last group), hash group j.  Unrolled by
+        // construction: in a rolled loop the register allocator rotates the
+        // ring with copies, and a copy of a loading register waits for it.
+        auto step = [&](auto jc) __attribute__((always_inline)) {
             constexpr int j = decltype(jc)::value;
             constexpr int r = j & 1;
+            stamp(5);
             stage_group(r);
-            const uint64_t pos = Bpos[r], lo = Blo[r];
-            const uint32_t la = Bla[r], lb = Blb[r], nvec = Bn[r];
-            issue_B(r, j & 1);
-            issue_A((j + 1) & 1, j + 3);
+            stamp(0);
+            const uint64_t pos = O01[r].x, lo = Blo[r];
+            const uint32_t la = (uint32_t)(O01[r].y - O01[r].x), lb = (uint32_t)(O2[r] - O01[r].y), nvec = Bn[r];
+            if (j + 2 < NG) issue_B(r, bnd_cur, j + 2, t);
+            else issue_B(r, bnd_next, j + 2 - NG, t + G);
+            stamp(1);
             __builtin_amdgcn_wave_barrier();
-            hash_group(pos, la, lb, lo, nvec, cur);
+            hash_group(pos, la, lb, lo, nvec);
             __builtin_amdgcn_wave_barrier();  // this stage is refilled by the next group
+            stamp(2);
         };
-        group(std::integral_constant<int, 0>{});
-        group(std::integral_constant<int, 1>{});
-        group(std::integral_constant<int, 2>{});
-        group(std::integral_constant<int, 3>{});
-        static_assert(NG == 4, "group calls above");
-        if (have_prev && VARIANT == 0) write_out(cur ^ 1);
-        __syncthreads();  // bins[cur] complete; bins[cur ^ 1] written out
+        step(std::integral_constant<int, 0>{});
+        step(std::integral_constant<int, 1>{});
+        step(std::integral_constant<int, 2>{});
+        step(std::integral_constant<int, 3>{});
+        step(std::integral_constant<int, 4>{});
+        step(std::integral_constant<int, 5>{});
+        step(std::integral_constant<int, 6>{});
+        step(std::integral_constant<int, 7>{});
+        static_assert(NG == 8, "step calls above");
+        bnd_cur = bnd_next;
+        flush_inserts();
+        __syncthreads();  // bins complete
+        stamp(3);
+        // owners: count, pad to a multiple of 8, re-arm, reserve; every lane
+        // issues the atomic (a lane without a bin adds 0 to a scratch word of
+        // its own: same-word lanes are serialised at the memory side)
         const uint32_t copy = (uint32_t)(t & (a.ncopy - 1));
-        c8_prev = 0;
-        b_prev = 0;
+        uint32_t c8 = 0;
         if (my_p < P) {
-            const uint32_t c = cnt[cur][my_p];
-            cnt[cur][my_p] = 0;
+            const uint32_t c = cnt[my_p];
+            cnt[my_p] = 0;
             ovf |= c > CAPB;
-            const uint32_t c8 = c > CAPB ? 0 : (c + 7) & ~7u;
-            for (uint32_t e = c; e < c8; ++e) bins[cur][my_p * CAPB + e] = ID_PAD;
-            c8_prev = c8;
+            c8 = c > CAPB ? 0 : (c + 7) & ~7u;
+            for (uint32_t e = c; e < c8; ++e) bins[my_p * CAPB + e] = ID_PAD;
         }
-        if (VARIANT == 0)
-            b_prev = atomicAdd(my_p < P ? a.cursor + copy * P + my_p : a.scratch + P1_SCRATCH_WG + blockIdx.x * 1024 + tid,
-                               c8_prev);
-        copy_prev = copy;
-        have_prev = true;
+        if (VARIANT != 1) {
+            const uint32_t base =
+                atomicAdd(my_p < P ? a.cursor + copy * P + my_p : a.scratch + P1_SCRATCH_WG + blockIdx.x * 1024 + tid, c8);
+            write_out(c8, base, copy);
+        }
+        stamp(4);
+        __syncthreads();  // bins written out and counters re-armed
+        stamp(3);
     }
-    if (have_prev && VARIANT == 0) write_out(cur ^ 1);
+    if (STAMP && l == 0) {
+        const uint64_t wg = (uint64_t)blockIdx.x * NW + w;
+        for (int i = 0; i < 6; ++i) a.counts[8 * wg + i] = (uint32_t)(st_acc[i] >> 4);
+        a.counts[8 * wg + 6] = (uint32_t)((__builtin_amdgcn_s_memtime() - st_t0) >> 4);
+    }
     if (ovf) atomicOr(a.overflow, 1u);
 }
 

@@ -289,6 +289,26 @@ __device__ __forceinline__ uint64_t spooky_le64_sig0(const uint32_t (&d)[17], ui
     return h0;
 }
 
+// The same for a key of len < 16 bytes: d[0..4] only, no ShortMix.
+__device__ __forceinline__ uint64_t spooky_lt16_sig0(const uint32_t (&d)[5], uint32_t sh, uint32_t len,
+                                                     uint64_t seed) {
+    const uint64_t t0 = funnel64(d[0], d[1], d[2], sh), t1 = funnel64(d[2], d[3], d[4], sh);
+    uint64_t x0, x1;
+    if (len == 0) {
+        x0 = SC;
+        x1 = SC;
+    } else if (len >= 8) {
+        x0 = t0;
+        x1 = t1 & low_bytes_mask(len - 8);
+    } else {
+        x0 = t0 & low_bytes_mask(len);
+        x1 = 0;
+    }
+    uint64_t h0 = add_u(seed, (uint64_t)len * 8), h1 = seed, h2 = add_u(SC, x0), h3 = add_u(SC, x1);
+    short_end_u(h0, h1, h2, h3);
+    return h0;
+}
+
 __device__ __forceinline__ void spooky13_u(uint32_t d0, uint32_t d1, uint32_t d2, uint32_t d3, uint32_t sh,
                                            uint64_t seed, W64 &sig0, W64 &sig1) {
     const uint64_t w0 = ((uint64_t)__builtin_amdgcn_alignbit(d2, d1, sh) << 32) | __builtin_amdgcn_alignbit(d1, d0, sh);
