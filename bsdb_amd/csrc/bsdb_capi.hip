@@ -166,7 +166,7 @@ uint64_t round64(double x) { return ((uint64_t)x + 63) & ~63ULL; }
 using D13Kernel = void (*)(P1Args, uint64_t);
 
 // The persistent pass-1 kernel a context runs.  Variable-length keys:
-// k_pass1_vare (BSDB_D13_VARIANT 1, 4, 6: its profiling variants).  13-byte keys (BSDB_D13_VARIANT): 0 k_pass1_d13e
+// k_pass1_vare (BSDB_D13_VARIANT 1, 4: its profiling variants).  13-byte keys (BSDB_D13_VARIANT): 0 k_pass1_d13e
 // (production), 1 its hash-and-bins-only profile (results invalid), 2 the
 // round-1 sort kernel k_pass1_d13, 4 k_pass1_d13e with phase stamps over
 // counts[] (results invalid).
@@ -183,7 +183,6 @@ D13Sel d13_select(const bsdb_ctx *c, bool var = false) {
         D13Kernel k = k_pass1_vare<0>;
         if (c->d13_variant == 1) k = k_pass1_vare<1>;
         if (c->d13_variant == 4) k = k_pass1_vare<4>;
-        if (c->d13_variant == 6) k = k_pass1_vare<6>;
         return {k, VARE_NT, VARE_TILE, VARE_MAXP, true, VARE_BIN_IDS};
     }
     switch (c->d13_variant) {

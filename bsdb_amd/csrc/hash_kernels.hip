@@ -780,7 +780,7 @@ __device__ __forceinline__ uint64_t readlane64(uint64_t x, int l) {
 
 // VARIANT 0 is production.  Profiling only (results invalid): 1 = no cursor
 // atomics and no write-out; 4 = phase cycles (s_memtime) over counts[8*wave
-// ..]; 6 = no LDS reads of the keys (hash of stand-in words).
+// ..].
 // k_pass1_vare's general-length paths (keys over 64 B, groups over the stage),
 // out of line: the unrolled hot loop then carries one copy of each.
 __device__ __forceinline__ uint64_t vare_sig0_lds(const uint32_t *stage, uint32_t o, uint32_t len,
@@ -809,7 +809,7 @@ template <int VARIANT>
 __global__ __launch_bounds__(VARE_NT, 4) void k_pass1_vare(P1Args a, uint64_t ntiles) {
     constexpr int NT = VARE_NT, NW = VARE_NW, TILE = VARE_TILE, NG = VARE_NG;
     __shared__ __align__(16) uint16_t bins[VARE_BIN_IDS];
-    __shared__ uint32_t cnt[VARE_MAXP];
+    __shared__ uint32_t cnt[2][VARE_MAXP];  // rank counters, by tile parity
     __shared__ __align__(16) uint32_t stage_all[NW * VARE_STAGE_WORDS];
     __shared__ uint32_t perm_all[NW * VARE_PERM_WORDS];
     const int tid = threadIdx.x;
@@ -822,7 +822,8 @@ __global__ __launch_bounds__(VARE_NT, 4) void k_pass1_vare(P1Args a, uint64_t nt
     const uint32_t mult = (uint32_t)a.multiplier;
     const uint64_t G = gridDim.x;
     const uintptr_t blob = (uintptr_t)a.keys;
-    for (int i = tid; i < VARE_MAXP; i += NT) cnt[i] = 0;
+    for (int i = tid; i < 2 * VARE_MAXP; i += NT) (&cnt[0][0])[i] = 0;
+    uint32_t cb = 0;  // counters of the tile being hashed
     const uint64_t t0 = blockIdx.x;
     if (t0 >= ntiles) return;
     const uint32_t PPW = (P + NW - 1) / NW;  // <= 18
@@ -901,7 +902,7 @@ __global__ __launch_bounds__(VARE_NT, 4) void k_pass1_vare(P1Args a, uint64_t nt
     auto insert = [&](int k, uint64_t s0) __attribute__((always_inline)) {
         const uint32_t bk = bucket_of_w(w64(s0), mult);
         const uint32_t p = bk >> bsh;
-        pend_rk[k] = atomicAdd(&cnt[p], 1u);  // first used by flush_inserts
+        pend_rk[k] = atomicAdd(&cnt[cb][p], 1u);  // first used by flush_inserts
         pend_p[k] = p;
         pend_id[k] = (uint16_t)(bk & (PART_BUCKETS - 1));
     };
@@ -1003,46 +1004,45 @@ __global__ __launch_bounds__(VARE_NT, 4) void k_pass1_vare(P1Args a, uint64_t nt
         }
     };
 
+    // step j of tile tt: stage group j, issue group j+2's range and offsets
+    // (from the next tile's bounds past the last group), hash group j.
+    // Unrolled by construction: in a rolled loop the register allocator
+    // rotates the ring with copies, and a copy of a loading register waits
+    // for the load.
+    uint64_t bnd_cur = 0, bnd_next = 0;
+    auto step = [&](auto jc, uint64_t tt) __attribute__((always_inline)) {
+        constexpr int j = decltype(jc)::value;
+        constexpr int r = j & 1;
+        stamp(5);
+        stage_group(r);
+        stamp(0);
+        const uint64_t pos = O01[r].x, lo = Blo[r];
+        const uint32_t la = (uint32_t)(O01[r].y - O01[r].x), lb = (uint32_t)(O2[r] - O01[r].y), nvec = Bn[r];
+        if (j + 2 < NG) issue_B(r, bnd_cur, j + 2, tt);
+        else issue_B(r, bnd_next, j + 2 - NG, tt + G);
+        stamp(1);
+        __builtin_amdgcn_wave_barrier();
+        hash_group(pos, la, lb, lo, nvec);
+        __builtin_amdgcn_wave_barrier();  // this stage is refilled by the next group
+        stamp(2);
+    };
+
     if (STAMP) st_t0 = st_last = __builtin_amdgcn_s_memtime();
-    uint64_t bnd_cur = load_bounds(t0), bnd_next = 0;
+    bnd_cur = load_bounds(t0);
     issue_B(0, bnd_cur, 0, t0);
     issue_B(1, bnd_cur, 1, t0);
     __syncthreads();  // cnt zeroed
+    bnd_next = load_bounds(t0 + G);
+    step(std::integral_constant<int, 0>{}, t0);
     for (uint64_t t = t0; t < ntiles; t += G) {
-        bnd_next = load_bounds(t + G);
-        // step j: stage group j, issue group j+2's range and offsets (from
-        // the next tile's bounds past the last group), hash group j; two
-        // steps per iteration so the ring slots are static
-        // step j: stage group j, issue group j+2's range and offsets (from the
-        // next tile's bounds past the last group), hash group j.  Unrolled by
-        // construction: in a rolled loop the register allocator rotates the
-        // ring with copies, and a copy of a loading register waits for it.
-        auto step = [&](auto jc) __attribute__((always_inline)) {
-            constexpr int j = decltype(jc)::value;
-            constexpr int r = j & 1;
-            stamp(5);
-            stage_group(r);
-            stamp(0);
-            const uint64_t pos = O01[r].x, lo = Blo[r];
-            const uint32_t la = (uint32_t)(O01[r].y - O01[r].x), lb = (uint32_t)(O2[r] - O01[r].y), nvec = Bn[r];
-            if (j + 2 < NG) issue_B(r, bnd_cur, j + 2, t);
-            else issue_B(r, bnd_next, j + 2 - NG, t + G);
-            stamp(1);
-            __builtin_amdgcn_wave_barrier();
-            hash_group(pos, la, lb, lo, nvec);
-            __builtin_amdgcn_wave_barrier();  // this stage is refilled by the next group
-            stamp(2);
-        };
-        step(std::integral_constant<int, 0>{});
-        step(std::integral_constant<int, 1>{});
-        step(std::integral_constant<int, 2>{});
-        step(std::integral_constant<int, 3>{});
-        step(std::integral_constant<int, 4>{});
-        step(std::integral_constant<int, 5>{});
-        step(std::integral_constant<int, 6>{});
-        step(std::integral_constant<int, 7>{});
-        static_assert(NG == 8, "step calls above");
-        bnd_cur = bnd_next;
+        step(std::integral_constant<int, 1>{}, t);
+        step(std::integral_constant<int, 2>{}, t);
+        step(std::integral_constant<int, 3>{}, t);
+        step(std::integral_constant<int, 4>{}, t);
+        step(std::integral_constant<int, 5>{}, t);
+        step(std::integral_constant<int, 6>{}, t);
+        step(std::integral_constant<int, 7>{}, t);
+        static_assert(NG == 8, "step calls");
         flush_inserts();
         __syncthreads();  // bins complete
         stamp(3);
@@ -1052,17 +1052,24 @@ __global__ __launch_bounds__(VARE_NT, 4) void k_pass1_vare(P1Args a, uint64_t nt
         const uint32_t copy = (uint32_t)(t & (a.ncopy - 1));
         uint32_t c8 = 0;
         if (my_p < P) {
-            const uint32_t c = cnt[my_p];
-            cnt[my_p] = 0;
+            const uint32_t c = cnt[cb][my_p];
+            cnt[cb][my_p] = 0;
             ovf |= c > CAPB;
             c8 = c > CAPB ? 0 : (c + 7) & ~7u;
             for (uint32_t e = c; e < c8; ++e) bins[my_p * CAPB + e] = ID_PAD;
         }
-        if (VARIANT != 1) {
-            const uint32_t base =
-                atomicAdd(my_p < P ? a.cursor + copy * P + my_p : a.scratch + P1_SCRATCH_WG + blockIdx.x * 1024 + tid, c8);
-            write_out(c8, base, copy);
-        }
+        uint32_t base = 0;
+        if (VARIANT != 1)
+            base = atomicAdd(my_p < P ? a.cursor + copy * P + my_p : a.scratch + P1_SCRATCH_WG + blockIdx.x * 1024 + tid, c8);
+        // while the atomics fly: step 0 of the next tile, up to its rank
+        // atomics (other counters; its ids reach the bins after the barrier
+        // below).  Past the last tile it hashes tile t0 again, to no effect.
+        cb ^= 1;
+        bnd_cur = bnd_next;
+        bnd_next = load_bounds(t + 2 * G);
+        step(std::integral_constant<int, 0>{}, t + G);
+        stamp(2);
+        if (VARIANT != 1) write_out(c8, base, copy);
         stamp(4);
         __syncthreads();  // bins written out and counters re-armed
         stamp(3);
