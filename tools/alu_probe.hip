@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdint>
+#include "../bsdb_amd/csrc/spooky_dev.hpp"
 
 constexpr int ITER = 4096;
 constexpr int CH = 8;
@@ -82,8 +83,23 @@ __global__ void k_pkadd(uint32_t *out, uint32_t s) {   // packed fp32 add: dual-
     if (r == 1.2345f) out[0] = 1;
 }
 
+// the 13-byte hash's ShortEnd on NK independent keys per lane (the
+// production formulation), 55 VALU per key per round
+template <int NK>
+__global__ void k_spooky(uint32_t *out, uint32_t s) {
+    uint64_t h[NK][4];
+    for (int c = 0; c < NK; c++) for (int q = 0; q < 4; q++) h[c][q] = threadIdx.x * 77 + c * 5 + q + s;
+    for (int i = 0; i < ITER / 8; i++) {
+#pragma unroll
+        for (int c = 0; c < NK; c++) bsdb::short_end_u(h[c][0], h[c][1], h[c][2], h[c][3]);
+    }
+    uint64_t r = 0;
+    for (int c = 0; c < NK; c++) r ^= h[c][0] ^ h[c][1];
+    if (r == 0x12345) out[0] = (uint32_t)r;
+}
+
 template <typename K>
-void run(const char *name, K k, int ops_per, uint32_t *d) {
+void run(const char *name, K k, int ops_per, uint32_t *d, int wpc = 32, double iters = ITER * CH) {
     hipEvent_t a, b;
     hipEventCreate(&a);
     hipEventCreate(&b);
@@ -91,7 +107,7 @@ void run(const char *name, K k, int ops_per, uint32_t *d) {
     hipGetDevice(&dev);
     hipDeviceProp_t p;
     hipGetDeviceProperties(&p, dev);
-    const int blocks = p.multiProcessorCount * 8;
+    const int blocks = p.multiProcessorCount * (wpc / 4);
     hipLaunchKernelGGL(k, dim3(blocks), dim3(256), 0, 0, d, 7u);
     hipEventRecord(a);
     for (int r = 0; r < 5; r++) hipLaunchKernelGGL(k, dim3(blocks), dim3(256), 0, 0, d, 7u);
@@ -99,7 +115,7 @@ void run(const char *name, K k, int ops_per, uint32_t *d) {
     hipEventSynchronize(b);
     float ms;
     hipEventElapsedTime(&ms, a, b);
-    const double instr = 5.0 * blocks * 256.0 * ITER * CH * ops_per;
+    const double instr = 5.0 * blocks * 256.0 * iters * ops_per;
     printf("%-12s %8.3f ms  %7.2f T lane-instr/s  (%.1f instr/clk/CU at %d MHz)\n", name, ms / 5, instr / (ms * 1e-3) / 1e12,
            instr / (ms * 1e-3) / (p.multiProcessorCount * (double)p.clockRate * 1e3), p.clockRate / 1000);
 }
@@ -108,6 +124,15 @@ int main() {
     uint32_t *d;
     hipMalloc(&d, 64);
     run("addc(2)", k_addc, 2, d);
+    for (int wpc : {8, 16, 32}) {
+        char nm[64];
+        snprintf(nm, sizeof nm, "spooky1 w%d", wpc);
+        run(nm, k_spooky<1>, 55, d, wpc, ITER / 8 * 1.0);
+        snprintf(nm, sizeof nm, "spooky2 w%d", wpc);
+        run(nm, k_spooky<2>, 55, d, wpc, ITER / 8 * 2.0);
+        snprintf(nm, sizeof nm, "spooky4 w%d", wpc);
+        run(nm, k_spooky<4>, 55, d, wpc, ITER / 8 * 4.0);
+    }
     run("lshl_add64", k_lshladd, 1, d);
     run("xor", k_xor, 1, d);
     run("alignbit", k_alignbit, 1, d);

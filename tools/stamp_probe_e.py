@@ -1,10 +1,10 @@
-"""Diagnostic: per-wave phase cycles of k_pass1_d13e (BSDB_D13_VARIANT=26
+"""Diagnostic: per-wave phase cycles of k_pass1_d13e (BSDB_D13_VARIANT=4
 writes s_memtime sums over the counts array; pass 2 then adds its counts on
 top, ~244 per word at 2^31 keys, negligible against the cycle sums)."""
 import os, sys
 import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-os.environ["BSDB_D13_VARIANT"] = "26"
+os.environ["BSDB_D13_VARIANT"] = "4"
 from bsdb_amd import Context  # noqa: E402
 n, m = 2147483648, 8795859
 ctx = Context(0)
