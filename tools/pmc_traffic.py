@@ -6,7 +6,7 @@ bytes of a wide coalesced streaming read -> x2; WRITE_SIZE is exact for
 usage: python tools/pmc_traffic.py FETCH_CSV WRITE_CSV OUT_JSON"""
 import csv, json, sys
 
-def per_dispatch(path, counter, kernel="k_pass1_d13"  # matches k_pass1_d13e too):
+def per_dispatch(path, counter, kernel="k_pass1_d13"):  # matches k_pass1_d13e too
     vals = {}
     for r in csv.DictReader(open(path)):
         if r["Counter_Name"] == counter and kernel in r["Kernel_Name"]:
