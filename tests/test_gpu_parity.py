@@ -474,3 +474,22 @@ def test_var_binned_ragged_groups(ctx):
         got = ctx.histogram_var(dev(blob), dev(off.view(np.int64)), m).cpu().numpy().view(np.uint32)
         np.testing.assert_array_equal(got, O.histogram_var(blob, off, m))
     assert ctx.fallback_count() == before
+
+
+def test_var_full_size_properties(ctx):
+    """C5 shape at scale: the binned var-len kernel equals the direct-atomics
+    histogram (an independent kernel) on 1e8 keys, sums to n, no fallback."""
+    n = 100_000_000
+    m = 4_000_000_000 // 1500 + 1
+    blob, off = ctx.gen_keys_var(0, n)
+    f0 = ctx.fallback_count()
+    c_bin = ctx.histogram_var(blob, off, m)
+    assert ctx.fallback_count() == f0
+    ctx.set_histogram_mode(2)
+    try:
+        c_atom = ctx.histogram_var(blob, off, m)
+    finally:
+        ctx.set_histogram_mode(0)
+    assert int(c_bin.sum(dtype=torch.int64)) == n
+    assert torch.equal(c_bin, c_atom)
+    del blob, off
