@@ -46,6 +46,8 @@ struct bsdb_ctx {
     // host-API staging
     uint8_t *d_keys = nullptr;
     size_t d_keys_bytes = 0;
+    uint64_t *d_off = nullptr;  // host var-len entry points: a batch's rebased offsets
+    size_t d_off_bytes = 0;
     void *d_out = nullptr;
     size_t d_out_bytes = 0;
     // GOV build workspace
@@ -468,6 +470,7 @@ int bsdb_close(bsdb_ctx *c) {
     (void)hipFree(c->overflow);
     (void)hipFree(c->scan_part);
     (void)hipFree(c->d_keys);
+    (void)hipFree(c->d_off);
     (void)hipFree(c->d_out);
     (void)hipFree(c->g_sorted);
     (void)hipFree(c->g_counts);
@@ -799,6 +802,83 @@ int bsdb_hash_fixed(bsdb_ctx *c, const uint8_t *h_keys, uint32_t key_len, uint64
         HIP_OK(hipMemcpyAsync(h_sig + 2 * k0, c->d_out, nk * 16, hipMemcpyDeviceToHost, s));
     }
     HIP_OK(hipStreamSynchronize(s));
+    return BSDB_OK;
+}
+
+// Batches of variable-length keys: [k0, k1) with at most VAR_BATCH_KEYS keys
+// and (unless one key alone is larger) VAR_BATCH_BYTES key bytes.
+constexpr uint64_t VAR_BATCH_KEYS = 1ULL << 24;
+constexpr uint64_t VAR_BATCH_BYTES = 256ULL << 20;
+static uint64_t var_batch_end(const uint64_t *off, uint64_t k0, uint64_t n) {
+    uint64_t k1 = std::min(n, k0 + VAR_BATCH_KEYS);
+    while (k1 - k0 > 1 && off[k1] - off[k0] > VAR_BATCH_BYTES) k1 = k0 + (k1 - k0) / 2;
+    return k1;
+}
+
+// One batch to the device: key bytes into c->d_keys, rebased offsets into
+// c->d_off (pinned by the stream order: the host copy `reb` outlives the
+// synchronous wait the callers do per batch).
+static int var_batch_upload(bsdb_ctx *c, const uint8_t *h_blob, const uint64_t *h_off, uint64_t k0, uint64_t k1,
+                            std::vector<uint64_t> &reb, hipStream_t s) {
+    const uint64_t nk = k1 - k0, bytes = h_off[k1] - h_off[k0];
+    int rc = grow((void **)&c->d_keys, &c->d_keys_bytes, (size_t)bytes + 16);
+    if (rc) return rc;
+    rc = grow((void **)&c->d_off, &c->d_off_bytes, (size_t)(nk + 1) * sizeof(uint64_t));
+    if (rc) return rc;
+    reb.resize(nk + 1);
+    for (uint64_t i = 0; i <= nk; ++i) {
+        if (h_off[k0 + i] < h_off[k0] || (i && h_off[k0 + i] < h_off[k0 + i - 1])) return BSDB_EINVAL;
+        reb[i] = h_off[k0 + i] - h_off[k0];
+    }
+    HIP_OK(hipMemcpyAsync(c->d_keys, h_blob + h_off[k0], bytes, hipMemcpyHostToDevice, s));
+    HIP_OK(hipMemcpyAsync(c->d_off, reb.data(), (nk + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, s));
+    return BSDB_OK;
+}
+
+int bsdb_histogram_var(bsdb_ctx *c, const uint8_t *h_blob, const uint64_t *h_off, uint64_t n, uint64_t seed,
+                       uint64_t m, uint32_t *h_counts) {
+    if (!c || m == 0 || m > 0x7FFFFFFFULL || (n && (!h_blob || !h_off)) || !h_counts) return BSDB_EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    HIP_OK(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    int rc = grow(&c->d_out, &c->d_out_bytes, m * sizeof(uint32_t));
+    if (rc) return rc;
+    uint32_t *d_counts = (uint32_t *)c->d_out;
+    HIP_OK(hipMemsetAsync(d_counts, 0, m * sizeof(uint32_t), s));
+    std::vector<uint64_t> reb;
+    for (uint64_t k0 = 0; k0 < n;) {
+        const uint64_t k1 = var_batch_end(h_off, k0, n);
+        if ((rc = var_batch_upload(c, h_blob, h_off, k0, k1, reb, s))) return rc;
+        if ((rc = histogram_impl(c, c->d_keys, c->d_off, h_off[k1] - h_off[k0], 0, k1 - k0, seed, m, d_counts, s)))
+            return rc;
+        HIP_OK(hipStreamSynchronize(s));  // reb is reused by the next batch
+        k0 = k1;
+    }
+    std::vector<uint32_t> tmp(m);
+    HIP_OK(hipMemcpyAsync(tmp.data(), d_counts, m * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    HIP_OK(hipStreamSynchronize(s));
+    for (uint64_t b = 0; b < m; ++b) h_counts[b] += tmp[b];
+    return BSDB_OK;
+}
+
+int bsdb_hash_var(bsdb_ctx *c, const uint8_t *h_blob, const uint64_t *h_off, uint64_t n, uint64_t seed,
+                  uint64_t *h_sig) {
+    if (!c || (n && (!h_blob || !h_off || !h_sig))) return BSDB_EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    HIP_OK(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    int rc = grow(&c->d_out, &c->d_out_bytes, (size_t)std::min(n, VAR_BATCH_KEYS) * 16 + 16);
+    if (rc) return rc;
+    std::vector<uint64_t> reb;
+    for (uint64_t k0 = 0; k0 < n;) {
+        const uint64_t k1 = var_batch_end(h_off, k0, n);
+        if ((rc = var_batch_upload(c, h_blob, h_off, k0, k1, reb, s))) return rc;
+        if ((rc = hash_impl(c, c->d_keys, c->d_off, h_off[k1] - h_off[k0], 0, k1 - k0, seed, (uint64_t *)c->d_out, s)))
+            return rc;
+        HIP_OK(hipMemcpyAsync(h_sig + 2 * k0, c->d_out, (k1 - k0) * 16, hipMemcpyDeviceToHost, s));
+        HIP_OK(hipStreamSynchronize(s));
+        k0 = k1;
+    }
     return BSDB_OK;
 }
 

@@ -47,6 +47,8 @@ SIGNATURES = [
     ("bsdb_profile_read", _i, [_vp, _i, C.POINTER(C.c_double), C.POINTER(_u64), C.POINTER(_u64)]),
     ("bsdb_histogram_fixed", _i, [_vp, _vp, _u32, _u64, _u64, _u64, _vp]),
     ("bsdb_hash_fixed", _i, [_vp, _vp, _u32, _u64, _u64, _vp]),
+    ("bsdb_histogram_var", _i, [_vp, _vp, _vp, _u64, _u64, _u64, _vp]),
+    ("bsdb_hash_var", _i, [_vp, _vp, _vp, _u64, _u64, _vp]),
     ("bsdb_dev_gen_keys13", _i, [_vp, _u64, _u64, _vp, _vp]),
     ("bsdb_dev_gen_keys_var", _i, [_vp, _u64, _u64, _vp, _vp, _u64, _vp]),
 ]
@@ -282,4 +284,35 @@ class Context:
         out = np.zeros((max(n, 1), 2), np.uint64)
         _check("bsdb_hash_fixed", lib().bsdb_hash_fixed(
             self._h, keys_np.ctypes.data, key_len, n, seed & (2**64 - 1), out.ctypes.data))
+        return out[:n]
+
+    @staticmethod
+    def _var_host_args(blob_np, off_np):
+        import numpy as np
+        blob_np = np.ascontiguousarray(blob_np, np.uint8)
+        off_np = np.ascontiguousarray(off_np, np.uint64)
+        if off_np.ndim != 1 or off_np.size < 1:
+            raise ValueError("offsets must be a 1-D array of n+1 entries")
+        if off_np.size > 1 and (int(off_np[-1]) > blob_np.size or np.any(off_np[1:] < off_np[:-1])):
+            raise ValueError("offsets must be non-decreasing and within the blob")
+        return blob_np, off_np, off_np.size - 1
+
+    def histogram_var_host(self, blob_np, off_np, m: int, counts_np=None, seed: int = 0):
+        """Host-buffer var-len histogram (bsdb_histogram_var): key i is
+        blob[off[i]:off[i+1]]; counts accumulate into counts_np (u32[m])."""
+        import numpy as np
+        blob_np, off_np, n = self._var_host_args(blob_np, off_np)
+        if counts_np is None:
+            counts_np = np.zeros(m, np.uint32)
+        _check("bsdb_histogram_var", lib().bsdb_histogram_var(
+            self._h, blob_np.ctypes.data, off_np.ctypes.data, n, seed & (2**64 - 1), m, counts_np.ctypes.data))
+        return counts_np
+
+    def hash_var_host(self, blob_np, off_np, seed: int = 0):
+        """Host-buffer var-len signatures (bsdb_hash_var), (n, 2) u64."""
+        import numpy as np
+        blob_np, off_np, n = self._var_host_args(blob_np, off_np)
+        out = np.zeros((max(n, 1), 2), np.uint64)
+        _check("bsdb_hash_var", lib().bsdb_hash_var(
+            self._h, blob_np.ctypes.data, off_np.ctypes.data, n, seed & (2**64 - 1), out.ctypes.data))
         return out[:n]

@@ -134,8 +134,12 @@ int bsdb_dev_gov_build(bsdb_ctx *ctx, const uint64_t *d_sig, uint64_t n, uint32_
 /* Histogram path selection for bsdb_dev_histogram_* (benchmarks/tests):
  *   0 = auto (partitioned two-pass), 1 = partitioned two-pass, 2 = direct atomics. */
 int bsdb_set_histogram_mode(bsdb_ctx *ctx, int mode);
-/* Key-load front end for 13-byte keys: 0 = auto (direct dword-aligned 16-byte
- * windows), 1 = LDS-staged sub-tiles, 2 = direct. */
+/* Key-load front end (for comparison runs; results are identical):
+ * 0 = auto: 13-byte keys by the persistent binned kernel (dword-aligned
+ *     16-byte windows), variable-length keys by the persistent binned kernel
+ *     with per-wave LDS staging of 128-key groups;
+ * 1 = the one-tile-per-workgroup kernel with LDS-staged sub-tiles;
+ * 2 = the one-tile-per-workgroup kernel with direct reads. */
 int bsdb_set_frontend(bsdb_ctx *ctx, int frontend);
 /* Per-chunk key count of the partitioned path (0 = default). */
 int bsdb_set_chunk_keys(bsdb_ctx *ctx, uint64_t chunk_keys);
@@ -161,6 +165,15 @@ int bsdb_histogram_fixed(bsdb_ctx *ctx, const uint8_t *h_keys, uint32_t key_len,
                          uint64_t seed, uint64_t num_buckets, uint32_t *h_counts);
 int bsdb_hash_fixed(bsdb_ctx *ctx, const uint8_t *h_keys, uint32_t key_len, uint64_t n,
                     uint64_t seed, uint64_t *h_sig);
+/* Variable-length keys in host memory, as BSDBWriter.put receives them
+ * (byte[] of 0..255 bytes, kLen u8, BaseKVWriter.java:44-49): key i is
+ * h_blob[h_off[i] .. h_off[i+1]), h_off[0..n] non-decreasing.  Same results
+ * as bsdb_dev_{histogram,hash}_var on the same bytes; the keys are copied H2D
+ * in batches of <= 256 MiB of key bytes (offsets rebased per batch). */
+int bsdb_histogram_var(bsdb_ctx *ctx, const uint8_t *h_blob, const uint64_t *h_off, uint64_t n,
+                       uint64_t seed, uint64_t num_buckets, uint32_t *h_counts);
+int bsdb_hash_var(bsdb_ctx *ctx, const uint8_t *h_blob, const uint64_t *h_off, uint64_t n,
+                  uint64_t seed, uint64_t *h_sig);
 
 /* Synthetic SURVEY.md §8(d) D2 13-byte keys for indices [first, first+n),
  * written on device (benchmark input generator; not part of the build path). */

@@ -188,6 +188,33 @@ def test_host_buffer_api(ctx):
     np.testing.assert_array_equal(ctx.hash_fixed_host(keys, 13), O.hash_fixed(keys, 13))
 
 
+def test_host_buffer_var_api(ctx, golden):
+    """Host var-len entry points (what the JNI shim binds for byte[] keys):
+    the reference's own NativeTest keys and random 0..255-byte keys, against
+    the oracle; batch boundaries crossed by shrinking nothing (one batch) and
+    by a key set over the 16 Mi-key batch."""
+    rng = np.random.default_rng(31)
+    lens = rng.integers(0, 256, 50_000)
+    lens[:100] = 0
+    off = np.zeros(lens.size + 1, np.uint64)
+    off[1:] = np.cumsum(lens)
+    blob = rng.integers(0, 256, int(off[-1]), dtype=np.uint8)
+    m = 777
+    np.testing.assert_array_equal(ctx.histogram_var_host(blob, off, m), O.histogram_var(blob, off, m))
+    np.testing.assert_array_equal(ctx.hash_var_host(blob, off).reshape(-1), O.hash_var(blob, off).reshape(-1))
+    gb, go = golden["var_blob"], golden["var_off"]
+    np.testing.assert_array_equal(ctx.hash_var_host(gb, go).reshape(-1), golden["var_sig"].reshape(-1))
+    # more keys than one batch (1 << 24): C5 keys from the device generator
+    n = (1 << 24) + 12_345
+    dblob, doff = ctx.gen_keys_var(3, n)
+    hb, ho = dblob.cpu().numpy()[: int(doff[-1])], u64(doff)
+    mm = O.num_buckets(n)
+    np.testing.assert_array_equal(ctx.histogram_var_host(hb, ho, mm),
+                                  ctx.histogram_var(dblob, doff, mm).cpu().numpy().view(np.uint32))
+    with pytest.raises(ValueError):
+        ctx.histogram_var_host(blob, off[::-1].copy(), m)
+
+
 def test_generator_beyond_2e32_work_items(ctx):
     # 5e9 keys: more than 2^32 keys -> the generator must grid-stride
     n = 5_000_000_000
