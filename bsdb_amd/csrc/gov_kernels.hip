@@ -413,9 +413,13 @@ __device__ bool try_seed(SolveLds &L, const ulonglong2 *sig, uint32_t cnt, uint3
         const uint32_t W = (sz + 1 + 63) / 64;
         for (uint32_t i = tid; i < sz; i += GS_THREADS) L.col_of[L.members[beg + i]] = (int16_t)i;
         __syncthreads();
+        // Rows live word-major in the workgroup's scratch: plane q (the two
+        // bit planes of GF(3)) of word w of row rr at scr[(2w + q) * GS_CMAX
+        // + rr], so a wave's 64 rows read 64 consecutive words (row-major
+        // rows 2W words apart cost a 64-byte sector per lane).
+        auto X = [&](uint32_t rr, uint32_t w, uint32_t q) -> uint64_t & { return scr[(size_t)(2 * w + q) * GS_CMAX + rr]; };
         for (uint32_t rr = tid; rr < sz; rr += GS_THREADS) {
-            uint64_t *r1 = scr + (size_t)rr * 2 * W, *r2 = r1 + W;
-            for (uint32_t w = 0; w < W; ++w) r1[w] = r2[w] = 0;
+            for (uint32_t w = 0; w < W; ++w) X(rr, w, 0) = X(rr, w, 1) = 0;
             const int k = L.members[beg + rr];
             int h = 0;
             while (L.e[3 * k + h] != (uint32_t)L.hinge[k]) ++h;
@@ -425,14 +429,14 @@ __device__ bool try_seed(SolveLds &L, const ulonglong2 *sig, uint32_t cnt, uint3
                 const int o = L.vowner[v];
                 if (o >= 0 && L.col_of[o] >= 0) {
                     const uint32_t cc = (uint32_t)L.col_of[o];
-                    gf3_add(r1[cc >> 6], r2[cc >> 6], 1ULL << (cc & 63), 0);
+                    gf3_add(X(rr, cc >> 6, 0), X(rr, cc >> 6, 1), 1ULL << (cc & 63), 0);
                 } else {
                     sub += L.xval[v];
                 }
             }
             const uint32_t rhs = ((uint32_t)h + 6 - sub % 3) % 3;
-            if (rhs == 1) r1[sz >> 6] |= 1ULL << (sz & 63);
-            if (rhs == 2) r2[sz >> 6] |= 1ULL << (sz & 63);
+            if (rhs == 1) X(rr, sz >> 6, 0) |= 1ULL << (sz & 63);
+            if (rhs == 2) X(rr, sz >> 6, 1) |= 1ULL << (sz & 63);
         }
         if (tid == 0) L.flag = 1;
         __threadfence_block();
@@ -443,8 +447,7 @@ __device__ bool try_seed(SolveLds &L, const ulonglong2 *sig, uint32_t cnt, uint3
             if (tid == 0) L.pivot = 0xFFFFFFFFu;
             __syncthreads();
             for (uint32_t rr = cc + tid; rr < sz; rr += GS_THREADS) {
-                const uint64_t *r1 = scr + (size_t)rr * 2 * W;
-                if ((r1[wc] | r1[W + wc]) & bit) {
+                if ((X(rr, wc, 0) | X(rr, wc, 1)) & bit) {
                     atomicMin(&L.pivot, rr);
                     break;
                 }
@@ -456,40 +459,45 @@ __device__ bool try_seed(SolveLds &L, const ulonglong2 *sig, uint32_t cnt, uint3
                 __syncthreads();
                 break;
             }
-            // pivot row -> LDS (normalised to coefficient 1), then swap rows p and cc
+            // pivot row -> LDS (normalised to coefficient 1), then swap rows p
+            // and cc.  Gauss-Jordan: the pivot row is zero in every earlier
+            // pivot column, so words below wc stay untouched from here on.
             {
-                uint64_t *rp = scr + (size_t)p * 2 * W, *rc = scr + (size_t)cc * 2 * W;
-                const bool two = (rp[W + wc] & bit) != 0;
-                for (uint32_t w = tid; w < W; w += GS_THREADS) {
-                    const uint64_t p1 = rp[w], p2 = rp[W + w];
+                const bool two = (X(p, wc, 1) & bit) != 0;
+                for (uint32_t w = wc + tid; w < W; w += GS_THREADS) {
+                    const uint64_t p1 = X(p, w, 0), p2 = X(p, w, 1);
                     L.prow[w] = two ? p2 : p1;
                     L.prow[W + w] = two ? p1 : p2;
                 }
                 __syncthreads();
                 if (p != cc)
-                    for (uint32_t w = tid; w < 2 * W; w += GS_THREADS) rp[w] = rc[w];
+                    for (uint32_t w = wc + tid; w < W; w += GS_THREADS) {
+                        X(p, w, 0) = X(cc, w, 0);
+                        X(p, w, 1) = X(cc, w, 1);
+                    }
                 __syncthreads();
-                for (uint32_t w = tid; w < 2 * W; w += GS_THREADS) rc[w] = L.prow[w];
+                for (uint32_t w = wc + tid; w < W; w += GS_THREADS) {
+                    X(cc, w, 0) = L.prow[w];
+                    X(cc, w, 1) = L.prow[W + w];
+                }
                 __syncthreads();
             }
             for (uint32_t rr = tid; rr < sz; rr += GS_THREADS) {
                 if (rr == cc) continue;
-                uint64_t *r1 = scr + (size_t)rr * 2 * W, *r2 = r1 + W;
-                const uint64_t f1 = r1[wc] & bit, f2 = r2[wc] & bit;
+                const uint64_t f1 = X(rr, wc, 0) & bit, f2 = X(rr, wc, 1) & bit;
                 if (!f1 && !f2) continue;
-                for (uint32_t w = 0; w < W; ++w) {
+                for (uint32_t w = wc; w < W; ++w) {
                     const uint64_t y1 = f1 ? L.prow[W + w] : L.prow[w];
                     const uint64_t y2 = f1 ? L.prow[w] : L.prow[W + w];
-                    gf3_add(r1[w], r2[w], y1, y2);
+                    gf3_add(X(rr, w, 0), X(rr, w, 1), y1, y2);
                 }
             }
             __syncthreads();
         }
         if (!L.flag) return false;
         for (uint32_t i = tid; i < sz; i += GS_THREADS) {
-            const uint64_t *r1 = scr + (size_t)i * 2 * W;
             const uint64_t bit = 1ULL << (sz & 63);
-            L.xval[L.hinge[L.members[beg + i]]] = (r1[sz >> 6] & bit) ? 1 : (r1[W + (sz >> 6)] & bit) ? 2 : 0;
+            L.xval[L.hinge[L.members[beg + i]]] = (X(i, sz >> 6, 0) & bit) ? 1 : (X(i, sz >> 6, 1) & bit) ? 2 : 0;
         }
         for (uint32_t i = tid; i < sz; i += GS_THREADS) L.col_of[L.members[beg + i]] = -1;
         __syncthreads();
