@@ -226,10 +226,16 @@ __device__ bool try_seed(SolveLds &L, const ulonglong2 *sig, uint32_t cnt, uint3
     const int rounds = r;
     pc.lap(GP_PEEL);
 
-    // ---- 2. orientation of the core (lane 0): greedy, then BFS augmenting paths
+    // ---- 2. orientation of the core (lane 0): greedy, then BFS augmenting paths.
+    // A vertex is seen by BFS number `epoch` when seen[v] == epoch (the peel
+    // degrees are dead here, their words hold the stamps), so no BFS clears
+    // the vertex array.
+    uint32_t *seen = L.deg;
+    for (uint32_t v = tid; v < nv; v += GS_THREADS) seen[v] = 0;
+    __syncthreads();
     if (tid == 0) {
         int16_t *bfs_prev = L.a0, *queue = L.a1;
-        uint8_t *seen = L.b0;
+        uint32_t epoch = 0;
         uint32_t ok = 1;
         for (uint32_t k = 0; k < cnt; ++k) {
             if (L.round_of[k] >= 0) continue;
@@ -248,7 +254,7 @@ __device__ bool try_seed(SolveLds &L, const ulonglong2 *sig, uint32_t cnt, uint3
             for (uint32_t k = 0; k < cnt; ++k) ncore += L.round_of[k] < 0;
         for (uint32_t k0 = 0; k0 < cnt && ok; ++k0) {
             if (L.round_of[k0] >= 0 || L.hinge[k0] >= 0) continue;
-            for (uint32_t v = 0; v < nv; ++v) seen[v] = 0;
+            ++epoch;
             int qh = 0, qt = 0, found_v = -1, found_e = -1;
             queue[qt++] = (int16_t)k0;
             bfs_prev[k0] = -1;
@@ -258,8 +264,8 @@ __device__ bool try_seed(SolveLds &L, const ulonglong2 *sig, uint32_t cnt, uint3
                 ++npops;
                 for (int i = 0; i < 3; ++i) {
                     const uint32_t v = L.e[3 * k + i];
-                    if (seen[v]) continue;
-                    seen[v] = 1;
+                    if (seen[v] == epoch) continue;
+                    seen[v] = epoch;
                     const int o = L.vowner[v];
                     if (o < 0) {
                         found_v = (int)v;
@@ -321,14 +327,15 @@ __device__ bool try_seed(SolveLds &L, const ulonglong2 *sig, uint32_t cnt, uint3
     }
 
     // ---- 3a. SCCs of the core dependency graph (lane 0, iterative Tarjan)
+    for (uint32_t k = tid; k < cnt; k += GS_THREADS) {
+        L.a0[k] = -1;     // tidx
+        L.col_of[k] = -1;
+        L.b0[k] = 0;      // onst
+    }
+    __syncthreads();
     if (tid == 0) {
         int16_t *tidx = L.a0, *tlow = L.a1, *tstk = L.a2, *cstk = L.a3;
         uint8_t *onst = L.b0, *cpos = L.b1;
-        for (uint32_t k = 0; k < cnt; ++k) {
-            tidx[k] = -1;
-            L.col_of[k] = -1;
-            onst[k] = 0;
-        }
         int counter = 0, sp = 0, nm = 0, nc = 0;
         for (uint32_t r0 = 0; r0 < cnt; ++r0) {
             if (L.round_of[r0] >= 0 || tidx[r0] >= 0) continue;
