@@ -125,6 +125,7 @@ struct SolveLds {
     // orientation BFS / Tarjan (not live together)
     int16_t a0[GS_CMAX], a1[GS_CMAX], a2[GS_CMAX], a3[GS_CMAX];
     uint8_t b0[GS_NVMAX], b1[GS_CMAX];
+    int16_t dep[3 * GS_CMAX];   // Tarjan: owner of edge k's i-th non-hinge vertex, or -1
     int16_t members[GS_CMAX];   // components, in emission order
     int16_t comp_end[GS_CMAX];  // end (exclusive) of component c in members
     int16_t col_of[GS_CMAX];
@@ -262,18 +263,32 @@ __device__ bool try_seed(SolveLds &L, const ulonglong2 *sig, uint32_t cnt, uint3
             while (qh < qt && found_v < 0) {
                 const int k = queue[qh++];
                 ++npops;
+                // the edge's three vertices, their marks and owners read at
+                // once (vowner is constant during a BFS; a vertex repeated in
+                // the edge counts as seen after its first visit), then the
+                // sequential visit order on registers
+                uint32_t v[3], sn[3];
+                int o[3];
+#pragma unroll
+                for (int i = 0; i < 3; ++i) v[i] = L.e[3 * k + i];
+#pragma unroll
                 for (int i = 0; i < 3; ++i) {
-                    const uint32_t v = L.e[3 * k + i];
-                    if (seen[v] == epoch) continue;
-                    seen[v] = epoch;
-                    const int o = L.vowner[v];
-                    if (o < 0) {
-                        found_v = (int)v;
+                    sn[i] = seen[v[i]];
+                    o[i] = L.vowner[v[i]];
+                }
+#pragma unroll
+                for (int i = 0; i < 3; ++i) {
+                    bool was = sn[i] == epoch;
+                    for (int jj = 0; jj < i; ++jj) was |= v[i] == v[jj];
+                    if (was) continue;
+                    seen[v[i]] = epoch;
+                    if (o[i] < 0) {
+                        found_v = (int)v[i];
                         found_e = k;
                         break;
                     }
-                    bfs_prev[o] = (int16_t)k;
-                    queue[qt++] = (int16_t)o;
+                    bfs_prev[o[i]] = (int16_t)k;
+                    queue[qt++] = (int16_t)o[i];
                 }
             }
             if (found_v < 0) {
@@ -326,11 +341,19 @@ __device__ bool try_seed(SolveLds &L, const ulonglong2 *sig, uint32_t cnt, uint3
         return L.flag != 0;
     }
 
-    // ---- 3a. SCCs of the core dependency graph (lane 0, iterative Tarjan)
+    // ---- 3a. SCCs of the core dependency graph (lane 0, iterative Tarjan).
+    // Edge k depends on the owners of its non-hinge vertices: precomputed by
+    // the whole workgroup (hinges and owners are fixed from here on), so the
+    // walk reads one word per neighbour instead of three dependent ones.
     for (uint32_t k = tid; k < cnt; k += GS_THREADS) {
         L.a0[k] = -1;     // tidx
         L.col_of[k] = -1;
         L.b0[k] = 0;      // onst
+        if (L.round_of[k] < 0)
+            for (int i = 0; i < 3; ++i) {
+                const uint32_t v = L.e[3 * k + i];
+                L.dep[3 * k + i] = (v != (uint32_t)L.hinge[k]) ? L.vowner[v] : (int16_t)-1;
+            }
     }
     __syncthreads();
     if (tid == 0) {
@@ -349,9 +372,8 @@ __device__ bool try_seed(SolveLds &L, const ulonglong2 *sig, uint32_t cnt, uint3
             while (csp) {
                 const int k = cstk[csp - 1];
                 if (cpos[csp - 1] < 3) {
-                    const uint32_t v = L.e[3 * k + cpos[csp - 1]];
+                    const int w = L.dep[3 * k + cpos[csp - 1]];
                     ++cpos[csp - 1];
-                    const int w = (v != (uint32_t)L.hinge[k]) ? L.vowner[v] : -1;
                     if (w < 0) continue;
                     if (tidx[w] < 0) {
                         tidx[w] = tlow[w] = (int16_t)counter++;
