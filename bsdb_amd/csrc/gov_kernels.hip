@@ -111,7 +111,7 @@ struct SolveArgs {
 
 // phase counters (cycles, or counts for the GP_N_* slots)
 enum GovProf { GP_EDGES, GP_PEEL, GP_GREEDY, GP_BFS, GP_TARJAN, GP_SINGLE, GP_DENSE, GP_BACK, GP_STORE,
-               GP_N_SEEDS, GP_N_BFS, GP_N_BFS_POPS, GP_N_DENSE_ROWS, GP_N_DENSE_MAX, GP_N_CORE, GP_N };
+               GP_N_SEEDS, GP_N_BFS, GP_N_BFS_POPS, GP_N_DENSE_ROWS, GP_N_DENSE_MAX, GP_N_CORE, GP_N_BLOCKS, GP_N_BIG_ROWS, GP_N };
 
 struct SolveLds {
     uint16_t e[3 * GS_CMAX];
@@ -533,6 +533,8 @@ __device__ bool try_seed(SolveLds &L, const ulonglong2 *sig, uint32_t cnt, uint3
         pc.lap(GP_DENSE);
         pc.add(GP_N_DENSE_ROWS, sz);
         pc.max(GP_N_DENSE_MAX, sz);
+        pc.add(GP_N_BLOCKS, 1);
+        if (sz > 440) pc.add(GP_N_BIG_ROWS, sz);
         ++c;
     }
     if (!L.flag) return false;
