@@ -24,7 +24,7 @@
 
 namespace bsdb {
 
-constexpr int GS_THREADS = 256;
+constexpr int GS_THREADS = 1024;
 constexpr int GS_CMAX = 2048;    // keys per bucket handled (expected ~1500, sigma ~39)
 constexpr int GS_NVMAX = 2304;   // > vertex_offset span of GS_CMAX keys
 constexpr int GS_TINY = 12;      // brute-force buckets (only in sets of < ~1500 keys)
