@@ -467,66 +467,73 @@ __device__ bool try_seed(SolveLds &L, const ulonglong2 *sig, uint32_t cnt, uint3
             if (rhs == 1) X(rr, sz >> 6, 0) |= 1ULL << (sz & 63);
             if (rhs == 2) X(rr, sz >> 6, 1) |= 1ULL << (sz & 63);
         }
-        if (tid == 0) L.flag = 1;
+        // Gauss-Jordan without row swaps: column cc's pivot is the first
+        // unused row with a nonzero there (found while column cc-1 is
+        // eliminated), rows stay in place, piv[cc] remembers it.  The block is
+        // square, so a nonsingular one has ONE solution whatever the pivots:
+        // the values equal the oracle's row-swapping elimination.
+        int16_t *piv = L.a0;   // (Tarjan's arrays are dead here)
+        uint8_t *used = L.b1;
+        for (uint32_t rr = tid; rr < sz; rr += GS_THREADS) used[rr] = 0;
+        if (tid == 0) {
+            L.flag = 1;
+            L.pivot = 0xFFFFFFFFu;
+        }
         __threadfence_block();
+        __syncthreads();
+        for (uint32_t rr = tid; rr < sz; rr += GS_THREADS)
+            if ((X(rr, 0, 0) | X(rr, 0, 1)) & 1ULL) atomicMin(&L.pivot, rr);
         __syncthreads();
         for (uint32_t cc = 0; cc < sz; ++cc) {
             const uint32_t wc = cc >> 6;
             const uint64_t bit = 1ULL << (cc & 63);
-            if (tid == 0) L.pivot = 0xFFFFFFFFu;
-            __syncthreads();
-            for (uint32_t rr = cc + tid; rr < sz; rr += GS_THREADS) {
-                if ((X(rr, wc, 0) | X(rr, wc, 1)) & bit) {
-                    atomicMin(&L.pivot, rr);
-                    break;
-                }
-            }
-            __syncthreads();
             const uint32_t p = L.pivot;
-            if (p == 0xFFFFFFFFu) {
+            if (p == 0xFFFFFFFFu) {  // singular block
                 if (tid == 0) L.flag = 0;
                 __syncthreads();
                 break;
             }
-            // pivot row -> LDS (normalised to coefficient 1), then swap rows p
-            // and cc.  Gauss-Jordan: the pivot row is zero in every earlier
-            // pivot column, so words below wc stay untouched from here on.
-            {
-                const bool two = (X(p, wc, 1) & bit) != 0;
-                for (uint32_t w = wc + tid; w < W; w += GS_THREADS) {
-                    const uint64_t p1 = X(p, w, 0), p2 = X(p, w, 1);
-                    L.prow[w] = two ? p2 : p1;
-                    L.prow[W + w] = two ? p1 : p2;
-                }
-                __syncthreads();
-                if (p != cc)
-                    for (uint32_t w = wc + tid; w < W; w += GS_THREADS) {
-                        X(p, w, 0) = X(cc, w, 0);
-                        X(p, w, 1) = X(cc, w, 1);
-                    }
-                __syncthreads();
-                for (uint32_t w = wc + tid; w < W; w += GS_THREADS) {
-                    X(cc, w, 0) = L.prow[w];
-                    X(cc, w, 1) = L.prow[W + w];
-                }
-                __syncthreads();
+            // the pivot row, normalised to coefficient 1, into LDS; it is zero
+            // in every earlier pivot column, so words below wc stay untouched
+            const bool two = (X(p, wc, 1) & bit) != 0;
+            for (uint32_t w = wc + tid; w < W; w += GS_THREADS) {
+                const uint64_t p1 = X(p, w, 0), p2 = X(p, w, 1);
+                L.prow[w] = two ? p2 : p1;
+                L.prow[W + w] = two ? p1 : p2;
             }
+            if (tid == 0) {
+                piv[cc] = (int16_t)p;
+                used[p] = 1;
+            }
+            __syncthreads();
+            if (tid == 0) L.pivot = 0xFFFFFFFFu;  // read by every lane above, before the barrier
+            // eliminate column cc from every other row; meanwhile the first
+            // unused row with a nonzero in column cc+1 becomes the next pivot
+            const uint32_t wn = (cc + 1) >> 6;
+            const uint64_t nbit = 1ULL << ((cc + 1) & 63);
+            __syncthreads();
             for (uint32_t rr = tid; rr < sz; rr += GS_THREADS) {
-                if (rr == cc) continue;
+                if (rr == p) continue;
                 const uint64_t f1 = X(rr, wc, 0) & bit, f2 = X(rr, wc, 1) & bit;
-                if (!f1 && !f2) continue;
-                for (uint32_t w = wc; w < W; ++w) {
-                    const uint64_t y1 = f1 ? L.prow[W + w] : L.prow[w];
-                    const uint64_t y2 = f1 ? L.prow[w] : L.prow[W + w];
-                    gf3_add(X(rr, w, 0), X(rr, w, 1), y1, y2);
-                }
+                if (f1 || f2)
+                    for (uint32_t w = wc; w < W; ++w) {
+                        const uint64_t y1 = f1 ? L.prow[W + w] : L.prow[w];
+                        const uint64_t y2 = f1 ? L.prow[w] : L.prow[W + w];
+                        gf3_add(X(rr, w, 0), X(rr, w, 1), y1, y2);
+                    }
+                if (cc + 1 < sz && !used[rr] && ((X(rr, wn, 0) | X(rr, wn, 1)) & nbit)) atomicMin(&L.pivot, rr);
             }
             __syncthreads();
         }
         if (!L.flag) return false;
-        for (uint32_t i = tid; i < sz; i += GS_THREADS) {
-            const uint64_t bit = 1ULL << (sz & 63);
-            L.xval[L.hinge[L.members[beg + i]]] = (X(i, sz >> 6, 0) & bit) ? 1 : (X(i, sz >> 6, 1) & bit) ? 2 : 0;
+        // column cc's value: its pivot row reads c * x = rhs with c in {1, 2}
+        // (every other column eliminated), so x = c * rhs mod 3
+        for (uint32_t cc = tid; cc < sz; cc += GS_THREADS) {
+            const uint32_t pr = (uint32_t)piv[cc];
+            const uint64_t rbit = 1ULL << (sz & 63), cbit = 1ULL << (cc & 63);
+            const uint32_t rhs = (X(pr, sz >> 6, 0) & rbit) ? 1 : (X(pr, sz >> 6, 1) & rbit) ? 2 : 0;
+            const uint32_t c = (X(pr, cc >> 6, 1) & cbit) ? 2 : 1;
+            L.xval[L.hinge[L.members[beg + cc]]] = (uint8_t)(c * rhs % 3);
         }
         for (uint32_t i = tid; i < sz; i += GS_THREADS) L.col_of[L.members[beg + i]] = -1;
         __syncthreads();
