@@ -513,15 +513,21 @@ __device__ bool try_seed(SolveLds &L, const ulonglong2 *sig, uint32_t cnt, uint3
             const uint64_t nbit = 1ULL << ((cc + 1) & 63);
             __syncthreads();
             for (uint32_t rr = tid; rr < sz; rr += GS_THREADS) {
-                if (rr == p) continue;
-                const uint64_t f1 = X(rr, wc, 0) & bit, f2 = X(rr, wc, 1) & bit;
-                if (f1 || f2)
-                    for (uint32_t w = wc; w < W; ++w) {
-                        const uint64_t y1 = f1 ? L.prow[W + w] : L.prow[w];
-                        const uint64_t y2 = f1 ? L.prow[w] : L.prow[W + w];
-                        gf3_add(X(rr, w, 0), X(rr, w, 1), y1, y2);
-                    }
-                if (cc + 1 < sz && !used[rr] && ((X(rr, wn, 0) | X(rr, wn, 1)) & nbit)) atomicMin(&L.pivot, rr);
+                bool cand = false;
+                if (rr != p) {
+                    const uint64_t f1 = X(rr, wc, 0) & bit, f2 = X(rr, wc, 1) & bit;
+                    if (f1 || f2)
+                        for (uint32_t w = wc; w < W; ++w) {
+                            const uint64_t y1 = f1 ? L.prow[W + w] : L.prow[w];
+                            const uint64_t y2 = f1 ? L.prow[w] : L.prow[W + w];
+                            gf3_add(X(rr, w, 0), X(rr, w, 1), y1, y2);
+                        }
+                    cand = cc + 1 < sz && !used[rr] && ((X(rr, wn, 0) | X(rr, wn, 1)) & nbit);
+                }
+                // a wave's lanes hold consecutive rows: its lowest candidate
+                // lane alone competes (one LDS atomic per wave, not per row)
+                const uint64_t bal = __builtin_amdgcn_ballot_w64(cand);
+                if (cand && (uint32_t)__builtin_ctzll(bal) == (tid & 63)) atomicMin(&L.pivot, rr);
             }
             __syncthreads();
         }
