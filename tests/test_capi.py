@@ -52,3 +52,19 @@ def test_host_only_calls(lib):
     assert lib.bsdb_strerror(-17) == b"duplicate key signature"
     lib.bsdb_open.argtypes = [C.c_int, C.POINTER(C.c_void_p)]
     assert lib.bsdb_open(0, None) == -22
+
+
+def test_var_host_argument_checks():
+    """The host var-len wrappers validate offsets before any device call."""
+    import numpy as np
+    from bsdb_amd.native import Context
+    blob = np.arange(10, dtype=np.uint8)
+    ok = np.array([0, 3, 3, 10], np.uint64)
+    b, o, n = Context._var_host_args(blob, ok)
+    assert n == 3 and o.dtype == np.uint64 and b.dtype == np.uint8
+    for bad in (np.array([0, 4, 3], np.uint64),      # decreasing
+                np.array([0, 11], np.uint64),        # past the blob
+                np.zeros((2, 2), np.uint64),         # not 1-D
+                np.zeros(0, np.uint64)):             # no n+1 entries
+        with pytest.raises(ValueError):
+            Context._var_host_args(blob, bad)
