@@ -269,10 +269,16 @@ int histogram_impl(bsdb_ctx *c, const uint8_t *keys, const uint64_t *offsets, ui
     chunk = std::max<uint64_t>(P1_TILE, chunk / P1_TILE * P1_TILE);
     chunk = std::min<uint64_t>(chunk, (n + P1_TILE - 1) / P1_TILE * P1_TILE);
     // the persistent kernels: 13-byte keys and variable-length keys
-    const D13Sel sel = d13_select(c, var);
+    D13Sel sel = d13_select(c, var);
     uint32_t bsh = 0, nb = 0, cb = 0;
-    const bool d13 = (var || key_len == 13) && c->frontend == 0 &&
-                     (sel.binned ? binned_layout(sel, m, bsh, nb, cb) : nparts <= sel.maxp);
+    bool d13 = (var || key_len == 13) && c->frontend == 0 &&
+               (sel.binned ? binned_layout(sel, m, bsh, nb, cb) : nparts <= sel.maxp);
+    if (!d13 && !var && key_len == 13 && c->frontend == 0 && sel.binned) {
+        // more bins than the binned kernel holds (m > 288 * 32768): the
+        // round-1 persistent sort kernel (up to 1024 partitions)
+        sel = D13Sel{k_pass1_d13<512>, 512, 512 * P1_KEYS_PER_THREAD, 1024, false, 0};
+        d13 = nparts <= sel.maxp;
+    }
     PartPlan pp = plan_partitions(c, chunk, m, d13, sel);
     // the id buffer takes at most half of the device memory left (workspace
     // included); the 13-byte kernel addresses one region set (P segments)
