@@ -180,11 +180,13 @@ struct D13Sel {
     bool binned;        // runs padded to 8 ids, region copies = d13_copies
     uint32_t bin_ids;   // binned: ids per LDS bin buffer
 };
-D13Sel d13_select(const bsdb_ctx *c, bool var = false) {
+D13Sel d13_select(const bsdb_ctx *c, bool var = false, uint32_t key_len = 13) {
+    if (!var && key_len != 13)  // every other fixed length: the var-len kernel on k * L offsets
+        return {k_pass1_vare<0, true>, VARE_NT, VARE_TILE, VARE_MAXP, true, VARE_BIN_IDS};
     if (var) {
-        D13Kernel k = k_pass1_vare<0>;
-        if (c->d13_variant == 1) k = k_pass1_vare<1>;
-        if (c->d13_variant == 4) k = k_pass1_vare<4>;
+        D13Kernel k = k_pass1_vare<0, false>;
+        if (c->d13_variant == 1) k = k_pass1_vare<1, false>;
+        if (c->d13_variant == 4) k = k_pass1_vare<4, false>;
         return {k, VARE_NT, VARE_TILE, VARE_MAXP, true, VARE_BIN_IDS};
     }
     switch (c->d13_variant) {
@@ -269,9 +271,12 @@ int histogram_impl(bsdb_ctx *c, const uint8_t *keys, const uint64_t *offsets, ui
     chunk = std::max<uint64_t>(P1_TILE, chunk / P1_TILE * P1_TILE);
     chunk = std::min<uint64_t>(chunk, (n + P1_TILE - 1) / P1_TILE * P1_TILE);
     // the persistent kernels: 13-byte keys and variable-length keys
-    D13Sel sel = d13_select(c, var);
+    D13Sel sel = d13_select(c, var, key_len);
     uint32_t bsh = 0, nb = 0, cb = 0;
-    bool d13 = (var || key_len == 13) && c->frontend == 0 &&
+    const bool fixed_other = !var && key_len != 13;
+    // (fixed keys over 32 B: a 128-key group would overflow the var-len
+    // kernel's LDS stage, so they stay on the one-tile-per-workgroup kernels)
+    bool d13 = c->frontend == 0 && !(fixed_other && (key_len == 0 || key_len > 32)) &&
                (sel.binned ? binned_layout(sel, m, bsh, nb, cb) : nparts <= sel.maxp);
     if (!d13 && !var && key_len == 13 && c->frontend == 0 && sel.binned) {
         // more bins than the binned kernel holds (m > 288 * 32768): the
@@ -336,7 +341,7 @@ int histogram_impl(bsdb_ctx *c, const uint8_t *keys, const uint64_t *offsets, ui
         {
             ProfScope ps(c, s, 0, nk);
             const uint64_t tiles = (nk + P1_TILE - 1) / P1_TILE;
-            if (d13 && var) {
+            if (d13 && (var || fixed_other)) {
                 // full tiles to the persistent kernel, the rest (< 1 of its
                 // tiles) to the generic kernel, in the tail regions
                 const uint64_t nfast = nk / sel.tile;
@@ -347,13 +352,19 @@ int histogram_impl(bsdb_ctx *c, const uint8_t *keys, const uint64_t *offsets, ui
                 const uint64_t done = nfast * sel.tile;
                 if (done < nk) {
                     P1Args at = ac;
-                    at.offsets = ac.offsets + done;
                     at.n = nk - done;
                     at.ids = a.ids + (size_t)pp.nmain * pp.nparts * pp.cap;
                     at.cursor = a.cursor + (size_t)pp.nmain * pp.nparts;
                     at.cap = pp.cap_tail;
                     at.nregions = pp.ntail;
-                    k_pass1<SRC_VAR, EPI_PARTITION, 1, 0><<<(uint32_t)((at.n + P1_TILE - 1) / P1_TILE), P1_THREADS, 0, s>>>(at);
+                    if (var) {
+                        at.offsets = ac.offsets + done;
+                        k_pass1<SRC_VAR, EPI_PARTITION, 1, 0><<<(uint32_t)((at.n + P1_TILE - 1) / P1_TILE), P1_THREADS, 0, s>>>(at);
+                    } else {
+                        at.keys = ac.keys + done * key_len;
+                        at.blob_bytes = at.n * key_len;
+                        launch_pass1<EPI_PARTITION>(at, false, key_len, (at.n + P1_TILE - 1) / P1_TILE, s, 0);
+                    }
                 }
             } else if (d13) {
                 // full tiles whose 16-byte windows stay inside the chunk go to the

@@ -805,7 +805,9 @@ __device__ __forceinline__ uint64_t vare_sig0_global(const uint32_t *src, uint64
     return spooky_short_sig0_u(rd, len, seed);
 }
 
-template <int VARIANT>
+// FIXED: keys of a.key_len bytes each, no offsets array (key k at k * L):
+// the same kernel serves every fixed length but 13 (k_pass1_d13e).
+template <int VARIANT, bool FIXED>
 __global__ __launch_bounds__(VARE_NT, 4) void k_pass1_vare(P1Args a, uint64_t ntiles) {
     constexpr int NT = VARE_NT, NW = VARE_NW, TILE = VARE_TILE, NG = VARE_NG;
     __shared__ __align__(16) uint16_t bins[VARE_BIN_IDS];
@@ -845,7 +847,9 @@ __global__ __launch_bounds__(VARE_NT, 4) void k_pass1_vare(P1Args a, uint64_t nt
     auto load_bounds = [&](uint64_t tt) __attribute__((always_inline)) {
         const uint64_t ts = tt < ntiles ? tt : t0;
         const uint32_t i = (uint32_t)l < 2 * NG ? (uint32_t)l : 2 * NG - 1;
-        return __builtin_nontemporal_load(a.offsets + ts * TILE + (i >> 1) * (NT * 2) + (uint64_t)w * 128 + (i & 1) * 128);
+        const uint64_t k = ts * TILE + (i >> 1) * (NT * 2) + (uint64_t)w * 128 + (i & 1) * 128;
+        if (FIXED) return k * a.key_len;
+        return __builtin_nontemporal_load(a.offsets + k);
     };
     // B: a group's byte range (3 vectors per lane) and the lane's offsets
     // off[k], off[k+1], off[k+2] (k = its first key), ring of 2
@@ -862,7 +866,7 @@ __global__ __launch_bounds__(VARE_NT, 4) void k_pass1_vare(P1Args a, uint64_t nt
         // an empty group reads the offsets array instead (always readable);
         // pointers derived from the kernel arguments, not from integers, so
         // the loads stay global_load (a flat load makes every wait a full drain)
-        const uint8_t *src = nvec ? a.keys + (lo - blob) : reinterpret_cast<const uint8_t *>(a.offsets);
+        const uint8_t *src = nvec || FIXED ? a.keys + (lo - blob) : reinterpret_cast<const uint8_t *>(a.offsets);
         const uint32_t nl = nvec ? nvec - 1 : 0;
 #pragma unroll
         for (int i = 0; i < 3; ++i)
@@ -870,8 +874,14 @@ __global__ __launch_bounds__(VARE_NT, 4) void k_pass1_vare(P1Args a, uint64_t nt
                 reinterpret_cast<const u32x4 *>(src + 16 * (uint64_t)min((uint32_t)(64 * i + l), nl)));
         const uint64_t ts = tt < ntiles ? tt : t0;
         const uint64_t k = ts * TILE + (uint64_t)gi * (NT * 2) + (uint64_t)w * 128 + 2 * l;
-        O01[r] = __builtin_nontemporal_load(reinterpret_cast<const u64x2 *>(a.offsets + k));
-        O2[r] = __builtin_nontemporal_load(a.offsets + k + 2);
+        if (FIXED) {
+            const uint64_t L = a.key_len;
+            O01[r] = u64x2{k * L, (k + 1) * L};
+            O2[r] = (k + 2) * L;
+        } else {
+            O01[r] = __builtin_nontemporal_load(reinterpret_cast<const u64x2 *>(a.offsets + k));
+            O2[r] = __builtin_nontemporal_load(a.offsets + k + 2);
+        }
         Blo[r] = lo;
         Bn[r] = nvec;
     };
