@@ -114,7 +114,7 @@ def test_device_key_generator(ctx, golden):
     np.testing.assert_array_equal(d[: 13 * 5_000].cpu().numpy(), O.gen_keys13(123_456_789_000, 5_000))
 
 
-@pytest.mark.parametrize("L", [13, 5, 20, 40, 80])
+@pytest.mark.parametrize("L", [13, 1, 5, 8, 16, 20, 32, 33, 40, 80])
 @pytest.mark.parametrize("m", [1, 667, 32_768, 32_769, 8_795_859])
 def test_histogram_partitioned_many_partitions(ctx, L, m):
     # m up to the C4 bucket count: 269 partitions of 32768 buckets
