@@ -227,7 +227,7 @@ __device__ bool try_seed(SolveLds &L, const ulonglong2 *sig, uint32_t cnt, uint3
     const int rounds = r;
     pc.lap(GP_PEEL);
 
-    // ---- 2. orientation of the core (lane 0): greedy, then BFS augmenting paths.
+    // ---- 2. orientation of the core: greedy (lane 0), then BFS augmenting paths (wave 0).
     // A vertex is seen by BFS number `epoch` when seen[v] == epoch (the peel
     // degrees are dead here, their words hold the stamps), so no BFS clears
     // the vertex array.
@@ -235,9 +235,6 @@ __device__ bool try_seed(SolveLds &L, const ulonglong2 *sig, uint32_t cnt, uint3
     for (uint32_t v = tid; v < nv; v += GS_THREADS) seen[v] = 0;
     __syncthreads();
     if (tid == 0) {
-        int16_t *bfs_prev = L.a0, *queue = L.a1;
-        uint32_t epoch = 0;
-        uint32_t ok = 1;
         for (uint32_t k = 0; k < cnt; ++k) {
             if (L.round_of[k] >= 0) continue;
             for (int i = 0; i < 3; ++i) {
@@ -250,65 +247,93 @@ __device__ bool try_seed(SolveLds &L, const ulonglong2 *sig, uint32_t cnt, uint3
             }
         }
         pc.lap(GP_GREEDY);
-        uint32_t nbfs = 0, npops = 0, ncore = 0;
+    }
+    // BFS augmenting paths, one wave: the queue is consumed in chunks of up
+    // to 21 edges, lane 3e+i taking vertex i of the chunk's edge e, which is
+    // the sequential visit order; a vertex repeated in the chunk counts for
+    // its lowest lane only (atomicMin over its stamp word), the first free
+    // vertex in lane order ends the BFS (lanes after it do nothing, as the
+    // sequential loop breaks there), and the newly reached owners are
+    // appended in lane order.  Same queue, same marks, same path.
+    if (tid < 64) {
+        int16_t *bfs_prev = L.a0, *queue = L.a1;
+        uint32_t *first_lane = L.xe;  // (dead after peeling)
+        const uint32_t lane = tid;
+        uint32_t epoch = 0, ok = 1, nbfs = 0, npops = 0, ncore = 0;
         if (pc.acc)
             for (uint32_t k = 0; k < cnt; ++k) ncore += L.round_of[k] < 0;
         for (uint32_t k0 = 0; k0 < cnt && ok; ++k0) {
-            if (L.round_of[k0] >= 0 || L.hinge[k0] >= 0) continue;
+            if (L.round_of[k0] >= 0 || L.hinge[k0] >= 0) continue;  // wave-uniform
             ++epoch;
-            int qh = 0, qt = 0, found_v = -1, found_e = -1;
-            queue[qt++] = (int16_t)k0;
-            bfs_prev[k0] = -1;
             ++nbfs;
+            if (lane == 0) {
+                queue[0] = (int16_t)k0;
+                bfs_prev[k0] = -1;
+            }
+            __builtin_amdgcn_wave_barrier();
+            uint32_t qh = 0, qt = 1;
+            int found_v = -1, found_e = -1;
             while (qh < qt && found_v < 0) {
-                const int k = queue[qh++];
-                ++npops;
-                // the edge's three vertices, their marks and owners read at
-                // once (vowner is constant during a BFS; a vertex repeated in
-                // the edge counts as seen after its first visit), then the
-                // sequential visit order on registers
-                uint32_t v[3], sn[3];
-                int o[3];
-#pragma unroll
-                for (int i = 0; i < 3; ++i) v[i] = L.e[3 * k + i];
-#pragma unroll
-                for (int i = 0; i < 3; ++i) {
-                    sn[i] = seen[v[i]];
-                    o[i] = L.vowner[v[i]];
+                const uint32_t ch = min(21u, qt - qh);
+                const bool act = lane < 3 * ch;
+                const uint32_t ei = lane / 3, vi = lane - 3 * ei;
+                int k = 0, o = -1;
+                uint32_t v = 0, sn = 0;
+                if (act) {
+                    k = queue[qh + ei];
+                    v = L.e[3 * k + vi];
+                    first_lane[v] = 64;
                 }
-#pragma unroll
-                for (int i = 0; i < 3; ++i) {
-                    bool was = sn[i] == epoch;
-                    for (int jj = 0; jj < i; ++jj) was |= v[i] == v[jj];
-                    if (was) continue;
-                    seen[v[i]] = epoch;
-                    if (o[i] < 0) {
-                        found_v = (int)v[i];
-                        found_e = k;
-                        break;
-                    }
-                    bfs_prev[o[i]] = (int16_t)k;
-                    queue[qt++] = (int16_t)o[i];
+                __builtin_amdgcn_wave_barrier();
+                if (act) {
+                    sn = seen[v];
+                    o = L.vowner[v];
+                    atomicMin(&first_lane[v], lane);
                 }
+                __builtin_amdgcn_wave_barrier();
+                const bool valid = act && first_lane[v] == lane && sn != epoch;
+                const uint64_t fb = __builtin_amdgcn_ballot_w64(valid && o < 0);
+                const uint32_t F = fb ? (uint32_t)__builtin_ctzll(fb) : 64u;
+                const bool take = valid && lane < F;  // (o >= 0 below F)
+                const uint64_t tb = __builtin_amdgcn_ballot_w64(take);
+                if (valid && lane <= F) seen[v] = epoch;
+                if (take) {
+                    const uint32_t pos = qt + __builtin_amdgcn_mbcnt_hi((uint32_t)(tb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)tb, 0u));
+                    bfs_prev[o] = (int16_t)k;
+                    queue[pos] = (int16_t)o;
+                }
+                qt += (uint32_t)__builtin_popcountll(tb);
+                qh += ch;
+                npops += ch;
+                if (fb) {
+                    found_v = __builtin_amdgcn_readlane((int)v, (int)F);
+                    found_e = __builtin_amdgcn_readlane(k, (int)F);
+                }
+                __builtin_amdgcn_wave_barrier();
             }
             if (found_v < 0) {
                 ok = 0;
                 break;
             }
-            int k = found_e, v = found_v;
-            for (;;) {
-                const int old = L.hinge[k];
-                L.hinge[k] = (int16_t)v;
-                L.vowner[v] = (int16_t)k;
-                if (k == (int)k0) break;
-                v = old;
-                k = bfs_prev[k];
+            if (lane == 0) {
+                int k = found_e, v = found_v;
+                for (;;) {
+                    const int old = L.hinge[k];
+                    L.hinge[k] = (int16_t)v;
+                    L.vowner[v] = (int16_t)k;
+                    if (k == (int)k0) break;
+                    v = old;
+                    k = bfs_prev[k];
+                }
             }
+            __builtin_amdgcn_wave_barrier();
         }
-        L.flag = ok;
-        pc.add(GP_N_BFS, nbfs);
-        pc.add(GP_N_BFS_POPS, npops);
-        pc.add(GP_N_CORE, ncore);
+        if (lane == 0) {
+            L.flag = ok;
+            pc.add(GP_N_BFS, nbfs);
+            pc.add(GP_N_BFS_POPS, npops);
+            pc.add(GP_N_CORE, ncore);
+        }
     }
     __syncthreads();
     pc.lap(GP_BFS);
