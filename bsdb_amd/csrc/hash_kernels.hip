@@ -8,11 +8,16 @@
 // Why two passes: m = n/1500+1 buckets (8.8 M at 13 B keys) is a 35 MB
 // table, far beyond LDS, and per-key device-scope atomics into it run at the
 // memory-side atomic rate (~20 G random adds/s), 20x slower than the key
-// stream.  So pass 1 hashes a tile of 8192 keys, counting-sorts the tile's
-// bucket ids by partition (32768 buckets each) in LDS and writes 2-byte
-// partition-local ids in runs; pass 2 histograms one partition at a time in a
-// 128 KiB LDS table and flushes it with coalesced atomics.  Extra traffic is
-// 4 B/key on top of the key bytes.  See DESIGN.md.
+// stream.  So pass 1 hashes a tile of keys, drops each key's 2-byte
+// partition-local id (bucket mod 32768) into an LDS bin of its bucket range,
+// and writes the bins out as padded 16-byte runs; pass 2 histograms one
+// partition at a time in a 128 KiB LDS table and flushes it with coalesced
+// atomics.  Extra traffic is ~4.3 B/key on top of the key bytes.
+//
+// Pass-1 kernels: k_pass1_d13e (13-byte keys, production), k_pass1_vare
+// (variable-length keys, and fixed lengths up to 32 B on computed offsets),
+// k_pass1_d13 (13-byte keys past 288 bins), k_pass1 (generic: tails, the
+// signature and direct-atomic epilogues, comparison front ends).  DESIGN.md §4.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
