@@ -130,7 +130,7 @@ struct SolveLds {
     int16_t comp_end[GS_CMAX];  // end (exclusive) of component c in members
     int16_t col_of[GS_CMAX];
     uint64_t prow[2 * GS_WMAX]; // pivot row
-    uint32_t ncomp, flag, pivot, rounds;
+    uint32_t ncomp, flag, pivot, rounds, chg, nleft;
 };
 
 __device__ __forceinline__ void gf3_add(uint64_t &x1, uint64_t &x2, uint64_t y1, uint64_t y2) {
@@ -464,7 +464,6 @@ __device__ bool try_seed(SolveLds &L, const ulonglong2 *sig, uint32_t cnt, uint3
         // dense block c
         const uint32_t beg = c ? (uint32_t)L.comp_end[c - 1] : 0;
         const uint32_t sz = (uint32_t)L.comp_end[c] - beg;
-        const uint32_t W = (sz + 1 + 63) / 64;
         for (uint32_t i = tid; i < sz; i += GS_THREADS) L.col_of[L.members[beg + i]] = (int16_t)i;
         __syncthreads();
         // Rows live word-major in the workgroup's scratch: plane q (the two
@@ -472,99 +471,329 @@ __device__ bool try_seed(SolveLds &L, const ulonglong2 *sig, uint32_t cnt, uint3
         // + rr], so a wave's 64 rows read 64 consecutive words (row-major
         // rows 2W words apart cost a 64-byte sector per lane).
         auto X = [&](uint32_t rr, uint32_t w, uint32_t q) -> uint64_t & { return scr[(size_t)(2 * w + q) * GS_CMAX + rr]; };
-        for (uint32_t rr = tid; rr < sz; rr += GS_THREADS) {
-            for (uint32_t w = 0; w < W; ++w) X(rr, w, 0) = X(rr, w, 1) = 0;
-            const int k = L.members[beg + rr];
-            int h = 0;
-            while (L.e[3 * k + h] != (uint32_t)L.hinge[k]) ++h;
-            uint32_t sub = 0;
-            for (int i = 0; i < 3; ++i) {
-                const uint32_t v = L.e[3 * k + i];
-                const int o = L.vowner[v];
-                if (o >= 0 && L.col_of[o] >= 0) {
-                    const uint32_t cc = (uint32_t)L.col_of[o];
-                    gf3_add(X(rr, cc >> 6, 0), X(rr, cc >> 6, 1), 1ULL << (cc & 63), 0);
-                } else {
-                    sub += L.xval[v];
-                }
-            }
-            const uint32_t rhs = ((uint32_t)h + 6 - sub % 3) % 3;
-            if (rhs == 1) X(rr, sz >> 6, 0) |= 1ULL << (sz & 63);
-            if (rhs == 2) X(rr, sz >> 6, 1) |= 1ULL << (sz & 63);
-        }
-        // Gauss-Jordan without row swaps: column cc's pivot is the first
-        // unused row with a nonzero there (found while column cc-1 is
-        // eliminated), rows stay in place, piv[cc] remembers it.  The block is
-        // square, so a nonsingular one has ONE solution whatever the pivots:
-        // the values equal the oracle's row-swapping elimination.
-        int16_t *piv = L.a0;   // (Tarjan's arrays are dead here)
-        uint8_t *used = L.b1;
-        for (uint32_t rr = tid; rr < sz; rr += GS_THREADS) used[rr] = 0;
-        if (tid == 0) {
-            L.flag = 1;
-            L.pivot = 0xFFFFFFFFu;
-        }
-        __threadfence_block();
-        __syncthreads();
-        for (uint32_t rr = tid; rr < sz; rr += GS_THREADS)
-            if ((X(rr, 0, 0) | X(rr, 0, 1)) & 1ULL) atomicMin(&L.pivot, rr);
-        __syncthreads();
-        for (uint32_t cc = 0; cc < sz; ++cc) {
-            const uint32_t wc = cc >> 6;
-            const uint64_t bit = 1ULL << (cc & 63);
-            const uint32_t p = L.pivot;
-            if (p == 0xFFFFFFFFu) {  // singular block
-                if (tid == 0) L.flag = 0;
-                __syncthreads();
-                break;
-            }
-            // the pivot row, normalised to coefficient 1, into LDS; it is zero
-            // in every earlier pivot column, so words below wc stay untouched
-            const bool two = (X(p, wc, 1) & bit) != 0;
-            for (uint32_t w = wc + tid; w < W; w += GS_THREADS) {
-                const uint64_t p1 = X(p, w, 0), p2 = X(p, w, 1);
-                L.prow[w] = two ? p2 : p1;
-                L.prow[W + w] = two ? p1 : p2;
-            }
+        uint8_t *colval = L.b0;  // (Tarjan's arrays are dead here)
+        // Gauss-Jordan on rows 0..n-1 of X (n equations, n unknowns, the
+        // right-hand side in column n), without row swaps: column cc's pivot
+        // is the first unused row with a nonzero there (found while column
+        // cc-1 is eliminated), piv[cc] remembers it.  A nonsingular square
+        // system has ONE solution whatever the pivots, so the values equal
+        // the oracle's row-swapping elimination.  colval[cc] = x_cc.
+        auto gauss_jordan = [&](uint32_t n) -> bool {
+            const uint32_t W = (n + 1 + 63) / 64;
+            int16_t *piv = L.a0;
+            uint8_t *used = L.b1;
+            for (uint32_t rr = tid; rr < n; rr += GS_THREADS) used[rr] = 0;
             if (tid == 0) {
-                piv[cc] = (int16_t)p;
-                used[p] = 1;
+                L.flag = 1;
+                L.pivot = 0xFFFFFFFFu;
             }
+            __threadfence_block();
             __syncthreads();
-            if (tid == 0) L.pivot = 0xFFFFFFFFu;  // read by every lane above, before the barrier
-            // eliminate column cc from every other row; meanwhile the first
-            // unused row with a nonzero in column cc+1 becomes the next pivot
-            const uint32_t wn = (cc + 1) >> 6;
-            const uint64_t nbit = 1ULL << ((cc + 1) & 63);
+            for (uint32_t rr = tid; rr < n; rr += GS_THREADS)
+                if ((X(rr, 0, 0) | X(rr, 0, 1)) & 1ULL) atomicMin(&L.pivot, rr);
             __syncthreads();
-            for (uint32_t rr = tid; rr < sz; rr += GS_THREADS) {
-                bool cand = false;
-                if (rr != p) {
-                    const uint64_t f1 = X(rr, wc, 0) & bit, f2 = X(rr, wc, 1) & bit;
-                    if (f1 || f2)
-                        for (uint32_t w = wc; w < W; ++w) {
-                            const uint64_t y1 = f1 ? L.prow[W + w] : L.prow[w];
-                            const uint64_t y2 = f1 ? L.prow[w] : L.prow[W + w];
-                            gf3_add(X(rr, w, 0), X(rr, w, 1), y1, y2);
-                        }
-                    cand = cc + 1 < sz && !used[rr] && ((X(rr, wn, 0) | X(rr, wn, 1)) & nbit);
+            for (uint32_t cc = 0; cc < n; ++cc) {
+                const uint32_t wc = cc >> 6;
+                const uint64_t bit = 1ULL << (cc & 63);
+                const uint32_t p = L.pivot;
+                if (p == 0xFFFFFFFFu) {  // singular
+                    if (tid == 0) L.flag = 0;
+                    __syncthreads();
+                    break;
                 }
-                // a wave's lanes hold consecutive rows: its lowest candidate
-                // lane alone competes (one LDS atomic per wave, not per row)
-                const uint64_t bal = __builtin_amdgcn_ballot_w64(cand);
-                if (cand && (uint32_t)__builtin_ctzll(bal) == (tid & 63)) atomicMin(&L.pivot, rr);
+                // the pivot row, normalised to coefficient 1, into LDS; it is
+                // zero in every earlier pivot column, so words below wc stay
+                // untouched
+                const bool two = (X(p, wc, 1) & bit) != 0;
+                for (uint32_t w = wc + tid; w < W; w += GS_THREADS) {
+                    const uint64_t p1 = X(p, w, 0), p2 = X(p, w, 1);
+                    L.prow[w] = two ? p2 : p1;
+                    L.prow[W + w] = two ? p1 : p2;
+                }
+                if (tid == 0) {
+                    piv[cc] = (int16_t)p;
+                    used[p] = 1;
+                }
+                __syncthreads();
+                if (tid == 0) L.pivot = 0xFFFFFFFFu;  // read by every lane above, before the barrier
+                // eliminate column cc from every other row; meanwhile the
+                // first unused row with a nonzero in column cc+1 becomes the
+                // next pivot
+                const uint32_t wn = (cc + 1) >> 6;
+                const uint64_t nbit = 1ULL << ((cc + 1) & 63);
+                __syncthreads();
+                for (uint32_t rr = tid; rr < n; rr += GS_THREADS) {
+                    bool cand = false;
+                    if (rr != p) {
+                        const uint64_t f1 = X(rr, wc, 0) & bit, f2 = X(rr, wc, 1) & bit;
+                        if (f1 || f2)
+                            for (uint32_t w = wc; w < W; ++w) {
+                                const uint64_t y1 = f1 ? L.prow[W + w] : L.prow[w];
+                                const uint64_t y2 = f1 ? L.prow[w] : L.prow[W + w];
+                                gf3_add(X(rr, w, 0), X(rr, w, 1), y1, y2);
+                            }
+                        cand = cc + 1 < n && !used[rr] && ((X(rr, wn, 0) | X(rr, wn, 1)) & nbit);
+                    }
+                    // a wave's lanes hold consecutive rows: its lowest
+                    // candidate lane alone competes (one LDS atomic per wave)
+                    const uint64_t bal = __builtin_amdgcn_ballot_w64(cand);
+                    if (cand && (uint32_t)__builtin_ctzll(bal) == (tid & 63)) atomicMin(&L.pivot, rr);
+                }
+                __syncthreads();
+            }
+            const bool ok = L.flag != 0;
+            if (ok)
+                // column cc's pivot row reads cf * x = rhs with cf in {1, 2}
+                // (every other column eliminated), so x = cf * rhs mod 3
+                for (uint32_t cc = tid; cc < n; cc += GS_THREADS) {
+                    const uint32_t pr = (uint32_t)piv[cc];
+                    const uint64_t rbit = 1ULL << (n & 63), cbit = 1ULL << (cc & 63);
+                    const uint32_t rhs = (X(pr, n >> 6, 0) & rbit) ? 1 : (X(pr, n >> 6, 1) & rbit) ? 2 : 0;
+                    const uint32_t cf = (X(pr, cc >> 6, 1) & cbit) ? 2 : 1;
+                    colval[cc] = (uint8_t)(cf * rhs % 3);
+                }
+            __syncthreads();
+            return ok;
+        };
+        // Block equation of member i: cf*x_hinge + sum of its other vertices
+        // = h (mod 3), h = the hinge's position in the edge, cf = its count.
+        // Large blocks: heavy variables chosen so that the others follow in
+        // dependency order (a feedback vertex set of the block's dependency
+        // graph); every other hinge becomes an affine form of the heavy ones
+        // (vectors over nH heavy columns + a constant column), the heavy
+        // hinges' own equations are an nH x nH system (~20 % of the block),
+        // and the forms are evaluated.  Block elimination by a triangular
+        // part with unit-or-two diagonal: the same unique solution, singular
+        // exactly when the block is.
+        constexpr uint32_t FVS_MIN = 96, FVS_NH_MAX = 380, FW = 6;  // <= 6 words per form / heavy row
+        constexpr size_t V0 = (size_t)16 * GS_CMAX;          // affine forms, past that region
+        auto V = [&](uint32_t i, uint32_t w, uint32_t q) -> uint64_t & { return scr[V0 + (size_t)(2 * w + q) * GS_CMAX + i]; };
+        bool solved = false;
+        if (sz >= FVS_MIN) {
+            uint32_t *st = L.xe, *indeg = L.claim;  // 0 open, 1 formed, 2 heavy (dead arrays)
+            int16_t *rnd = L.a1, *hid = L.a2;
+            auto in_dep = [&](uint32_t k, int i) -> int {  // member index of the owner of vertex i, or -1
+                const uint32_t v = L.e[3 * k + i];
+                if (v == (uint32_t)L.hinge[k]) return -1;
+                const int o = L.vowner[v];
+                return (o >= 0 && L.col_of[o] >= 0) ? L.col_of[o] : -1;
+            };
+            for (uint32_t i = tid; i < sz; i += GS_THREADS) {
+                st[i] = 0;
+                rnd[i] = -1;
             }
             __syncthreads();
+            uint32_t r = 0, nH = 0;
+            bool fall_back = false;
+            for (;;) {
+                if (tid == 0) {
+                    L.chg = 0;
+                    L.nleft = 0;
+                }
+                __syncthreads();
+                for (uint32_t i = tid; i < sz; i += GS_THREADS) {
+                    if (st[i] != 0) continue;
+                    L.nleft = 1;  // (any open member)
+                    const uint32_t k = (uint32_t)L.members[beg + i];
+                    bool ready = true;
+                    for (int t = 0; t < 3; ++t) {
+                        const int d = in_dep(k, t);
+                        ready &= d < 0 || st[d] != 0;
+                    }
+                    if (ready) {
+                        rnd[i] = (int16_t)r;
+                        L.chg = 1;
+                    }
+                }
+                __syncthreads();
+                const uint32_t chg = L.chg, open = L.nleft;
+                for (uint32_t i = tid; i < sz; i += GS_THREADS)
+                    if (st[i] == 0 && rnd[i] == (int16_t)r) st[i] = 1;
+                __syncthreads();
+                if (chg) {
+                    ++r;
+                    continue;
+                }
+                if (open == 0) break;
+                if (nH >= FVS_NH_MAX) {
+                    fall_back = true;
+                    break;
+                }
+                // stuck: the open hinge most open members depend on turns heavy
+                for (uint32_t i = tid; i < sz; i += GS_THREADS) indeg[i] = 0;
+                if (tid == 0) L.pivot = 0;
+                __syncthreads();
+                for (uint32_t i = tid; i < sz; i += GS_THREADS) {
+                    if (st[i] != 0) continue;
+                    const uint32_t k = (uint32_t)L.members[beg + i];
+                    for (int t = 0; t < 3; ++t) {
+                        const int d = in_dep(k, t);
+                        if (d >= 0 && st[d] == 0) atomicAdd(&indeg[d], 1u);
+                    }
+                }
+                __syncthreads();
+                for (uint32_t i = tid; i < sz; i += GS_THREADS)
+                    if (st[i] == 0) atomicMax(&L.pivot, (indeg[i] << 16) | (0xFFFFu - i));
+                __syncthreads();
+                const uint32_t hsel = 0xFFFFu - (L.pivot & 0xFFFFu);
+                if (tid == 0) {
+                    st[hsel] = 2;
+                    hid[hsel] = (int16_t)nH;
+                    rnd[hsel] = (int16_t)r;
+                }
+                ++nH;
+                ++r;
+                __syncthreads();
+            }
+            if (!fall_back) {
+                const uint32_t HW = (nH + 1 + 63) / 64;  // words per form (column nH = constant)
+                for (uint32_t i = tid; i < sz; i += GS_THREADS)
+                    if (st[i] == 2)
+                        for (uint32_t w = 0; w < HW; ++w) {
+                            V(i, w, 0) = (w == (uint32_t)hid[i] >> 6) ? 1ULL << (hid[i] & 63) : 0;
+                            V(i, w, 1) = 0;
+                        }
+                __syncthreads();
+                // sum over the non-hinge vertices of member k: in-block ones as
+                // forms, the rest as known values (into the constant column)
+                // (register arrays indexed by unrolled constants only: a
+                // runtime index would put them in scratch)
+                auto accumulate = [&](uint32_t k, uint64_t (&a1)[FW], uint64_t (&a2)[FW], uint32_t &cst) {
+#pragma unroll
+                    for (uint32_t w = 0; w < FW; ++w) a1[w] = a2[w] = 0;
+                    cst = 0;
+                    for (int t = 0; t < 3; ++t) {
+                        const uint32_t v = L.e[3 * k + t];
+                        if (v == (uint32_t)L.hinge[k]) continue;
+                        const int o = L.vowner[v];
+                        if (o >= 0 && L.col_of[o] >= 0) {
+                            const uint32_t j = (uint32_t)L.col_of[o];
+#pragma unroll
+                            for (uint32_t w = 0; w < FW; ++w)
+                                if (w < HW) gf3_add(a1[w], a2[w], V(j, w, 0), V(j, w, 1));
+                        } else {
+                            cst += L.xval[v];
+                        }
+                    }
+                };
+                // word w's share of k * e_col (k in {0, 1, 2}) into planes
+                auto add_unit = [&](uint64_t (&a1)[FW], uint64_t (&a2)[FW], uint32_t col, uint32_t kk) {
+#pragma unroll
+                    for (uint32_t w = 0; w < FW; ++w)
+                        if (w == (col >> 6)) gf3_add(a1[w], a2[w], kk == 1 ? 1ULL << (col & 63) : 0, kk == 2 ? 1ULL << (col & 63) : 0);
+                };
+                auto hinge_pos = [&](uint32_t k, uint32_t &h, uint32_t &cf) {
+                    h = 0;
+                    while (L.e[3 * k + h] != (uint32_t)L.hinge[k]) ++h;
+                    cf = 0;
+                    for (int t = 0; t < 3; ++t) cf += L.e[3 * k + t] == (uint32_t)L.hinge[k];
+                };
+                const uint32_t cw = nH >> 6;
+                const uint64_t cbit = 1ULL << (nH & 63);
+                for (uint32_t R = 0; R < r; ++R) {
+                    for (uint32_t i = tid; i < sz; i += GS_THREADS) {
+                        if (st[i] != 1 || rnd[i] != (int16_t)R) continue;
+                        const uint32_t k = (uint32_t)L.members[beg + i];
+                        uint64_t a1[FW], a2[FW];
+                        uint32_t cst, h, cf;
+                        accumulate(k, a1, a2, cst);
+                        hinge_pos(k, h, cf);
+                        // x = cf * (h - sum): -sum has the planes swapped; add
+                        // h - cst in the constant column of (a2, a1)
+                        add_unit(a2, a1, nH, (h + 3 * 64 - cst) % 3);
+#pragma unroll
+                        for (uint32_t w = 0; w < FW; ++w)
+                            if (w < HW) {
+                                // times cf = 2 swaps the planes back
+                                V(i, w, 0) = cf == 2 ? a1[w] : a2[w];
+                                V(i, w, 1) = cf == 2 ? a2[w] : a1[w];
+                            }
+                    }
+                    __syncthreads();
+                }
+                // the heavy members' equations: cf*x_j + forms = h
+                for (uint32_t i = tid; i < sz; i += GS_THREADS) {
+                    if (st[i] != 2) continue;
+                    const uint32_t k = (uint32_t)L.members[beg + i], j = (uint32_t)hid[i];
+                    uint64_t a1[FW], a2[FW];
+                    uint32_t cst, h, cf;
+                    accumulate(k, a1, a2, cst);
+                    hinge_pos(k, h, cf);
+                    add_unit(a1, a2, j, cf);
+                    // the forms' constant column moves to the right-hand side:
+                    // rhs = h - cst - const
+                    uint32_t cform = 0;
+#pragma unroll
+                    for (uint32_t w = 0; w < FW; ++w)
+                        if (w == cw) {
+                            cform = (a1[w] & cbit) ? 1 : (a2[w] & cbit) ? 2 : 0;
+                            a1[w] &= ~cbit;
+                            a2[w] &= ~cbit;
+                        }
+                    add_unit(a1, a2, nH, (h + 3 * 64 - cst - cform) % 3);
+#pragma unroll
+                    for (uint32_t w = 0; w < FW; ++w)
+                        if (w < HW) {
+                            X(j, w, 0) = a1[w];
+                            X(j, w, 1) = a2[w];
+                        }
+                }
+                __syncthreads();
+                if (!gauss_jordan(nH)) return false;
+                // evaluate: x_i = forms . (x_heavy, 1)
+                uint64_t *X1 = L.prow, *X2 = L.prow + 8;
+                for (uint32_t w = tid; w < 16; w += GS_THREADS) L.prow[w] = 0;
+                __syncthreads();
+                for (uint32_t j = tid; j < nH; j += GS_THREADS) {
+                    if (colval[j] == 1) atomicOr((unsigned long long *)&X1[j >> 6], 1ULL << (j & 63));
+                    if (colval[j] == 2) atomicOr((unsigned long long *)&X2[j >> 6], 1ULL << (j & 63));
+                }
+                __syncthreads();
+                for (uint32_t i = tid; i < sz; i += GS_THREADS) {
+                    const uint32_t k = (uint32_t)L.members[beg + i];
+                    uint32_t val;
+                    if (st[i] == 2) {
+                        val = colval[hid[i]];
+                    } else {
+                        uint32_t s = 0;
+                        for (uint32_t w = 0; w < HW; ++w) {
+                            const uint64_t p1 = V(i, w, 0), p2 = V(i, w, 1);
+                            s += __builtin_popcountll(p1 & X1[w]) + 2 * __builtin_popcountll(p1 & X2[w]) +
+                                 2 * __builtin_popcountll(p2 & X1[w]) + __builtin_popcountll(p2 & X2[w]);
+                        }
+                        s += (V(i, cw, 0) & cbit) ? 1 : (V(i, cw, 1) & cbit) ? 2 : 0;
+                        val = s % 3;
+                    }
+                    L.xval[L.hinge[k]] = (uint8_t)val;
+                }
+                __syncthreads();
+                solved = true;
+            }
         }
-        if (!L.flag) return false;
-        // column cc's value: its pivot row reads c * x = rhs with c in {1, 2}
-        // (every other column eliminated), so x = c * rhs mod 3
-        for (uint32_t cc = tid; cc < sz; cc += GS_THREADS) {
-            const uint32_t pr = (uint32_t)piv[cc];
-            const uint64_t rbit = 1ULL << (sz & 63), cbit = 1ULL << (cc & 63);
-            const uint32_t rhs = (X(pr, sz >> 6, 0) & rbit) ? 1 : (X(pr, sz >> 6, 1) & rbit) ? 2 : 0;
-            const uint32_t c = (X(pr, cc >> 6, 1) & cbit) ? 2 : 1;
-            L.xval[L.hinge[L.members[beg + cc]]] = (uint8_t)(c * rhs % 3);
+        if (!solved) {
+            const uint32_t W = (sz + 1 + 63) / 64;
+            for (uint32_t rr = tid; rr < sz; rr += GS_THREADS) {
+                for (uint32_t w = 0; w < W; ++w) X(rr, w, 0) = X(rr, w, 1) = 0;
+                const int k = L.members[beg + rr];
+                int h = 0;
+                while (L.e[3 * k + h] != (uint32_t)L.hinge[k]) ++h;
+                uint32_t sub = 0;
+                for (int i = 0; i < 3; ++i) {
+                    const uint32_t v = L.e[3 * k + i];
+                    const int o = L.vowner[v];
+                    if (o >= 0 && L.col_of[o] >= 0) {
+                        const uint32_t cc = (uint32_t)L.col_of[o];
+                        gf3_add(X(rr, cc >> 6, 0), X(rr, cc >> 6, 1), 1ULL << (cc & 63), 0);
+                    } else {
+                        sub += L.xval[v];
+                    }
+                }
+                const uint32_t rhs = ((uint32_t)h + 6 - sub % 3) % 3;
+                if (rhs == 1) X(rr, sz >> 6, 0) |= 1ULL << (sz & 63);
+                if (rhs == 2) X(rr, sz >> 6, 1) |= 1ULL << (sz & 63);
+            }
+            if (!gauss_jordan(sz)) return false;
+            for (uint32_t cc = tid; cc < sz; cc += GS_THREADS) L.xval[L.hinge[L.members[beg + cc]]] = colval[cc];
         }
         for (uint32_t i = tid; i < sz; i += GS_THREADS) L.col_of[L.members[beg + i]] = -1;
         __syncthreads();
