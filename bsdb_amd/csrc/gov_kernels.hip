@@ -578,9 +578,14 @@ __device__ bool try_seed(SolveLds &L, const ulonglong2 *sig, uint32_t cnt, uint3
                 const int o = L.vowner[v];
                 return (o >= 0 && L.col_of[o] >= 0) ? L.col_of[o] : -1;
             };
+            // the block's dependency graph, once: idep[3i+t] = member index
+            // of the owner of member i's vertex t, or -1 (L.dep is dead here)
+            int16_t *idep = L.dep;
             for (uint32_t i = tid; i < sz; i += GS_THREADS) {
                 st[i] = 0;
                 rnd[i] = -1;
+                const uint32_t k = (uint32_t)L.members[beg + i];
+                for (int t = 0; t < 3; ++t) idep[3 * i + t] = (int16_t)in_dep(k, t);
             }
             __syncthreads();
             uint32_t r = 0, nH = 0;
@@ -594,10 +599,9 @@ __device__ bool try_seed(SolveLds &L, const ulonglong2 *sig, uint32_t cnt, uint3
                 for (uint32_t i = tid; i < sz; i += GS_THREADS) {
                     if (st[i] != 0) continue;
                     L.nleft = 1;  // (any open member)
-                    const uint32_t k = (uint32_t)L.members[beg + i];
                     bool ready = true;
                     for (int t = 0; t < 3; ++t) {
-                        const int d = in_dep(k, t);
+                        const int d = idep[3 * i + t];
                         ready &= d < 0 || st[d] != 0;
                     }
                     if (ready) {
@@ -625,15 +629,19 @@ __device__ bool try_seed(SolveLds &L, const ulonglong2 *sig, uint32_t cnt, uint3
                 __syncthreads();
                 for (uint32_t i = tid; i < sz; i += GS_THREADS) {
                     if (st[i] != 0) continue;
-                    const uint32_t k = (uint32_t)L.members[beg + i];
                     for (int t = 0; t < 3; ++t) {
-                        const int d = in_dep(k, t);
+                        const int d = idep[3 * i + t];
                         if (d >= 0 && st[d] == 0) atomicAdd(&indeg[d], 1u);
                     }
                 }
                 __syncthreads();
-                for (uint32_t i = tid; i < sz; i += GS_THREADS)
-                    if (st[i] == 0) atomicMax(&L.pivot, (indeg[i] << 16) | (0xFFFFu - i));
+                for (uint32_t i0 = 0; i0 < sz; i0 += GS_THREADS) {  // (uniform trip count: every lane shuffles)
+                    const uint32_t i = i0 + tid;
+                    uint32_t key = (i < sz && st[i] == 0) ? (indeg[i] << 16) | (0xFFFFu - i) : 0u;
+#pragma unroll
+                    for (int d = 32; d >= 1; d >>= 1) key = max(key, (uint32_t)__shfl_xor((int)key, d, 64));
+                    if ((tid & 63) == 0 && key) atomicMax(&L.pivot, key);  // one per wave
+                }
                 __syncthreads();
                 const uint32_t hsel = 0xFFFFu - (L.pivot & 0xFFFFu);
                 if (tid == 0) {
