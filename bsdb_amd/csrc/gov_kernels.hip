@@ -130,6 +130,7 @@ struct SolveLds {
     int16_t comp_end[GS_CMAX];  // end (exclusive) of component c in members
     int16_t col_of[GS_CMAX];
     uint64_t prow[2 * GS_WMAX]; // pivot row
+    uint64_t hsys[2 * 6 * 256]; // a heavy-hinge system of <= 255 unknowns, word-major (stride 256)
     uint32_t ncomp, flag, pivot, rounds, chg, nleft;
 };
 
@@ -472,13 +473,14 @@ __device__ bool try_seed(SolveLds &L, const ulonglong2 *sig, uint32_t cnt, uint3
         // rows 2W words apart cost a 64-byte sector per lane).
         auto X = [&](uint32_t rr, uint32_t w, uint32_t q) -> uint64_t & { return scr[(size_t)(2 * w + q) * GS_CMAX + rr]; };
         uint8_t *colval = L.b0;  // (Tarjan's arrays are dead here)
+        auto HS = [&](uint32_t rr, uint32_t w, uint32_t q) -> uint64_t & { return L.hsys[(2 * w + q) * 256 + rr]; };
         // Gauss-Jordan on rows 0..n-1 of X (n equations, n unknowns, the
         // right-hand side in column n), without row swaps: column cc's pivot
         // is the first unused row with a nonzero there (found while column
         // cc-1 is eliminated), piv[cc] remembers it.  A nonsingular square
         // system has ONE solution whatever the pivots, so the values equal
         // the oracle's row-swapping elimination.  colval[cc] = x_cc.
-        auto gauss_jordan = [&](uint32_t n) -> bool {
+        auto gauss_jordan = [&](uint32_t n, auto &&X) -> bool {
             const uint32_t W = (n + 1 + 63) / 64;
             int16_t *piv = L.a0;
             uint8_t *used = L.b1;
@@ -742,12 +744,17 @@ __device__ bool try_seed(SolveLds &L, const ulonglong2 *sig, uint32_t cnt, uint3
 #pragma unroll
                     for (uint32_t w = 0; w < FW; ++w)
                         if (w < HW) {
-                            X(j, w, 0) = a1[w];
-                            X(j, w, 1) = a2[w];
+                            if (nH < 256) {
+                                HS(j, w, 0) = a1[w];
+                                HS(j, w, 1) = a2[w];
+                            } else {
+                                X(j, w, 0) = a1[w];
+                                X(j, w, 1) = a2[w];
+                            }
                         }
                 }
                 __syncthreads();
-                if (!gauss_jordan(nH)) return false;
+                if (!(nH < 256 ? gauss_jordan(nH, HS) : gauss_jordan(nH, X))) return false;
                 // evaluate: x_i = forms . (x_heavy, 1)
                 uint64_t *X1 = L.prow, *X2 = L.prow + 8;
                 for (uint32_t w = tid; w < 16; w += GS_THREADS) L.prow[w] = 0;
@@ -800,7 +807,7 @@ __device__ bool try_seed(SolveLds &L, const ulonglong2 *sig, uint32_t cnt, uint3
                 if (rhs == 1) X(rr, sz >> 6, 0) |= 1ULL << (sz & 63);
                 if (rhs == 2) X(rr, sz >> 6, 1) |= 1ULL << (sz & 63);
             }
-            if (!gauss_jordan(sz)) return false;
+            if (!gauss_jordan(sz, X)) return false;
             for (uint32_t cc = tid; cc < sz; cc += GS_THREADS) L.xval[L.hinge[L.members[beg + cc]]] = colval[cc];
         }
         for (uint32_t i = tid; i < sz; i += GS_THREADS) L.col_of[L.members[beg + i]] = -1;
