@@ -706,7 +706,8 @@ int bsdb_dev_gov_build(bsdb_ctx *c, const uint64_t *d_sig, uint64_t n, uint32_t 
         (void)hipFree(d_prof);
         const char *names[GP_N] = {"edges", "peel", "greedy", "bfs", "tarjan", "singletons", "dense", "back",
                                    "store", "n_seeds", "n_bfs", "n_bfs_pops", "n_dense_rows", "n_dense_max",
-                                   "n_core", "n_blocks", "n_rows_in_blocks_over_440"};
+                                   "n_core", "n_blocks", "n_rows_in_blocks_over_440", "n_scc_sweeps",
+                                   "n_small_scc_fallbacks"};
         std::vector<double> tot(GP_N, 0.0);
         for (uint32_t w = 0; w < solve_grid; ++w)
             for (int k = 0; k < GP_N; ++k) {

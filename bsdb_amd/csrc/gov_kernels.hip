@@ -111,7 +111,8 @@ struct SolveArgs {
 
 // phase counters (cycles, or counts for the GP_N_* slots)
 enum GovProf { GP_EDGES, GP_PEEL, GP_GREEDY, GP_BFS, GP_TARJAN, GP_SINGLE, GP_DENSE, GP_BACK, GP_STORE,
-               GP_N_SEEDS, GP_N_BFS, GP_N_BFS_POPS, GP_N_DENSE_ROWS, GP_N_DENSE_MAX, GP_N_CORE, GP_N_BLOCKS, GP_N_BIG_ROWS, GP_N };
+               GP_N_SEEDS, GP_N_BFS, GP_N_BFS_POPS, GP_N_DENSE_ROWS, GP_N_DENSE_MAX, GP_N_CORE, GP_N_BLOCKS, GP_N_BIG_ROWS,
+               GP_N_SCC_SWEEPS, GP_N_SMALL_S, GP_N };
 
 struct SolveLds {
     uint16_t e[3 * GS_CMAX];
@@ -131,7 +132,7 @@ struct SolveLds {
     int16_t col_of[GS_CMAX];
     uint64_t prow[2 * GS_WMAX]; // pivot row
     uint64_t hsys[2 * 6 * 256]; // a heavy-hinge system of <= 255 unknowns, word-major (stride 256)
-    uint32_t ncomp, flag, pivot, rounds, chg, nleft;
+    uint32_t ncomp, flag, pivot, rounds, chg, nleft, nscc;
 };
 
 __device__ __forceinline__ void gf3_add(uint64_t &x1, uint64_t &x2, uint64_t y1, uint64_t y2) {
@@ -382,12 +383,126 @@ __device__ bool try_seed(SolveLds &L, const ulonglong2 *sig, uint32_t cnt, uint3
             }
     }
     __syncthreads();
+    // The core is nearly one strongly connected component (~97 % of its
+    // edges).  That component is found by the whole workgroup: S = F & B,
+    // F = edges reachable from a pivot along dependencies, B = edges that
+    // reach it (fixpoint sweeps, one barrier each).  Tarjan on lane 0 then
+    // only walks the rest: first from roots in F \ S (closed under
+    // dependencies), then S as one component, then from the other roots
+    // (F is finished by then).  SCCs are unique and this is a valid
+    // dependency order, and a nonsingular block has one solution, so the
+    // values are those of a whole-core Tarjan.
+    uint32_t *fb = L.claim;  // bit 0: in F, bit 1: in B (dead after peeling)
+    int16_t *roots = reinterpret_cast<int16_t *>(L.xe);  // Tarjan roots: F \ S, then the rest (dead after the BFS)
+    if (tid == 0) {
+        L.pivot = 0xFFFFFFFFu;
+        L.nscc = 0;
+    }
+    for (uint32_t k = tid; k < cnt; k += GS_THREADS) fb[k] = 0;
+    __syncthreads();
+    for (uint32_t k = tid; k < cnt; k += GS_THREADS)
+        if (L.round_of[k] < 0) {
+            atomicMin(&L.pivot, k);
+            break;
+        }
+    __syncthreads();
+    if (tid == 0 && L.pivot != 0xFFFFFFFFu) {
+        // follow first dependencies from the first core edge: the walk ends
+        // on a cycle, almost surely inside the big component
+        int p = (int)L.pivot;
+        for (int step = 0; step < 64; ++step) {
+            const int d0 = L.dep[3 * p], d1 = L.dep[3 * p + 1], d2 = L.dep[3 * p + 2];
+            const int nx = d0 >= 0 ? d0 : d1 >= 0 ? d1 : d2;
+            if (nx < 0) break;
+            p = nx;
+        }
+        L.pivot = (uint32_t)p;
+        fb[p] = 3u;
+    }
+    __syncthreads();
+    if (L.pivot != 0xFFFFFFFFu) {
+        for (;;) {
+            int ch = 0;
+            for (uint32_t k = tid; k < cnt; k += GS_THREADS) {
+                if (L.round_of[k] >= 0) continue;
+                const uint32_t fk = fb[k];
+                for (int i = 0; i < 3; ++i) {
+                    const int w = L.dep[3 * k + i];
+                    if (w < 0) continue;
+                    const uint32_t fw = fb[w];
+                    if ((fk & 1u) && !(fw & 1u)) { atomicOr(&fb[w], 1u); ch = 1; }                   // F: push
+                    if ((fw & 2u) && !(fk & 2u) && !(fb[k] & 2u)) { atomicOr(&fb[k], 2u); ch = 1; }  // B: pull
+                }
+            }
+            pc.add(GP_N_SCC_SWEEPS, 1);
+            if (!__syncthreads_or(ch)) break;
+        }
+        uint32_t ns = 0;
+        for (uint32_t k = tid; k < cnt; k += GS_THREADS) ns += fb[k] == 3u;
+        if (ns) atomicAdd(&L.nscc, ns);
+        __syncthreads();
+    }
+    const bool big = L.nscc >= 64;  // (a small S: plain Tarjan over the whole core)
+    if (!big) pc.add(GP_N_SMALL_S, 1);
+    // ordered compaction (wave ballots, wave totals by barrier): class 0 =
+    // F \ S roots, 1 = S (straight into members[], after the F \ S
+    // components, which hold exactly |F \ S| members), 2 = the other roots
+    uint32_t *wcnt = L.deg;  // 3 x 16 wave totals (the BFS stamps are dead)
+    const uint32_t lane = tid & 63, wv = tid >> 6;
+    uint32_t base0 = 0, base1 = 0, base2 = 0;
+    for (int phase = 0; phase < 2; ++phase) {  // 0: class sizes; 1: positions
+        uint32_t run0 = 0, run1 = 0, run2 = 0;
+        for (uint32_t k0 = 0; k0 < cnt; k0 += GS_THREADS) {
+            const uint32_t k = k0 + tid;
+            uint32_t cl = 3;
+            if (k < cnt && L.round_of[k] < 0) {
+                const uint32_t f = big ? fb[k] : 0u;
+                cl = f == 1u ? 0u : f == 3u ? 1u : 2u;
+            }
+            const uint64_t b0 = __builtin_amdgcn_ballot_w64(cl == 0), b1 = __builtin_amdgcn_ballot_w64(cl == 1),
+                           b2 = __builtin_amdgcn_ballot_w64(cl == 2);
+            if (lane == 0) {
+                wcnt[wv] = (uint32_t)__builtin_popcountll(b0);
+                wcnt[16 + wv] = (uint32_t)__builtin_popcountll(b1);
+                wcnt[32 + wv] = (uint32_t)__builtin_popcountll(b2);
+            }
+            __syncthreads();
+            uint32_t p0 = 0, p1 = 0, p2 = 0, t0 = 0, t1 = 0, t2 = 0;
+            for (uint32_t w = 0; w < GS_THREADS / 64; ++w) {
+                const uint32_t c0 = wcnt[w], c1 = wcnt[16 + w], c2 = wcnt[32 + w];
+                if (w < wv) { p0 += c0; p1 += c1; p2 += c2; }
+                t0 += c0; t1 += c1; t2 += c2;
+            }
+            if (phase == 1 && cl < 3) {
+                const uint64_t bm = cl == 0 ? b0 : cl == 1 ? b1 : b2;
+                const uint32_t r = (uint32_t)__builtin_popcountll(bm & ((1ULL << lane) - 1ULL));
+                if (cl == 0) roots[base0 + run0 + p0 + r] = (int16_t)k;
+                else if (cl == 1) {
+                    L.members[base1 + run1 + p1 + r] = (int16_t)k;
+                    L.a0[k] = 0x7FFF;  // S is finished for Tarjan (never on its stack)
+                }
+                else roots[base2 + run2 + p2 + r] = (int16_t)k;
+            }
+            run0 += t0; run1 += t1; run2 += t2;
+            __syncthreads();
+        }
+        base1 = run0;             // S members follow the F \ S components
+        base2 = run0;             // roots: F \ S, then the rest
+        if (phase == 0) { L.rounds = run0; L.chg = run1; L.nleft = run2; }
+    }
+    const uint32_t nA = L.rounds, nS = L.chg, nC = L.nleft;
     if (tid == 0) {
         int16_t *tidx = L.a0, *tlow = L.a1, *tstk = L.a2, *cstk = L.a3;
         uint8_t *onst = L.b0, *cpos = L.b1;
         int counter = 0, sp = 0, nm = 0, nc = 0;
-        for (uint32_t r0 = 0; r0 < cnt; ++r0) {
-            if (L.round_of[r0] >= 0 || tidx[r0] >= 0) continue;
+        for (uint32_t ri = 0; ri <= nA + nC; ++ri) {
+            if (ri == nA && nS) {  // S, one component
+                nm += (int)nS;
+                L.comp_end[nc++] = (int16_t)nm;
+            }
+            if (ri == nA + nC) break;
+            const uint32_t r0 = (uint32_t)roots[ri];
+            if (tidx[r0] >= 0) continue;
             int csp = 0;
             cstk[csp] = (int16_t)r0;
             cpos[csp] = 0;
