@@ -236,17 +236,42 @@ __device__ bool try_seed(SolveLds &L, const ulonglong2 *sig, uint32_t cnt, uint3
     uint32_t *seen = L.deg;
     for (uint32_t v = tid; v < nv; v += GS_THREADS) seen[v] = 0;
     __syncthreads();
-    if (tid == 0) {
-        for (uint32_t k = 0; k < cnt; ++k) {
-            if (L.round_of[k] >= 0) continue;
-            for (int i = 0; i < 3; ++i) {
-                const uint32_t v = L.e[3 * k + i];
-                if (L.vowner[v] < 0) {
-                    L.vowner[v] = (int16_t)k;
-                    L.hinge[k] = (int16_t)v;
-                    break;
+    // Greedy: every core edge in increasing order takes its first free
+    // vertex.  Wave 0 reads 64 edges' ownership at once, then resolves them
+    // in edge order in registers: lane j's choice is broadcast and clears that
+    // vertex in the later lanes, which is the sequential outcome.
+    if (tid < 64) {
+        for (uint32_t k0 = 0; k0 < cnt; k0 += 64) {
+            const uint32_t k = k0 + tid;
+            const bool act = k < cnt && L.round_of[k] < 0;
+            uint32_t v0 = 0, v1 = 0, v2 = 0;
+            bool f0 = false, f1 = false, f2 = false;
+            if (act) {
+                v0 = L.e[3 * k];
+                v1 = L.e[3 * k + 1];
+                v2 = L.e[3 * k + 2];
+                f0 = L.vowner[v0] < 0;
+                f1 = L.vowner[v1] < 0;
+                f2 = L.vowner[v2] < 0;
+            }
+            int chosen = -1;
+            uint64_t todo = __builtin_amdgcn_ballot_w64(act);
+            while (todo) {
+                const uint32_t j = (uint32_t)__builtin_ctzll(todo);
+                todo &= todo - 1;
+                if (tid == j) chosen = f0 ? (int)v0 : f1 ? (int)v1 : f2 ? (int)v2 : -1;
+                const int c = __builtin_amdgcn_readlane(chosen, j);
+                if (c >= 0) {
+                    f0 = f0 && v0 != (uint32_t)c;
+                    f1 = f1 && v1 != (uint32_t)c;
+                    f2 = f2 && v2 != (uint32_t)c;
                 }
             }
+            if (chosen >= 0) {
+                L.vowner[chosen] = (int16_t)k;
+                L.hinge[k] = (int16_t)chosen;
+            }
+            __builtin_amdgcn_wave_barrier();
         }
         pc.lap(GP_GREEDY);
     }
@@ -960,7 +985,16 @@ __global__ __launch_bounds__(GS_THREADS) void k_gov_solve(SolveArgs a) {
     __shared__ SolveLds L;
     uint64_t *scr = a.scratch + (size_t)blockIdx.x * 2 * GS_CMAX * GS_WMAX;
     PhaseClock pc{a.prof ? a.prof + (size_t)blockIdx.x * GP_N : nullptr, 0};
-    for (uint64_t b = blockIdx.x; b < a.m; b += gridDim.x) {
+    // buckets from a queue (status[2], zeroed with the status word): seed
+    // retries make per-bucket cost uneven, a static stride left the slowest
+    // workgroup ~13 % (C2) to ~40 % (1e7 keys) behind the mean
+    __shared__ uint32_t next_b;
+    for (;;) {
+        __syncthreads();
+        if (threadIdx.x == 0) next_b = atomicAdd(a.status + 2, 1u);
+        __syncthreads();
+        const uint64_t b = next_b;
+        if (b >= a.m) break;
         const uint64_t lo = a.E[b] & OFFSET_MASK, hi = a.E[b + 1] & OFFSET_MASK;
         const uint32_t cnt = (uint32_t)(hi - lo);
         const uint64_t vo = vertex_offset(lo);
