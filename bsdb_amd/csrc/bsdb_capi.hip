@@ -707,7 +707,7 @@ int bsdb_dev_gov_build(bsdb_ctx *c, const uint64_t *d_sig, uint64_t n, uint32_t 
         const char *names[GP_N] = {"edges", "peel", "greedy", "bfs", "tarjan", "singletons", "dense", "back",
                                    "store", "n_seeds", "n_bfs", "n_bfs_pops", "n_dense_rows", "n_dense_max",
                                    "n_core", "n_blocks", "n_rows_in_blocks_over_440", "n_scc_sweeps",
-                                   "n_small_scc_fallbacks"};
+                                   "n_small_scc_fallbacks", "fvs_select", "fvs_forms", "fvs_gauss_jordan"};
         std::vector<double> tot(GP_N, 0.0);
         for (uint32_t w = 0; w < solve_grid; ++w)
             for (int k = 0; k < GP_N; ++k) {
@@ -716,7 +716,7 @@ int bsdb_dev_gov_build(bsdb_ctx *c, const uint64_t *d_sig, uint64_t n, uint32_t 
             }
         fprintf(stderr, "[gov-profile] m=%llu grid=%u", (unsigned long long)m, solve_grid);
         for (int k = 0; k < GP_N; ++k)
-            fprintf(stderr, " %s=%.4g", names[k], k == GP_N_DENSE_MAX ? tot[k] : tot[k] / (k < GP_N_SEEDS ? solve_grid : 1));
+            fprintf(stderr, " %s=%.4g", names[k], k == GP_N_DENSE_MAX ? tot[k] : tot[k] / ((k < GP_N_SEEDS || k >= GP_FVS_SEL) ? solve_grid : 1));
         fprintf(stderr, "  (cycles: mean per workgroup; counts: totals)\n");
     }
     if (width) {

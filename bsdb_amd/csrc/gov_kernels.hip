@@ -112,7 +112,7 @@ struct SolveArgs {
 // phase counters (cycles, or counts for the GP_N_* slots)
 enum GovProf { GP_EDGES, GP_PEEL, GP_GREEDY, GP_BFS, GP_TARJAN, GP_SINGLE, GP_DENSE, GP_BACK, GP_STORE,
                GP_N_SEEDS, GP_N_BFS, GP_N_BFS_POPS, GP_N_DENSE_ROWS, GP_N_DENSE_MAX, GP_N_CORE, GP_N_BLOCKS, GP_N_BIG_ROWS,
-               GP_N_SCC_SWEEPS, GP_N_SMALL_S, GP_N };
+               GP_N_SCC_SWEEPS, GP_N_SMALL_S, GP_FVS_SEL, GP_FVS_FORMS, GP_FVS_GJ, GP_N };
 
 struct SolveLds {
     uint16_t e[3 * GS_CMAX];
@@ -795,6 +795,7 @@ __device__ bool try_seed(SolveLds &L, const ulonglong2 *sig, uint32_t cnt, uint3
                 ++r;
                 __syncthreads();
             }
+            pc.lap(GP_FVS_SEL);
             if (!fall_back) {
                 const uint32_t HW = (nH + 1 + 63) / 64;  // words per form (column nH = constant)
                 for (uint32_t i = tid; i < sz; i += GS_THREADS)
@@ -861,6 +862,7 @@ __device__ bool try_seed(SolveLds &L, const ulonglong2 *sig, uint32_t cnt, uint3
                     }
                     __syncthreads();
                 }
+                pc.lap(GP_FVS_FORMS);
                 // the heavy members' equations: cf*x_j + forms = h
                 for (uint32_t i = tid; i < sz; i += GS_THREADS) {
                     if (st[i] != 2) continue;
@@ -894,7 +896,9 @@ __device__ bool try_seed(SolveLds &L, const ulonglong2 *sig, uint32_t cnt, uint3
                         }
                 }
                 __syncthreads();
-                if (!(nH < 256 ? gauss_jordan(nH, HS) : gauss_jordan(nH, X))) return false;
+                const bool hok = nH < 256 ? gauss_jordan(nH, HS) : gauss_jordan(nH, X);
+                pc.lap(GP_FVS_GJ);
+                if (!hok) return false;
                 // evaluate: x_i = forms . (x_heavy, 1)
                 uint64_t *X1 = L.prow, *X2 = L.prow + 8;
                 for (uint32_t w = tid; w < 16; w += GS_THREADS) L.prow[w] = 0;
