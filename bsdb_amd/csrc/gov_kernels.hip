@@ -841,23 +841,81 @@ __device__ bool try_seed(SolveLds &L, const ulonglong2 *sig, uint32_t cnt, uint3
                 };
                 const uint32_t cw = nH >> 6;
                 const uint64_t cbit = 1ULL << (nH & 63);
+                // formed members listed by round (counting sort), each with its
+                // in-block dependencies (idep) and constant (h - known values,
+                // cf) precomputed: a round reads only its own members, rounds
+                // that only picked a heavy hinge cost nothing
+                uint32_t *roff = L.deg, *rcur = indeg;  // (peel degrees / BFS stamps dead; indeg done)
+                int16_t *rlist = L.a3, *rinfo = L.a0;   // (Tarjan's arrays dead; a0 is reused by the GJ later)
+                for (uint32_t R = tid; R <= r; R += GS_THREADS) roff[R] = 0;
+                __syncthreads();
+                for (uint32_t i = tid; i < sz; i += GS_THREADS) {
+                    if (st[i] != 1) continue;
+                    atomicAdd(&roff[rnd[i]], 1u);
+                    const uint32_t k = (uint32_t)L.members[beg + i];
+                    uint32_t h, cf, cst = 0;
+                    hinge_pos(k, h, cf);
+                    for (int t = 0; t < 3; ++t) {
+                        const uint32_t v = L.e[3 * k + t];
+                        if (v != (uint32_t)L.hinge[k] && idep[3 * i + t] < 0) cst += L.xval[v];
+                    }
+                    rinfo[i] = (int16_t)(((h + 3 * 64 - cst) % 3) | (cf == 2 ? 4u : 0u));
+                }
+                __syncthreads();
+                {   // exclusive scan of roff[0..r], 3 entries per thread
+                    uint32_t *wsum = L.xe + GS_CMAX;  // 16 wave totals past st[] (xe holds GS_NVMAX words)
+                    const uint32_t i0 = 3 * tid;
+                    uint32_t c0 = i0 <= r ? roff[i0] : 0, c1 = i0 + 1 <= r ? roff[i0 + 1] : 0,
+                             c2 = i0 + 2 <= r ? roff[i0 + 2] : 0;
+                    const uint32_t tot = c0 + c1 + c2;
+                    uint32_t inc = tot;
+#pragma unroll
+                    for (int d = 1; d < 64; d <<= 1) {
+                        const uint32_t o = (uint32_t)__shfl_up((int)inc, d, 64);
+                        if ((tid & 63) >= (uint32_t)d) inc += o;
+                    }
+                    if ((tid & 63) == 63) wsum[tid >> 6] = inc;
+                    __syncthreads();
+                    uint32_t base = 0;
+                    for (uint32_t w = 0; w < (tid >> 6); ++w) base += wsum[w];
+                    const uint32_t ex = base + inc - tot;
+                    __syncthreads();
+                    if (i0 <= r) roff[i0] = ex;
+                    if (i0 + 1 <= r) roff[i0 + 1] = ex + c0;
+                    if (i0 + 2 <= r) roff[i0 + 2] = ex + c0 + c1;
+                }
+                __syncthreads();
+                for (uint32_t R = tid; R < r; R += GS_THREADS) rcur[R] = roff[R];
+                __syncthreads();
+                for (uint32_t i = tid; i < sz; i += GS_THREADS)
+                    if (st[i] == 1) rlist[atomicAdd(&rcur[rnd[i]], 1u)] = (int16_t)i;
+                __syncthreads();
                 for (uint32_t R = 0; R < r; ++R) {
-                    for (uint32_t i = tid; i < sz; i += GS_THREADS) {
-                        if (st[i] != 1 || rnd[i] != (int16_t)R) continue;
-                        const uint32_t k = (uint32_t)L.members[beg + i];
+                    const uint32_t o0 = roff[R], nR = roff[R + 1] - o0;
+                    if (nR == 0) continue;  // (uniform)
+                    for (uint32_t t = tid; t < nR; t += GS_THREADS) {
+                        const uint32_t i = (uint32_t)rlist[o0 + t];
+                        const int d0 = idep[3 * i], d1 = idep[3 * i + 1], d2 = idep[3 * i + 2];
+                        const uint32_t info = (uint32_t)rinfo[i];
                         uint64_t a1[FW], a2[FW];
-                        uint32_t cst, h, cf;
-                        accumulate(k, a1, a2, cst);
-                        hinge_pos(k, h, cf);
+#pragma unroll
+                        for (uint32_t w = 0; w < FW; ++w) a1[w] = a2[w] = 0;
+#pragma unroll
+                        for (uint32_t w = 0; w < FW; ++w)
+                            if (w < HW) {
+                                if (d0 >= 0) gf3_add(a1[w], a2[w], V(d0, w, 0), V(d0, w, 1));
+                                if (d1 >= 0) gf3_add(a1[w], a2[w], V(d1, w, 0), V(d1, w, 1));
+                                if (d2 >= 0) gf3_add(a1[w], a2[w], V(d2, w, 0), V(d2, w, 1));
+                            }
                         // x = cf * (h - sum): -sum has the planes swapped; add
                         // h - cst in the constant column of (a2, a1)
-                        add_unit(a2, a1, nH, (h + 3 * 64 - cst) % 3);
+                        add_unit(a2, a1, nH, info & 3u);
 #pragma unroll
                         for (uint32_t w = 0; w < FW; ++w)
                             if (w < HW) {
                                 // times cf = 2 swaps the planes back
-                                V(i, w, 0) = cf == 2 ? a1[w] : a2[w];
-                                V(i, w, 1) = cf == 2 ? a2[w] : a1[w];
+                                V(i, w, 0) = (info & 4u) ? a1[w] : a2[w];
+                                V(i, w, 1) = (info & 4u) ? a2[w] : a1[w];
                             }
                     }
                     __syncthreads();
