@@ -132,7 +132,7 @@ struct SolveLds {
     int16_t col_of[GS_CMAX];
     uint64_t prow[2 * GS_WMAX]; // pivot row
     uint64_t hsys[2 * 6 * 256]; // a heavy-hinge system of <= 255 unknowns, word-major (stride 256)
-    uint32_t ncomp, flag, pivot, rounds, chg, nleft, nscc;
+    uint32_t ncomp, flag, pivot, rounds, chg, nleft, nscc, qtail;
 };
 
 __device__ __forceinline__ void gf3_add(uint64_t &x1, uint64_t &x2, uint64_t y1, uint64_t y2) {
@@ -155,6 +155,30 @@ struct PhaseClock {
     __device__ void add(int slot, uint64_t v) { if (acc && threadIdx.x == 0) acc[slot] += v; }
     __device__ void max(int slot, uint64_t v) { if (acc && threadIdx.x == 0 && v > acc[slot]) acc[slot] = v; }
 };
+
+// In-place exclusive scan of a[0..n) (n <= 3 * GS_THREADS) by the whole
+// workgroup; wsum: 16 words of LDS scratch.  Ends with a barrier.
+__device__ void wg_excl_scan3(uint32_t *a, uint32_t n, uint32_t *wsum) {
+    const uint32_t tid = threadIdx.x, i0 = 3 * tid;
+    const uint32_t c0 = i0 < n ? a[i0] : 0, c1 = i0 + 1 < n ? a[i0 + 1] : 0, c2 = i0 + 2 < n ? a[i0 + 2] : 0;
+    const uint32_t tot = c0 + c1 + c2;
+    uint32_t inc = tot;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t o = (uint32_t)__shfl_up((int)inc, d, 64);
+        if ((tid & 63) >= (uint32_t)d) inc += o;
+    }
+    if ((tid & 63) == 63) wsum[tid >> 6] = inc;
+    __syncthreads();
+    uint32_t base = 0;
+    for (uint32_t w = 0; w < (tid >> 6); ++w) base += wsum[w];
+    const uint32_t ex = base + inc - tot;
+    __syncthreads();
+    if (i0 < n) a[i0] = ex;
+    if (i0 + 1 < n) a[i0 + 1] = ex + c0;
+    if (i0 + 2 < n) a[i0 + 2] = ex + c0 + c1;
+    __syncthreads();
+}
 
 // Tries local seed j on bucket (sig, cnt, nv).  Returns (WG-uniform) true on
 // success with L.xval / L.vowner describing the solution.
@@ -730,71 +754,115 @@ __device__ bool try_seed(SolveLds &L, const ulonglong2 *sig, uint32_t cnt, uint3
                 for (int t = 0; t < 3; ++t) idep[3 * i + t] = (int16_t)in_dep(k, t);
             }
             __syncthreads();
-            uint32_t r = 0, nH = 0;
-            bool fall_back = false;
-            for (;;) {
-                if (tid == 0) {
-                    L.chg = 0;
-                    L.nleft = 0;
-                }
-                __syncthreads();
-                for (uint32_t i = tid; i < sz; i += GS_THREADS) {
-                    if (st[i] != 0) continue;
-                    L.nleft = 1;  // (any open member)
-                    bool ready = true;
-                    for (int t = 0; t < 3; ++t) {
-                        const int d = idep[3 * i + t];
-                        ready &= d < 0 || st[d] != 0;
-                    }
-                    if (ready) {
-                        rnd[i] = (int16_t)r;
-                        L.chg = 1;
-                    }
-                }
-                __syncthreads();
-                const uint32_t chg = L.chg, open = L.nleft;
-                for (uint32_t i = tid; i < sz; i += GS_THREADS)
-                    if (st[i] == 0 && rnd[i] == (int16_t)r) st[i] = 1;
-                __syncthreads();
-                if (chg) {
-                    ++r;
-                    continue;
-                }
-                if (open == 0) break;
-                if (nH >= FVS_NH_MAX) {
-                    fall_back = true;
-                    break;
-                }
-                // stuck: the open hinge most open members depend on turns heavy
-                for (uint32_t i = tid; i < sz; i += GS_THREADS) indeg[i] = 0;
-                if (tid == 0) L.pivot = 0;
-                __syncthreads();
-                for (uint32_t i = tid; i < sz; i += GS_THREADS) {
-                    if (st[i] != 0) continue;
-                    for (int t = 0; t < 3; ++t) {
-                        const int d = idep[3 * i + t];
-                        if (d >= 0 && st[d] == 0) atomicAdd(&indeg[d], 1u);
+            // Selection, Kahn style: a member is placed (formed) once every
+            // in-block dependency is placed; with none ready, the open member
+            // most open members depend on turns heavy (ties: lowest index).
+            // The ready closure is the same whatever order it is reached in,
+            // so the heavy set is that of level-synchronous rounds.  A formed
+            // member's level is 1 + its dependencies' highest (heavy: 0):
+            // the forms are evaluated level by level.
+            uint32_t *roff = L.deg;                                        // reverse CSR offsets
+            int16_t *rev = reinterpret_cast<int16_t *>(L.hsys);            // 3 * GS_CMAX dependents
+            uint32_t *pend = reinterpret_cast<uint32_t *>(L.hsys) + 3 * GS_CMAX / 2;  // unplaced deps
+            int16_t *queue = L.a3;
+            for (uint32_t i = tid; i <= sz; i += GS_THREADS) roff[i] = 0;
+            if (tid == 0) L.qtail = 0;
+            __syncthreads();
+            for (uint32_t i = tid; i < sz; i += GS_THREADS) {
+                uint32_t np = 0;
+                for (int t = 0; t < 3; ++t) {
+                    const int d = idep[3 * i + t];
+                    if (d >= 0) {
+                        atomicAdd(&roff[d], 1u);
+                        ++np;
                     }
                 }
-                __syncthreads();
-                for (uint32_t i0 = 0; i0 < sz; i0 += GS_THREADS) {  // (uniform trip count: every lane shuffles)
-                    const uint32_t i = i0 + tid;
-                    uint32_t key = (i < sz && st[i] == 0) ? (indeg[i] << 16) | (0xFFFFu - i) : 0u;
+                pend[i] = np;
+            }
+            __syncthreads();
+            wg_excl_scan3(roff, sz + 1, L.xe + GS_CMAX);
+            for (uint32_t d = tid; d < sz; d += GS_THREADS) indeg[d] = roff[d];
+            __syncthreads();
+            for (uint32_t i = tid; i < sz; i += GS_THREADS)
+                for (int t = 0; t < 3; ++t) {
+                    const int d = idep[3 * i + t];
+                    if (d >= 0) rev[atomicAdd(&indeg[d], 1u)] = (int16_t)i;
+                }
+            __syncthreads();
+            for (uint32_t d = tid; d < sz; d += GS_THREADS) {
+                indeg[d] = roff[d + 1] - roff[d];  // slots of open members on d (all open)
+                if (pend[d] == 0) {
+                    st[d] = 1;
+                    rnd[d] = 1;
+                    queue[atomicAdd(&L.qtail, 1u)] = (int16_t)d;
+                }
+            }
+            __syncthreads();
+            if (tid < 64) {
+                const uint32_t lane = tid;
+                uint32_t qh = 0, qt = L.qtail, nh = 0, maxlev = 1;
+                bool fb = false;
+                for (;;) {
+                    while (qh < qt) {
+                        const uint32_t nb = min(64u, qt - qh);
+                        if (lane < nb) {
+                            const uint32_t p = (uint32_t)queue[qh + lane];
+                            for (int t = 0; t < 3; ++t) {
+                                const int d = idep[3 * p + t];
+                                if (d >= 0) atomicSub(&indeg[d], 1u);
+                            }
+                            for (uint32_t x = roff[p]; x < roff[p + 1]; ++x) {
+                                const uint32_t i = (uint32_t)rev[x];
+                                if (atomicSub(&pend[i], 1u) == 1u && st[i] == 0) {  // last dependency placed (not heavy)
+                                    int lev = 0;
+                                    for (int t = 0; t < 3; ++t) {
+                                        const int d = idep[3 * i + t];
+                                        if (d >= 0) lev = max(lev, (int)rnd[d]);
+                                    }
+                                    rnd[i] = (int16_t)(lev + 1);
+                                    st[i] = 1;
+                                    maxlev = max(maxlev, (uint32_t)lev + 1);
+                                    queue[atomicAdd(&L.qtail, 1u)] = (int16_t)i;
+                                }
+                            }
+                        }
+                        qh += nb;
+                        __builtin_amdgcn_wave_barrier();
+                        qt = L.qtail;
+                    }
+                    if (qt >= sz) break;  // every member placed (each enters the queue once)
+                    if (nh >= FVS_NH_MAX) {
+                        fb = true;
+                        break;
+                    }
+                    uint32_t key = 0;
+                    for (uint32_t i = lane; i < sz; i += 64)
+                        if (st[i] == 0) key = max(key, (indeg[i] << 16) | (0xFFFFu - i));
 #pragma unroll
                     for (int d = 32; d >= 1; d >>= 1) key = max(key, (uint32_t)__shfl_xor((int)key, d, 64));
-                    if ((tid & 63) == 0 && key) atomicMax(&L.pivot, key);  // one per wave
+                    const uint32_t hsel = 0xFFFFu - (key & 0xFFFFu);
+                    if (lane == 0) {
+                        st[hsel] = 2;
+                        hid[hsel] = (int16_t)nh;
+                        rnd[hsel] = 0;
+                        queue[qt] = (int16_t)hsel;
+                        L.qtail = qt + 1;
+                    }
+                    ++nh;
+                    __builtin_amdgcn_wave_barrier();
+                    qt = L.qtail;
                 }
-                __syncthreads();
-                const uint32_t hsel = 0xFFFFu - (L.pivot & 0xFFFFu);
-                if (tid == 0) {
-                    st[hsel] = 2;
-                    hid[hsel] = (int16_t)nH;
-                    rnd[hsel] = (int16_t)r;
+#pragma unroll
+                for (int d = 32; d >= 1; d >>= 1) maxlev = max(maxlev, (uint32_t)__shfl_xor((int)maxlev, d, 64));
+                if (lane == 0) {
+                    L.nleft = nh;
+                    L.rounds = maxlev + 1;
+                    L.chg = fb ? 1u : 0u;
                 }
-                ++nH;
-                ++r;
-                __syncthreads();
             }
+            __syncthreads();
+            const uint32_t nH = L.nleft, r = L.rounds;
+            const bool fall_back = L.chg != 0;
             pc.lap(GP_FVS_SEL);
             if (!fall_back) {
                 const uint32_t HW = (nH + 1 + 63) / 64;  // words per form (column nH = constant)
@@ -862,29 +930,7 @@ __device__ bool try_seed(SolveLds &L, const ulonglong2 *sig, uint32_t cnt, uint3
                     rinfo[i] = (int16_t)(((h + 3 * 64 - cst) % 3) | (cf == 2 ? 4u : 0u));
                 }
                 __syncthreads();
-                {   // exclusive scan of roff[0..r], 3 entries per thread
-                    uint32_t *wsum = L.xe + GS_CMAX;  // 16 wave totals past st[] (xe holds GS_NVMAX words)
-                    const uint32_t i0 = 3 * tid;
-                    uint32_t c0 = i0 <= r ? roff[i0] : 0, c1 = i0 + 1 <= r ? roff[i0 + 1] : 0,
-                             c2 = i0 + 2 <= r ? roff[i0 + 2] : 0;
-                    const uint32_t tot = c0 + c1 + c2;
-                    uint32_t inc = tot;
-#pragma unroll
-                    for (int d = 1; d < 64; d <<= 1) {
-                        const uint32_t o = (uint32_t)__shfl_up((int)inc, d, 64);
-                        if ((tid & 63) >= (uint32_t)d) inc += o;
-                    }
-                    if ((tid & 63) == 63) wsum[tid >> 6] = inc;
-                    __syncthreads();
-                    uint32_t base = 0;
-                    for (uint32_t w = 0; w < (tid >> 6); ++w) base += wsum[w];
-                    const uint32_t ex = base + inc - tot;
-                    __syncthreads();
-                    if (i0 <= r) roff[i0] = ex;
-                    if (i0 + 1 <= r) roff[i0 + 1] = ex + c0;
-                    if (i0 + 2 <= r) roff[i0 + 2] = ex + c0 + c1;
-                }
-                __syncthreads();
+                wg_excl_scan3(roff, r + 1, L.xe + GS_CMAX);  // (16 words past st[]; xe holds GS_NVMAX)
                 for (uint32_t R = tid; R < r; R += GS_THREADS) rcur[R] = roff[R];
                 __syncthreads();
                 for (uint32_t i = tid; i < sz; i += GS_THREADS)
