@@ -835,9 +835,20 @@ __device__ bool try_seed(SolveLds &L, const ulonglong2 *sig, uint32_t cnt, uint3
                         fb = true;
                         break;
                     }
+                    // (loads issued 8 at a time before any is used)
                     uint32_t key = 0;
-                    for (uint32_t i = lane; i < sz; i += 64)
-                        if (st[i] == 0) key = max(key, (indeg[i] << 16) | (0xFFFFu - i));
+                    for (uint32_t q0 = 0; q0 * 64 < sz; q0 += 8) {
+                        uint32_t sv[8], dv[8];
+#pragma unroll
+                        for (uint32_t q = 0; q < 8; ++q) {
+                            const uint32_t i = lane + 64 * (q0 + q);
+                            sv[q] = i < sz ? st[i] : 1u;
+                            dv[q] = i < sz ? indeg[i] : 0u;
+                        }
+#pragma unroll
+                        for (uint32_t q = 0; q < 8; ++q)
+                            if (sv[q] == 0) key = max(key, (dv[q] << 16) | (0xFFFFu - (lane + 64 * (q0 + q))));
+                    }
 #pragma unroll
                     for (int d = 32; d >= 1; d >>= 1) key = max(key, (uint32_t)__shfl_xor((int)key, d, 64));
                     const uint32_t hsel = 0xFFFFu - (key & 0xFFFFu);
