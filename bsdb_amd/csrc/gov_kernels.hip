@@ -5,12 +5,15 @@
 // step, so the device output is bit-identical to it:
 //   edges   signatureToEquation(sorted sig, j<<56, nv)       (mph.c:63-71)
 //   peel    rounds: every degree-1 vertex claims its edge (smallest wins)
-//   orient  greedy first-free vertex in edge order + BFS augmenting paths
-//           (one lane: sequential by definition, ~1000 edges)
-//   solve   core blocks = SCCs of the hinge dependency graph (Tarjan, one
-//           lane), each block Gauss-Jordan over F3 with the whole workgroup
-//           (bit-sliced rows in a per-workgroup global scratch: a ~900-row
-//           block needs ~250 KB, more than LDS), peeled edges by rounds
+//   orient  greedy first-free vertex in edge order (wave 0, 64 edges per
+//           step resolved in registers) + BFS augmenting paths (wave 0)
+//   solve   core blocks = SCCs of the hinge dependency graph (the big one
+//           by forward/backward reach sweeps of the workgroup, the rest by
+//           Tarjan on lane 0); small blocks Gauss-Jordan over F3 with the
+//           whole workgroup (bit-sliced rows in a per-workgroup global
+//           scratch), large ones through a feedback vertex set (Kahn
+//           selection on wave 0, affine forms by dependency level, the heavy
+//           system in LDS); peeled edges by rounds
 //   store   hinge value or 3 if 0, non-hinge 0 (GOV:126-139); local seed in
 //           the top 8 bits of edgeOffsetAndSeed[b] (GOV:434-436)
 // The reference's own solver (sux4j 5.4.1 Linear3SystemSolver) is not
