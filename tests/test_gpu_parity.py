@@ -332,7 +332,8 @@ def _rand_sigs(n, seed):
 
 
 @pytest.mark.parametrize("n,width", [(1, 0), (2, 8), (9, 0), (10, 16), (12, 3), (39, 64), (777, 5),
-                                     (1500, 0), (1501, 12), (3000, 1), (20_000, 4), (150_000, 32)])
+                                     (1500, 0), (1501, 12), (3000, 1), (20_000, 4), (150_000, 32),
+                                     (600_000, 4)])
 def test_gov_build_matches_oracle(ctx, n, width):
     """Device GOV build (sort, E, solve, sign) is bit-identical to oracle/bo_gov_build."""
     sig = _rand_sigs(n, n * 7 + width)
