@@ -838,8 +838,11 @@ __device__ bool try_seed(SolveLds &L, const ulonglong2 *sig, uint32_t cnt, uint3
                         fb = true;
                         break;
                     }
-                    // (loads issued 8 at a time before any is used)
-                    uint32_t key = 0;
+                    // (loads issued 8 at a time before any is used).  The two
+                    // best candidates turn heavy at once: any feedback vertex
+                    // set gives the same unique solution (and is singular
+                    // exactly when the block is); half the stuck cascades.
+                    uint32_t key = 0, key2 = 0;
                     for (uint32_t q0 = 0; q0 * 64 < sz; q0 += 8) {
                         uint32_t sv[8], dv[8];
 #pragma unroll
@@ -850,19 +853,35 @@ __device__ bool try_seed(SolveLds &L, const ulonglong2 *sig, uint32_t cnt, uint3
                         }
 #pragma unroll
                         for (uint32_t q = 0; q < 8; ++q)
-                            if (sv[q] == 0) key = max(key, (dv[q] << 16) | (0xFFFFu - (lane + 64 * (q0 + q))));
+                            if (sv[q] == 0) {
+                                const uint32_t k = (dv[q] << 16) | (0xFFFFu - (lane + 64 * (q0 + q)));
+                                key2 = max(key2, min(key, k));
+                                key = max(key, k);
+                            }
                     }
 #pragma unroll
-                    for (int d = 32; d >= 1; d >>= 1) key = max(key, (uint32_t)__shfl_xor((int)key, d, 64));
-                    const uint32_t hsel = 0xFFFFu - (key & 0xFFFFu);
+                    for (int d = 32; d >= 1; d >>= 1) {
+                        const uint32_t o1 = (uint32_t)__shfl_xor((int)key, d, 64), o2 = (uint32_t)__shfl_xor((int)key2, d, 64);
+                        key2 = max(min(key, o1), max(key2, o2));
+                        key = max(key, o1);
+                    }
                     if (lane == 0) {
+                        const uint32_t hsel = 0xFFFFu - (key & 0xFFFFu);
                         st[hsel] = 2;
                         hid[hsel] = (int16_t)nh;
                         rnd[hsel] = 0;
                         queue[qt] = (int16_t)hsel;
-                        L.qtail = qt + 1;
+                        uint32_t nt = qt + 1;
+                        if (key2) {
+                            const uint32_t h2 = 0xFFFFu - (key2 & 0xFFFFu);
+                            st[h2] = 2;
+                            hid[h2] = (int16_t)(nh + 1);
+                            rnd[h2] = 0;
+                            queue[nt++] = (int16_t)h2;
+                        }
+                        L.qtail = nt;
                     }
-                    ++nh;
+                    nh += key2 ? 2 : 1;
                     __builtin_amdgcn_wave_barrier();
                     qt = L.qtail;
                 }
