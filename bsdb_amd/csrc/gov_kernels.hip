@@ -30,7 +30,10 @@ namespace bsdb {
 constexpr int GS_THREADS = 1024;
 constexpr int GS_CMAX = 2048;    // keys per bucket handled (expected ~1500, sigma ~39)
 constexpr int GS_NVMAX = 2304;   // > vertex_offset span of GS_CMAX keys
-constexpr int GS_TINY = 12;      // brute-force buckets (only in sets of < ~1500 keys)
+constexpr int GS_TINY = 12;
+#ifndef GOV_PICK_REPS
+#define GOV_PICK_REPS 2  // FVS: pairs of heavy hinges taken per stuck cascade
+#endif      // brute-force buckets (only in sets of < ~1500 keys)
 constexpr int GS_WMAX = (GS_CMAX + 1 + 63) / 64;  // words per bit-sliced row
 
 enum GovStatus : uint32_t { GOV_TOO_BIG = 1u, GOV_SEEDS = 2u, GOV_DUP = 4u };
@@ -842,46 +845,51 @@ __device__ bool try_seed(SolveLds &L, const ulonglong2 *sig, uint32_t cnt, uint3
                     // best candidates turn heavy at once: any feedback vertex
                     // set gives the same unique solution (and is singular
                     // exactly when the block is); half the stuck cascades.
-                    uint32_t key = 0, key2 = 0;
-                    for (uint32_t q0 = 0; q0 * 64 < sz; q0 += 8) {
-                        uint32_t sv[8], dv[8];
+                    for (int rep = 0; rep < GOV_PICK_REPS; ++rep) {
+                        uint32_t key = 0, key2 = 0;
+                        for (uint32_t q0 = 0; q0 * 64 < sz; q0 += 8) {
+                            uint32_t sv[8], dv[8];
 #pragma unroll
-                        for (uint32_t q = 0; q < 8; ++q) {
-                            const uint32_t i = lane + 64 * (q0 + q);
-                            sv[q] = i < sz ? st[i] : 1u;
-                            dv[q] = i < sz ? indeg[i] : 0u;
-                        }
-#pragma unroll
-                        for (uint32_t q = 0; q < 8; ++q)
-                            if (sv[q] == 0) {
-                                const uint32_t k = (dv[q] << 16) | (0xFFFFu - (lane + 64 * (q0 + q)));
-                                key2 = max(key2, min(key, k));
-                                key = max(key, k);
+                            for (uint32_t q = 0; q < 8; ++q) {
+                                const uint32_t i = lane + 64 * (q0 + q);
+                                sv[q] = i < sz ? st[i] : 1u;
+                                dv[q] = i < sz ? indeg[i] : 0u;
                             }
-                    }
 #pragma unroll
-                    for (int d = 32; d >= 1; d >>= 1) {
-                        const uint32_t o1 = (uint32_t)__shfl_xor((int)key, d, 64), o2 = (uint32_t)__shfl_xor((int)key2, d, 64);
-                        key2 = max(min(key, o1), max(key2, o2));
-                        key = max(key, o1);
-                    }
-                    if (lane == 0) {
-                        const uint32_t hsel = 0xFFFFu - (key & 0xFFFFu);
-                        st[hsel] = 2;
-                        hid[hsel] = (int16_t)nh;
-                        rnd[hsel] = 0;
-                        queue[qt] = (int16_t)hsel;
-                        uint32_t nt = qt + 1;
-                        if (key2) {
-                            const uint32_t h2 = 0xFFFFu - (key2 & 0xFFFFu);
-                            st[h2] = 2;
-                            hid[h2] = (int16_t)(nh + 1);
-                            rnd[h2] = 0;
-                            queue[nt++] = (int16_t)h2;
+                            for (uint32_t q = 0; q < 8; ++q)
+                                if (sv[q] == 0) {
+                                    const uint32_t k = (dv[q] << 16) | (0xFFFFu - (lane + 64 * (q0 + q)));
+                                    key2 = max(key2, min(key, k));
+                                    key = max(key, k);
+                                }
                         }
-                        L.qtail = nt;
+#pragma unroll
+                        for (int d = 32; d >= 1; d >>= 1) {
+                            const uint32_t o1 = (uint32_t)__shfl_xor((int)key, d, 64), o2 = (uint32_t)__shfl_xor((int)key2, d, 64);
+                            key2 = max(min(key, o1), max(key2, o2));
+                            key = max(key, o1);
+                        }
+                        if (key == 0) break;  // (no open member left; wave-uniform)
+                        if (lane == 0) {
+                            const uint32_t hsel = 0xFFFFu - (key & 0xFFFFu);
+                            st[hsel] = 2;
+                            hid[hsel] = (int16_t)nh;
+                            rnd[hsel] = 0;
+                            queue[qt] = (int16_t)hsel;
+                            uint32_t nt = qt + 1;
+                            if (key2) {
+                                const uint32_t h2 = 0xFFFFu - (key2 & 0xFFFFu);
+                                st[h2] = 2;
+                                hid[h2] = (int16_t)(nh + 1);
+                                rnd[h2] = 0;
+                                queue[nt++] = (int16_t)h2;
+                            }
+                            L.qtail = nt;
+                        }
+                        nh += key2 ? 2 : 1;
+                        __builtin_amdgcn_wave_barrier();
+                        qt = L.qtail;
                     }
-                    nh += key2 ? 2 : 1;
                     __builtin_amdgcn_wave_barrier();
                     qt = L.qtail;
                 }
