@@ -32,7 +32,7 @@ constexpr int GS_CMAX = 2048;    // keys per bucket handled (expected ~1500, sig
 constexpr int GS_NVMAX = 2304;   // > vertex_offset span of GS_CMAX keys
 constexpr int GS_TINY = 12;
 #ifndef GOV_PICK_REPS
-#define GOV_PICK_REPS 4  // FVS: pairs of heavy hinges taken per stuck cascade
+#define GOV_PICK_REPS 8  // FVS: pairs of heavy hinges taken per stuck cascade
 #endif      // brute-force buckets (only in sets of < ~1500 keys)
 constexpr int GS_WMAX = (GS_CMAX + 1 + 63) / 64;  // words per bit-sliced row
 
