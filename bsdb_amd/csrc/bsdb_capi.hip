@@ -6,13 +6,18 @@
 // grown to the call's size), so a caller can capture them in a hipGraph.
 #include <hip/hip_runtime.h>
 
+#include <dlfcn.h>
+
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <mutex>
 #include <new>
+#include <thread>
 #include <vector>
 
 #include "../../include/bsdb_mi355x.h"
@@ -21,6 +26,16 @@
 #include "gov_kernels.hip"
 
 using namespace bsdb;
+
+// One slot of the double-buffered host feed: device buffers of a batch and
+// the events of its copy and of the compute that read it.
+struct FeedSlot {
+    void *buf[8] = {};
+    size_t cap[8] = {};
+    hipEvent_t copied = nullptr, done = nullptr;
+    bool used = false;
+    std::vector<uint64_t> reb;  // rebased var-len offsets of the batch (host)
+};
 
 struct bsdb_ctx {
     int device = 0;
@@ -43,16 +58,26 @@ struct bsdb_ctx {
     uint32_t *overflow = nullptr; // 1 word
     uint64_t *scan_part = nullptr;
     size_t scan_part_n = 0;
-    // host-API staging
-    uint8_t *d_keys = nullptr;
-    size_t d_keys_bytes = 0;
-    uint64_t *d_off = nullptr;  // host var-len entry points: a batch's rebased offsets
-    size_t d_off_bytes = 0;
+    // host-API staging: two feed slots (double-buffered uploads on copy_stream)
+    FeedSlot feed[2];
+    hipStream_t copy_stream = nullptr;
     void *d_out = nullptr;
     size_t d_out_bytes = 0;
     // GOV build workspace
     void *g_sorted = nullptr, *g_counts = nullptr, *g_cursor = nullptr, *g_scratch = nullptr, *g_status = nullptr;
     size_t g_sorted_bytes = 0, g_counts_bytes = 0, g_cursor_bytes = 0, g_scratch_bytes = 0, g_status_bytes = 0;
+    void *g_big = nullptr, *g_slabs = nullptr;  // oversized buckets: list, sort + solver slabs
+    size_t g_big_bytes = 0, g_slabs_bytes = 0;
+    bool verify = false;
+    // ordering of workspace use across streams: the last call's
+    // completion event and stream
+    hipEvent_t last_ev = nullptr;
+    hipStream_t last_stream = nullptr;
+    // RCCL rank (bsdb_comm_init) and the finalize packing buffer
+    void *comm = nullptr;
+    int nranks = 1, rank = 0;
+    void *pack = nullptr;
+    size_t pack_bytes = 0;
     // live profiling: event pairs per launch, per kind
     bool profiling = false;
     struct Rec { hipEvent_t a, b; int kind; uint64_t keys; };
@@ -63,6 +88,24 @@ struct bsdb_ctx {
         hipEvent_t e = nullptr;
         (void)hipEventCreate(&e);
         return e;
+    }
+};
+
+// A call that uses the context's workspace on stream s first waits for the
+// previous such call when that one ran on another stream, and leaves its own
+// completion event behind (launches are asynchronous: without this, two dev
+// calls on different streams, or a host call on the private stream beside a
+// dev call, would race on the shared buffers).
+struct Ordered {
+    bsdb_ctx *c;
+    hipStream_t s;
+    Ordered(bsdb_ctx *c_, hipStream_t s_) : c(c_), s(s_) {
+        if (c->last_ev && c->last_stream != s) (void)hipStreamWaitEvent(s, c->last_ev, 0);
+    }
+    ~Ordered() {
+        if (!c->last_ev && hipEventCreateWithFlags(&c->last_ev, hipEventDisableTiming) != hipSuccess) c->last_ev = nullptr;
+        if (c->last_ev) (void)hipEventRecord(c->last_ev, s);
+        c->last_stream = s;
     }
 };
 
@@ -79,6 +122,8 @@ struct ProfScope {
         c->recs.push_back({a, b, kind, keys});
     }
 };
+
+static void comm_destroy(bsdb_ctx *c);  // capi_comm.hip
 
 namespace {
 
@@ -425,6 +470,10 @@ int hash_impl(bsdb_ctx *c, const uint8_t *keys, const uint64_t *offsets, uint64_
 
 bool aligned16(const void *p) { return ((uintptr_t)p & 15) == 0; }
 
+// BSDBWriter.put keys are 1..255 bytes (Common.java MAX_KEY_SIZE); a fixed
+// layout of 0-byte keys is rejected
+bool bad_key_len(uint32_t key_len) { return key_len == 0 || key_len > 255; }
+
 }  // namespace
 
 extern "C" {
@@ -441,6 +490,9 @@ const char *bsdb_strerror(int code) {
         case BSDB_EDUP: return "duplicate key signature";
         case BSDB_ESEEDS: return "exhausted local seeds";
         case BSDB_E2BIG: return "bucket too large for the device solver";
+        case BSDB_ECOMM: return "RCCL unavailable or collective failed";
+        case BSDB_EFILE: return "file open/read/write failed";
+        case BSDB_EVERIFY: return "built MPHF failed the bijection check";
         default: return "unknown error";
     }
 }
@@ -486,14 +538,24 @@ int bsdb_close(bsdb_ctx *c) {
     (void)hipFree(c->p2_pref);
     (void)hipFree(c->overflow);
     (void)hipFree(c->scan_part);
-    (void)hipFree(c->d_keys);
-    (void)hipFree(c->d_off);
+    if (c->copy_stream) (void)hipStreamSynchronize(c->copy_stream);
+    for (auto &f : c->feed) {
+        for (void *p : f.buf) (void)hipFree(p);
+        if (f.copied) (void)hipEventDestroy(f.copied);
+        if (f.done) (void)hipEventDestroy(f.done);
+    }
+    if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
     (void)hipFree(c->d_out);
     (void)hipFree(c->g_sorted);
     (void)hipFree(c->g_counts);
     (void)hipFree(c->g_cursor);
     (void)hipFree(c->g_scratch);
     (void)hipFree(c->g_status);
+    (void)hipFree(c->g_big);
+    (void)hipFree(c->g_slabs);
+    (void)hipFree(c->pack);
+    comm_destroy(c);
+    if (c->last_ev) (void)hipEventDestroy(c->last_ev);
     for (auto &r : c->recs) { (void)hipEventDestroy(r.a); (void)hipEventDestroy(r.b); }
     for (auto e : c->pool) (void)hipEventDestroy(e);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -535,7 +597,8 @@ int bsdb_set_chunk_keys(bsdb_ctx *c, uint64_t chunk_keys) {
 
 int bsdb_dev_hash_fixed(bsdb_ctx *c, const uint8_t *d_keys, uint32_t key_len, uint64_t n, uint64_t seed,
                         uint64_t *d_sig, void *stream) {
-    if (!c || (n && (!d_keys || !d_sig)) || !aligned16(d_keys) || !aligned16(d_sig)) return BSDB_EINVAL;
+    if (!c || bad_key_len(key_len) || (n && (!d_keys || !d_sig)) || !aligned16(d_keys) || !aligned16(d_sig))
+        return BSDB_EINVAL;
     std::lock_guard<std::mutex> g(c->mu);
     HIP_OK(hipSetDevice(c->device));
     return hash_impl(c, d_keys, nullptr, n * key_len, key_len, n, seed, d_sig, pick(c, stream));
@@ -551,9 +614,11 @@ int bsdb_dev_hash_var(bsdb_ctx *c, const uint8_t *d_blob, uint64_t blob_bytes, c
 
 int bsdb_dev_histogram_fixed(bsdb_ctx *c, const uint8_t *d_keys, uint32_t key_len, uint64_t n, uint64_t seed,
                              uint64_t m, uint32_t *d_counts, void *stream) {
-    if (!c || m == 0 || m > 0x7FFFFFFFULL || (n && (!d_keys || !d_counts)) || !aligned16(d_keys)) return BSDB_EINVAL;
+    if (!c || bad_key_len(key_len) || m == 0 || m > 0x7FFFFFFFULL || (n && (!d_keys || !d_counts)) || !aligned16(d_keys))
+        return BSDB_EINVAL;
     std::lock_guard<std::mutex> g(c->mu);
     HIP_OK(hipSetDevice(c->device));
+    Ordered ord(c, pick(c, stream));
     return histogram_impl(c, d_keys, nullptr, n * key_len, key_len, n, seed, m, d_counts, pick(c, stream));
 }
 
@@ -562,6 +627,7 @@ int bsdb_dev_histogram_var(bsdb_ctx *c, const uint8_t *d_blob, uint64_t blob_byt
     if (!c || m == 0 || m > 0x7FFFFFFFULL || (n && (!d_blob || !d_off || !d_counts))) return BSDB_EINVAL;
     std::lock_guard<std::mutex> g(c->mu);
     HIP_OK(hipSetDevice(c->device));
+    Ordered ord(c, pick(c, stream));
     return histogram_impl(c, d_blob, d_off, blob_bytes, 0, n, seed, m, d_counts, pick(c, stream));
 }
 
@@ -571,6 +637,7 @@ int bsdb_dev_edge_offsets(bsdb_ctx *c, const uint32_t *d_counts, uint64_t m, uin
     if (!c || m == 0 || !d_counts || !d_E) return BSDB_EINVAL;
     std::lock_guard<std::mutex> g(c->mu);
     HIP_OK(hipSetDevice(c->device));
+    Ordered ord(c, pick(c, stream));
     return edge_offsets_impl(c, d_counts, m, d_E, stream);
 }
 
@@ -604,6 +671,7 @@ int bsdb_dev_gen_keys_var(bsdb_ctx *c, uint64_t first, uint64_t n, uint64_t *d_o
     std::lock_guard<std::mutex> g(c->mu);
     HIP_OK(hipSetDevice(c->device));
     hipStream_t s = pick(c, stream);
+    Ordered ord(c, s);
     if (n == 0) {
         HIP_OK(hipMemsetAsync(d_offsets, 0, 8, s));
         return launch_status();
@@ -661,6 +729,128 @@ static uint32_t grid_for(const bsdb_ctx *c, uint64_t n) {
 // ---- GOV build on the device (A5, A6, A8, A11) -------------------------------
 uint64_t bsdb_values_words(uint64_t n) { return (2 * (1 + ((n * 281) >> 8)) + 63) / 64; }
 
+static void print_gov_profile(const std::vector<uint64_t> &h, uint32_t solve_grid, uint64_t m) {
+    const char *names[GP_N] = {"edges", "peel", "greedy", "bfs", "tarjan", "singletons", "dense", "back",
+                               "store", "n_seeds", "n_bfs", "n_bfs_pops", "n_dense_rows", "n_dense_max",
+                               "n_core", "n_blocks", "n_rows_in_blocks_over_440", "n_scc_sweeps",
+                               "n_small_scc_fallbacks", "fvs_select", "fvs_forms", "fvs_gauss_jordan"};
+    std::vector<double> tot(GP_N, 0.0);
+    for (uint32_t w = 0; w < solve_grid; ++w)
+        for (int k = 0; k < GP_N; ++k) {
+            const double v = (double)h[(size_t)w * GP_N + k];
+            tot[k] = k == GP_N_DENSE_MAX ? std::max(tot[k], v) : tot[k] + v;
+        }
+    fprintf(stderr, "[gov-profile] m=%llu grid=%u", (unsigned long long)m, solve_grid);
+    for (int k = 0; k < GP_N; ++k)
+        fprintf(stderr, " %s=%.4g", names[k], k == GP_N_DENSE_MAX ? tot[k] : tot[k] / ((k < GP_N_SEEDS || k >= GP_FVS_SEL) ? solve_grid : 1));
+    fprintf(stderr, "  (cycles: mean per workgroup; counts: totals)\n");
+}
+
+struct DevFree {
+    void operator()(void *p) const { if (p) (void)hipFree(p); }
+};
+
+// A5 + A6 + A8 + A11 over the buckets [b_lo, b_hi) of a GOV structure on
+// n_global keys; d_sig = the n_local signatures of that range.  full: a whole
+// build (zeroes the outputs first); otherwise the caller zeroed full-size
+// outputs and E[b_hi] is cleared again unless b_hi == m (the next range owns it).
+static int gov_build_impl(bsdb_ctx *c, const uint64_t *d_sig, uint64_t n_local, uint64_t n_global, uint64_t b_lo,
+                          uint64_t b_hi, uint64_t e_lo, uint32_t width, uint64_t *d_E, uint64_t *d_values,
+                          uint64_t *d_sigbits, hipStream_t s, bool full) {
+    const uint64_t m = n_global / BUCKET_SIZE + 1, nb = b_hi - b_lo;
+    const uint32_t mult = (uint32_t)(2 * m);
+    int rc;
+    if ((rc = grow(&c->g_sorted, &c->g_sorted_bytes, std::max<uint64_t>(n_local, 1) * 16))) return rc;
+    if ((rc = grow(&c->g_counts, &c->g_counts_bytes, std::max<uint64_t>(nb, 1) * 4))) return rc;
+    if ((rc = grow(&c->g_cursor, &c->g_cursor_bytes, std::max<uint64_t>(nb, 1) * 8))) return rc;
+    if ((rc = grow(&c->g_status, &c->g_status_bytes, 16))) return rc;
+    const uint32_t big_cap = (uint32_t)(n_local / (GS_CMAX + 1) + 1);
+    if ((rc = grow(&c->g_big, &c->g_big_bytes, (size_t)big_cap * 4))) return rc;
+    const uint32_t solve_grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(nb, (uint64_t)c->num_cus));
+    if ((rc = grow(&c->g_scratch, &c->g_scratch_bytes, (size_t)solve_grid * solve_scratch_words<SolveLds>() * 8)))
+        return rc;
+    uint32_t *counts = (uint32_t *)c->g_counts, *status = (uint32_t *)c->g_status;
+    uint64_t *sorted = (uint64_t *)c->g_sorted;
+    HIP_OK(hipMemsetAsync(counts, 0, std::max<uint64_t>(nb, 1) * 4, s));
+    HIP_OK(hipMemsetAsync(status, 0, 16, s));
+    if (full) HIP_OK(hipMemsetAsync(d_values, 0, bsdb_values_words(n_global) * 8, s));
+    const uint32_t grid = grid_for(c, n_local);
+    uint64_t *Eb = d_E + b_lo;
+    if (n_local) k_bucket_count<<<grid, 256, 0, s>>>(d_sig, n_local, mult, (uint32_t)b_lo, counts);
+    if ((rc = edge_offsets_impl(c, counts, nb, Eb, s))) return rc;  // A6: Eb[0..nb]
+    if (e_lo) k_add_base<<<grid_for(c, nb + 1), 256, 0, s>>>(Eb, nb + 1, e_lo);
+    k_cursor_init<<<grid_for(c, nb), 256, 0, s>>>(Eb, nb, e_lo, (uint64_t *)c->g_cursor);
+    if (n_local)
+        k_bucket_scatter<<<grid, 256, 0, s>>>(d_sig, n_local, mult, (uint32_t)b_lo, (unsigned long long *)c->g_cursor,
+                                              sorted);
+    k_bucket_sort<<<(uint32_t)std::min<uint64_t>(nb, (uint64_t)c->num_cus * 8), 256, 0, s>>>(sorted, Eb, nb, e_lo,
+                                                                                              status);  // A5
+    k_big_list<<<grid_for(c, nb), 256, 0, s>>>(Eb, nb, status, (uint32_t *)c->g_big, big_cap);
+    if ((rc = launch_status())) return rc;
+    uint32_t st[4] = {0, 0, 0, 0};
+    HIP_OK(hipMemcpyAsync(st, status, 16, hipMemcpyDeviceToHost, s));
+    HIP_OK(hipStreamSynchronize(s));
+    if (st[0] & GOV_DUP) return BSDB_EDUP;
+    if (st[0] & GOV_TOO_BIG) return BSDB_E2BIG;
+    const uint32_t nbig = std::min(st[3], big_cap);
+    const uint32_t big_grid = std::min<uint32_t>(nbig, 8);
+    if (nbig) {
+        // oversized buckets: per-workgroup slabs for the sort, then the solver
+        const size_t sort_bytes = (size_t)big_grid * GB_CMAX * 16;
+        if ((rc = grow(&c->g_slabs, &c->g_slabs_bytes, std::max(sort_bytes, (size_t)big_grid * big_slab_bytes()))))
+            return rc;
+        k_bucket_sort_big<<<big_grid, GB_THREADS, 0, s>>>(sorted, Eb, e_lo, (const uint32_t *)c->g_big, nbig,
+                                                          (ulonglong2 *)c->g_slabs, status);
+    }
+    // BSDB_GOV_PROFILE=1: per-phase cycle totals of the solver printed to stderr
+    const bool gprof = getenv("BSDB_GOV_PROFILE") != nullptr;
+    std::unique_ptr<void, DevFree> prof_buf;
+    uint64_t *d_prof = nullptr;
+    if (gprof) {
+        void *p = nullptr;
+        HIP_OK(hipMalloc(&p, (size_t)solve_grid * GP_N * 8));
+        prof_buf.reset(p);
+        d_prof = (uint64_t *)p;
+        HIP_OK(hipMemsetAsync(d_prof, 0, (size_t)solve_grid * GP_N * 8, s));
+    }
+    uint32_t fvs_max = FVS_NH_MAX;
+    if (const char *v = getenv("BSDB_GOV_FVS_MAX")) fvs_max = (uint32_t)std::max(2, std::min(atoi(v), (int)FVS_NH_MAX));
+    SolveArgs sa{sorted, b_hi, d_E, d_values, (uint64_t *)c->g_scratch, status, d_prof, fvs_max, b_lo, e_lo};
+    // zeroing status[2] (the bucket queue) above happens before both launches
+    k_gov_solve<<<solve_grid, GS_THREADS, 0, s>>>(sa);  // A8
+    if (nbig)
+        k_gov_solve_big<<<big_grid, GS_THREADS, 0, s>>>(sa, (const uint32_t *)c->g_big, nbig, (uint8_t *)c->g_slabs,
+                                                        big_slab_bytes());
+    if (gprof) {
+        std::vector<uint64_t> h((size_t)solve_grid * GP_N);
+        HIP_OK(hipMemcpyAsync(h.data(), d_prof, h.size() * 8, hipMemcpyDeviceToHost, s));
+        HIP_OK(hipStreamSynchronize(s));
+        print_gov_profile(h, solve_grid, m);
+    }
+    const MphView v{d_E, d_values, nullptr, n_global, mult, width};
+    if (width) {
+        if (full) HIP_OK(hipMemsetAsync(d_sigbits, 0, ((n_global * width + 63) / 64 + 1) * 8, s));
+        if (n_local) k_sign<<<grid, 256, 0, s>>>(v, sorted, n_local, d_sigbits);  // A11
+    }
+    if (c->verify && n_local) {
+        void *p = nullptr;
+        HIP_OK(hipMalloc(&p, ((n_local + 63) / 64) * 8));
+        std::unique_ptr<void, DevFree> bm(p);
+        HIP_OK(hipMemsetAsync(p, 0, ((n_local + 63) / 64) * 8, s));
+        k_verify_ranks<<<grid, 256, 0, s>>>(v, sorted, n_local, e_lo, (unsigned long long *)p, status);
+        HIP_OK(hipStreamSynchronize(s));
+    }
+    if (b_hi < m) HIP_OK(hipMemsetAsync(d_E + b_hi, 0, 8, s));  // owned by the next range
+    if ((rc = launch_status())) return rc;
+    HIP_OK(hipMemcpyAsync(st, status, 4, hipMemcpyDeviceToHost, s));
+    HIP_OK(hipStreamSynchronize(s));
+    if (st[0] & GOV_DUP) return BSDB_EDUP;
+    if (st[0] & GOV_TOO_BIG) return BSDB_E2BIG;
+    if (st[0] & GOV_SEEDS) return BSDB_ESEEDS;
+    if (st[0] & GOV_VERIFY) return BSDB_EVERIFY;
+    return BSDB_OK;
+}
+
 int bsdb_dev_gov_build(bsdb_ctx *c, const uint64_t *d_sig, uint64_t n, uint32_t width, uint64_t *d_E,
                        uint64_t *d_values, uint64_t *d_sigbits, void *stream) {
     const uint64_t m = n / BUCKET_SIZE + 1;
@@ -670,67 +860,59 @@ int bsdb_dev_gov_build(bsdb_ctx *c, const uint64_t *d_sig, uint64_t n, uint32_t 
     std::lock_guard<std::mutex> g(c->mu);
     HIP_OK(hipSetDevice(c->device));
     hipStream_t s = pick(c, stream);
-    const uint32_t mult = (uint32_t)(2 * m);
+    Ordered ord(c, s);
+    return gov_build_impl(c, d_sig, n, n, 0, m, 0, width, d_E, d_values, d_sigbits, s, true);
+}
+
+int bsdb_dev_gov_build_range(bsdb_ctx *c, const uint64_t *d_sig, uint64_t n_local, uint64_t n_global, uint64_t b_lo,
+                             uint64_t b_hi, uint64_t e_lo, uint32_t width, uint64_t *d_E, uint64_t *d_values,
+                             uint64_t *d_sigbits, void *stream) {
+    const uint64_t m = n_global / BUCKET_SIZE + 1;
+    if (!c || width > 64 || !d_E || !d_values || (n_local && !d_sig) || (width && !d_sigbits) || !aligned16(d_sig) ||
+        m > 0x7FFFFFFFULL || b_lo >= b_hi || b_hi > m || n_local > n_global || e_lo + n_local > n_global)
+        return BSDB_EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    HIP_OK(hipSetDevice(c->device));
+    hipStream_t s = pick(c, stream);
+    Ordered ord(c, s);
+    return gov_build_impl(c, d_sig, n_local, n_global, b_lo, b_hi, e_lo, width, d_E, d_values, d_sigbits, s, false);
+}
+
+int bsdb_dev_partition_owners(bsdb_ctx *c, const uint64_t *d_sig, uint64_t n, uint64_t m, int nranks,
+                              uint64_t *d_out, uint64_t *h_counts, void *stream) {
+    if (!c || nranks < 1 || nranks > OWN_MAXR || m == 0 || m > 0x7FFFFFFFULL || !h_counts ||
+        (n && (!d_sig || !d_out)) || !aligned16(d_sig) || !aligned16(d_out))
+        return BSDB_EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    HIP_OK(hipSetDevice(c->device));
+    hipStream_t s = pick(c, stream);
+    Ordered ord(c, s);
     int rc;
-    if ((rc = grow(&c->g_sorted, &c->g_sorted_bytes, std::max<uint64_t>(n, 1) * 16))) return rc;
-    if ((rc = grow(&c->g_counts, &c->g_counts_bytes, m * 4))) return rc;
-    if ((rc = grow(&c->g_cursor, &c->g_cursor_bytes, m * 8))) return rc;
-    if ((rc = grow(&c->g_status, &c->g_status_bytes, 16))) return rc;
-    const uint32_t solve_grid = (uint32_t)std::min<uint64_t>(m, (uint64_t)c->num_cus);
-    if ((rc = grow(&c->g_scratch, &c->g_scratch_bytes, (size_t)solve_grid * 2 * GS_CMAX * GS_WMAX * 8))) return rc;
-    uint32_t *counts = (uint32_t *)c->g_counts, *status = (uint32_t *)c->g_status;
-    HIP_OK(hipMemsetAsync(counts, 0, m * 4, s));
-    HIP_OK(hipMemsetAsync(status, 0, 16, s));
-    HIP_OK(hipMemsetAsync(d_values, 0, bsdb_values_words(n) * 8, s));
-    const uint32_t grid = grid_for(c, n);
-    if (n) k_bucket_count<<<grid, 256, 0, s>>>(d_sig, n, mult, counts);
-    if ((rc = edge_offsets_impl(c, counts, m, d_E, s))) return rc;                 // A6
-    k_cursor_init<<<grid_for(c, m), 256, 0, s>>>(d_E, m, (uint64_t *)c->g_cursor);
-    if (n) k_bucket_scatter<<<grid, 256, 0, s>>>(d_sig, n, mult, (unsigned long long *)c->g_cursor,
-                                                 (uint64_t *)c->g_sorted);
-    k_bucket_sort<<<(uint32_t)std::min<uint64_t>(m, (uint64_t)c->num_cus * 8), 256, 0, s>>>(
-        (uint64_t *)c->g_sorted, d_E, m, status);                                 // A5
-    // BSDB_GOV_PROFILE=1: per-phase cycle totals of the solver printed to stderr
-    const bool gprof = getenv("BSDB_GOV_PROFILE") != nullptr;
-    uint64_t *d_prof = nullptr;
-    if (gprof) {
-        HIP_OK(hipMalloc(&d_prof, (size_t)solve_grid * GP_N * 8));
-        HIP_OK(hipMemsetAsync(d_prof, 0, (size_t)solve_grid * GP_N * 8, s));
-    }
-    SolveArgs sa{(const uint64_t *)c->g_sorted, m, d_E, d_values, (uint64_t *)c->g_scratch, status, d_prof};
-    k_gov_solve<<<solve_grid, GS_THREADS, 0, s>>>(sa);                              // A8
-    if (gprof) {
-        std::vector<uint64_t> h((size_t)solve_grid * GP_N);
-        HIP_OK(hipMemcpyAsync(h.data(), d_prof, h.size() * 8, hipMemcpyDeviceToHost, s));
-        HIP_OK(hipStreamSynchronize(s));
-        (void)hipFree(d_prof);
-        const char *names[GP_N] = {"edges", "peel", "greedy", "bfs", "tarjan", "singletons", "dense", "back",
-                                   "store", "n_seeds", "n_bfs", "n_bfs_pops", "n_dense_rows", "n_dense_max",
-                                   "n_core", "n_blocks", "n_rows_in_blocks_over_440", "n_scc_sweeps",
-                                   "n_small_scc_fallbacks", "fvs_select", "fvs_forms", "fvs_gauss_jordan"};
-        std::vector<double> tot(GP_N, 0.0);
-        for (uint32_t w = 0; w < solve_grid; ++w)
-            for (int k = 0; k < GP_N; ++k) {
-                const double v = (double)h[(size_t)w * GP_N + k];
-                tot[k] = k == GP_N_DENSE_MAX ? std::max(tot[k], v) : tot[k] + v;
-            }
-        fprintf(stderr, "[gov-profile] m=%llu grid=%u", (unsigned long long)m, solve_grid);
-        for (int k = 0; k < GP_N; ++k)
-            fprintf(stderr, " %s=%.4g", names[k], k == GP_N_DENSE_MAX ? tot[k] : tot[k] / ((k < GP_N_SEEDS || k >= GP_FVS_SEL) ? solve_grid : 1));
-        fprintf(stderr, "  (cycles: mean per workgroup; counts: totals)\n");
-    }
-    if (width) {
-        HIP_OK(hipMemsetAsync(d_sigbits, 0, ((n * width + 63) / 64 + 1) * 8, s));
-        const MphView v{d_E, d_values, nullptr, n, mult, width};
-        if (n) k_sign<<<grid, 256, 0, s>>>(v, (const uint64_t *)c->g_sorted, n, d_sigbits);   // A11
-    }
+    if ((rc = grow(&c->g_cursor, &c->g_cursor_bytes, std::max<size_t>(c->g_cursor_bytes, OWN_MAXR * 8)))) return rc;
+    unsigned long long *cur = (unsigned long long *)c->g_cursor;
+    HIP_OK(hipMemsetAsync(cur, 0, OWN_MAXR * 8, s));
+    if (n) k_owner_count<<<grid_for(c, n), 256, 0, s>>>(d_sig, n, (uint32_t)(2 * m), m, (uint32_t)nranks, cur);
     if ((rc = launch_status())) return rc;
-    uint32_t st = 0;
-    HIP_OK(hipMemcpyAsync(&st, status, 4, hipMemcpyDeviceToHost, s));
+    uint64_t cnt[OWN_MAXR];
+    HIP_OK(hipMemcpyAsync(cnt, cur, nranks * 8, hipMemcpyDeviceToHost, s));
     HIP_OK(hipStreamSynchronize(s));
-    if (st & GOV_DUP) return BSDB_EDUP;
-    if (st & GOV_TOO_BIG) return BSDB_E2BIG;
-    if (st & GOV_SEEDS) return BSDB_ESEEDS;
+    uint64_t start[OWN_MAXR], acc = 0;
+    for (int g2 = 0; g2 < nranks; ++g2) {
+        start[g2] = acc;
+        acc += cnt[g2];
+        h_counts[g2] = cnt[g2];
+    }
+    HIP_OK(hipMemcpyAsync(cur, start, nranks * 8, hipMemcpyHostToDevice, s));
+    if (n) k_owner_scatter<<<grid_for(c, n), 256, 0, s>>>(d_sig, n, (uint32_t)(2 * m), m, (uint32_t)nranks, cur, d_out);
+    if ((rc = launch_status())) return rc;
+    HIP_OK(hipStreamSynchronize(s));  // start[] is a stack buffer
+    return BSDB_OK;
+}
+
+int bsdb_set_verify(bsdb_ctx *c, int enable) {
+    if (!c) return BSDB_EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    c->verify = enable != 0;
     return BSDB_OK;
 }
 
@@ -775,51 +957,56 @@ int bsdb_dev_index_scatter(bsdb_ctx *c, const int64_t *d_rank, const uint64_t *d
     return launch_status();
 }
 
+}  // extern "C" (the definitions below keep the C linkage of their header declarations)
+
 // ---- host-buffer entry points ---------------------------------------------
-int bsdb_histogram_fixed(bsdb_ctx *c, const uint8_t *h_keys, uint32_t key_len, uint64_t n, uint64_t seed,
-                         uint64_t m, uint32_t *h_counts) {
-    if (!c || m == 0 || m > 0x7FFFFFFFULL || (n && !h_keys) || !h_counts) return BSDB_EINVAL;
-    std::lock_guard<std::mutex> g(c->mu);
-    HIP_OK(hipSetDevice(c->device));
-    hipStream_t s = c->stream;
-    const uint64_t batch = std::max<uint64_t>(P1_TILE, (256ULL << 20) / std::max<uint32_t>(key_len, 1) / P1_TILE * P1_TILE);
-    int rc = grow((void **)&c->d_keys, &c->d_keys_bytes, (size_t)std::min(batch, std::max<uint64_t>(n, 1)) * std::max<uint32_t>(key_len, 1) + 16);
-    if (rc) return rc;
-    rc = grow(&c->d_out, &c->d_out_bytes, m * sizeof(uint32_t));
-    if (rc) return rc;
-    uint32_t *d_counts = (uint32_t *)c->d_out;
-    HIP_OK(hipMemsetAsync(d_counts, 0, m * sizeof(uint32_t), s));
-    for (uint64_t k0 = 0; k0 < n; k0 += batch) {
-        const uint64_t nk = std::min(batch, n - k0);
-        HIP_OK(hipMemcpyAsync(c->d_keys, h_keys + k0 * key_len, nk * key_len, hipMemcpyHostToDevice, s));
-        if ((rc = histogram_impl(c, c->d_keys, nullptr, nk * key_len, key_len, nk, seed, m, d_counts, s))) return rc;
+// Keys in host memory reach the device through two feed slots: batch i is
+// copied on the context's copy stream into slot i % 2 while batch i-1's
+// kernels run on the compute stream (c->stream); a slot is refilled only after
+// the compute that read it finished (F3: copy and compute overlap).
+
+static int feed_init(bsdb_ctx *c) {
+    if (c->copy_stream) return BSDB_OK;
+    HIP_OK(hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
+    for (auto &f : c->feed) {
+        HIP_OK(hipEventCreateWithFlags(&f.copied, hipEventDisableTiming));
+        HIP_OK(hipEventCreateWithFlags(&f.done, hipEventDisableTiming));
     }
-    std::vector<uint32_t> tmp(m);
-    HIP_OK(hipMemcpyAsync(tmp.data(), d_counts, m * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-    HIP_OK(hipStreamSynchronize(s));
-    for (uint64_t b = 0; b < m; ++b) h_counts[b] += tmp[b];
     return BSDB_OK;
 }
 
-int bsdb_hash_fixed(bsdb_ctx *c, const uint8_t *h_keys, uint32_t key_len, uint64_t n, uint64_t seed,
-                    uint64_t *h_sig) {
-    if (!c || (n && (!h_keys || !h_sig))) return BSDB_EINVAL;
-    std::lock_guard<std::mutex> g(c->mu);
-    HIP_OK(hipSetDevice(c->device));
-    hipStream_t s = c->stream;
-    const uint64_t batch = std::max<uint64_t>(P1_TILE, (64ULL << 20) / std::max<uint32_t>(key_len, 1) / P1_TILE * P1_TILE);
-    const uint64_t cap = std::min(batch, std::max<uint64_t>(n, 1));
-    int rc = grow((void **)&c->d_keys, &c->d_keys_bytes, (size_t)cap * std::max<uint32_t>(key_len, 1) + 16);
+// Streams records [0, n) in batches [k0, next(k0)): upload(slot, k0, k1)
+// issues the batch's copies on the copy stream, compute(slot, k0, k1) its
+// kernels on c->stream.
+template <class Next, class Upload, class Compute>
+static int feed_batches(bsdb_ctx *c, uint64_t n, Next &&next, Upload &&upload, Compute &&compute) {
+    int rc = feed_init(c);
     if (rc) return rc;
-    rc = grow(&c->d_out, &c->d_out_bytes, cap * 16);
-    if (rc) return rc;
-    for (uint64_t k0 = 0; k0 < n; k0 += batch) {
-        const uint64_t nk = std::min(batch, n - k0);
-        HIP_OK(hipMemcpyAsync(c->d_keys, h_keys + k0 * key_len, nk * key_len, hipMemcpyHostToDevice, s));
-        if ((rc = hash_impl(c, c->d_keys, nullptr, nk * key_len, key_len, nk, seed, (uint64_t *)c->d_out, s))) return rc;
-        HIP_OK(hipMemcpyAsync(h_sig + 2 * k0, c->d_out, nk * 16, hipMemcpyDeviceToHost, s));
+    int i = 0;
+    for (uint64_t k0 = 0; k0 < n; ++i) {
+        const uint64_t k1 = next(k0);
+        FeedSlot &f = c->feed[i & 1];
+        if (f.used) HIP_OK(hipEventSynchronize(f.done));  // also frees the slot's host staging (reb)
+        if ((rc = upload(f, k0, k1))) return rc;
+        HIP_OK(hipEventRecord(f.copied, c->copy_stream));
+        HIP_OK(hipStreamWaitEvent(c->stream, f.copied, 0));
+        if ((rc = compute(f, k0, k1))) return rc;
+        HIP_OK(hipEventRecord(f.done, c->stream));
+        f.used = true;
+        k0 = k1;
     }
-    HIP_OK(hipStreamSynchronize(s));
+    return BSDB_OK;
+}
+
+static uint64_t fixed_batch(uint32_t key_len, uint64_t bytes) {
+    return std::max<uint64_t>(P1_TILE, bytes / key_len / P1_TILE * P1_TILE);
+}
+
+// Fixed-length keys of a batch into slot buffer 0 (+16 B of slack).
+static int upload_fixed(bsdb_ctx *c, FeedSlot &f, const uint8_t *h_keys, uint32_t key_len, uint64_t k0, uint64_t k1) {
+    int rc = grow(&f.buf[0], &f.cap[0], (size_t)(k1 - k0) * key_len + 16);
+    if (rc) return rc;
+    HIP_OK(hipMemcpyAsync(f.buf[0], h_keys + k0 * key_len, (k1 - k0) * key_len, hipMemcpyHostToDevice, c->copy_stream));
     return BSDB_OK;
 }
 
@@ -833,24 +1020,95 @@ static uint64_t var_batch_end(const uint64_t *off, uint64_t k0, uint64_t n) {
     return k1;
 }
 
-// One batch to the device: key bytes into c->d_keys, rebased offsets into
-// c->d_off (pinned by the stream order: the host copy `reb` outlives the
-// synchronous wait the callers do per batch).
-static int var_batch_upload(bsdb_ctx *c, const uint8_t *h_blob, const uint64_t *h_off, uint64_t k0, uint64_t k1,
-                            std::vector<uint64_t> &reb, hipStream_t s) {
-    const uint64_t nk = k1 - k0, bytes = h_off[k1] - h_off[k0];
-    int rc = grow((void **)&c->d_keys, &c->d_keys_bytes, (size_t)bytes + 16);
+// A var-len batch: key bytes into slot buffer 0, offsets rebased to the
+// batch into buffer 1 (host copy f.reb lives until the slot is reused).
+static int upload_var(bsdb_ctx *c, FeedSlot &f, const uint8_t *h_blob, const uint64_t *h_off, uint64_t k0,
+                      uint64_t k1) {
+    const uint64_t nk = k1 - k0;
+    if (h_off[k1] < h_off[k0]) return BSDB_EINVAL;
+    const uint64_t bytes = h_off[k1] - h_off[k0];
+    int rc = grow(&f.buf[0], &f.cap[0], (size_t)bytes + 16);
     if (rc) return rc;
-    rc = grow((void **)&c->d_off, &c->d_off_bytes, (size_t)(nk + 1) * sizeof(uint64_t));
-    if (rc) return rc;
-    reb.resize(nk + 1);
+    if ((rc = grow(&f.buf[1], &f.cap[1], (size_t)(nk + 1) * 8))) return rc;
+    f.reb.resize(nk + 1);
     for (uint64_t i = 0; i <= nk; ++i) {
         if (h_off[k0 + i] < h_off[k0] || (i && h_off[k0 + i] < h_off[k0 + i - 1])) return BSDB_EINVAL;
-        reb[i] = h_off[k0 + i] - h_off[k0];
+        f.reb[i] = h_off[k0 + i] - h_off[k0];
     }
-    HIP_OK(hipMemcpyAsync(c->d_keys, h_blob + h_off[k0], bytes, hipMemcpyHostToDevice, s));
-    HIP_OK(hipMemcpyAsync(c->d_off, reb.data(), (nk + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, s));
+    HIP_OK(hipMemcpyAsync(f.buf[0], h_blob + h_off[k0], bytes, hipMemcpyHostToDevice, c->copy_stream));
+    HIP_OK(hipMemcpyAsync(f.buf[1], f.reb.data(), (nk + 1) * 8, hipMemcpyHostToDevice, c->copy_stream));
     return BSDB_OK;
+}
+
+// Accumulates the histogram of n host keys into d_counts (device, c->stream).
+static int host_histogram_fixed(bsdb_ctx *c, const uint8_t *h_keys, uint32_t key_len, uint64_t n, uint64_t seed,
+                                uint64_t m, uint32_t *d_counts) {
+    const uint64_t batch = fixed_batch(key_len, 256ULL << 20);
+    return feed_batches(
+        c, n, [&](uint64_t k0) { return std::min(n, k0 + batch); },
+        [&](FeedSlot &f, uint64_t k0, uint64_t k1) { return upload_fixed(c, f, h_keys, key_len, k0, k1); },
+        [&](FeedSlot &f, uint64_t k0, uint64_t k1) {
+            return histogram_impl(c, (const uint8_t *)f.buf[0], nullptr, (k1 - k0) * key_len, key_len, k1 - k0, seed, m,
+                                  d_counts, c->stream);
+        });
+}
+
+static int host_histogram_var(bsdb_ctx *c, const uint8_t *h_blob, const uint64_t *h_off, uint64_t n, uint64_t seed,
+                              uint64_t m, uint32_t *d_counts) {
+    return feed_batches(
+        c, n, [&](uint64_t k0) { return var_batch_end(h_off, k0, n); },
+        [&](FeedSlot &f, uint64_t k0, uint64_t k1) { return upload_var(c, f, h_blob, h_off, k0, k1); },
+        [&](FeedSlot &f, uint64_t k0, uint64_t k1) {
+            return histogram_impl(c, (const uint8_t *)f.buf[0], (const uint64_t *)f.buf[1], h_off[k1] - h_off[k0], 0,
+                                  k1 - k0, seed, m, d_counts, c->stream);
+        });
+}
+
+// Signatures of n host keys into d_sig (device, 2n u64).
+static int host_hash_fixed_dev(bsdb_ctx *c, const uint8_t *h_keys, uint32_t key_len, uint64_t n, uint64_t seed,
+                               uint64_t *d_sig) {
+    const uint64_t batch = fixed_batch(key_len, 256ULL << 20);
+    return feed_batches(
+        c, n, [&](uint64_t k0) { return std::min(n, k0 + batch); },
+        [&](FeedSlot &f, uint64_t k0, uint64_t k1) { return upload_fixed(c, f, h_keys, key_len, k0, k1); },
+        [&](FeedSlot &f, uint64_t k0, uint64_t k1) {
+            return hash_impl(c, (const uint8_t *)f.buf[0], nullptr, (k1 - k0) * key_len, key_len, k1 - k0, seed,
+                             d_sig + 2 * k0, c->stream);
+        });
+}
+
+static int host_hash_var_dev(bsdb_ctx *c, const uint8_t *h_blob, const uint64_t *h_off, uint64_t n, uint64_t seed,
+                             uint64_t *d_sig) {
+    return feed_batches(
+        c, n, [&](uint64_t k0) { return var_batch_end(h_off, k0, n); },
+        [&](FeedSlot &f, uint64_t k0, uint64_t k1) { return upload_var(c, f, h_blob, h_off, k0, k1); },
+        [&](FeedSlot &f, uint64_t k0, uint64_t k1) {
+            return hash_impl(c, (const uint8_t *)f.buf[0], (const uint64_t *)f.buf[1], h_off[k1] - h_off[k0], 0,
+                             k1 - k0, seed, d_sig + 2 * k0, c->stream);
+        });
+}
+
+// counts of a host call: the context's d_out, zeroed, then added to h_counts
+static int host_counts_finish(bsdb_ctx *c, uint32_t *d_counts, uint64_t m, uint32_t *h_counts) {
+    std::vector<uint32_t> tmp(m);
+    HIP_OK(hipMemcpyAsync(tmp.data(), d_counts, m * sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
+    HIP_OK(hipStreamSynchronize(c->stream));
+    for (uint64_t b = 0; b < m; ++b) h_counts[b] += tmp[b];
+    return BSDB_OK;
+}
+
+int bsdb_histogram_fixed(bsdb_ctx *c, const uint8_t *h_keys, uint32_t key_len, uint64_t n, uint64_t seed,
+                         uint64_t m, uint32_t *h_counts) {
+    if (!c || bad_key_len(key_len) || m == 0 || m > 0x7FFFFFFFULL || (n && !h_keys) || !h_counts) return BSDB_EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    HIP_OK(hipSetDevice(c->device));
+    Ordered ord(c, c->stream);
+    int rc = grow(&c->d_out, &c->d_out_bytes, m * sizeof(uint32_t));
+    if (rc) return rc;
+    uint32_t *d_counts = (uint32_t *)c->d_out;
+    HIP_OK(hipMemsetAsync(d_counts, 0, m * sizeof(uint32_t), c->stream));
+    if ((rc = host_histogram_fixed(c, h_keys, key_len, n, seed, m, d_counts))) return rc;
+    return host_counts_finish(c, d_counts, m, h_counts);
 }
 
 int bsdb_histogram_var(bsdb_ctx *c, const uint8_t *h_blob, const uint64_t *h_off, uint64_t n, uint64_t seed,
@@ -858,25 +1116,39 @@ int bsdb_histogram_var(bsdb_ctx *c, const uint8_t *h_blob, const uint64_t *h_off
     if (!c || m == 0 || m > 0x7FFFFFFFULL || (n && (!h_blob || !h_off)) || !h_counts) return BSDB_EINVAL;
     std::lock_guard<std::mutex> g(c->mu);
     HIP_OK(hipSetDevice(c->device));
-    hipStream_t s = c->stream;
+    Ordered ord(c, c->stream);
     int rc = grow(&c->d_out, &c->d_out_bytes, m * sizeof(uint32_t));
     if (rc) return rc;
     uint32_t *d_counts = (uint32_t *)c->d_out;
-    HIP_OK(hipMemsetAsync(d_counts, 0, m * sizeof(uint32_t), s));
-    std::vector<uint64_t> reb;
-    for (uint64_t k0 = 0; k0 < n;) {
-        const uint64_t k1 = var_batch_end(h_off, k0, n);
-        if ((rc = var_batch_upload(c, h_blob, h_off, k0, k1, reb, s))) return rc;
-        if ((rc = histogram_impl(c, c->d_keys, c->d_off, h_off[k1] - h_off[k0], 0, k1 - k0, seed, m, d_counts, s)))
-            return rc;
-        HIP_OK(hipStreamSynchronize(s));  // reb is reused by the next batch
-        k0 = k1;
+    HIP_OK(hipMemsetAsync(d_counts, 0, m * sizeof(uint32_t), c->stream));
+    if ((rc = host_histogram_var(c, h_blob, h_off, n, seed, m, d_counts))) return rc;
+    return host_counts_finish(c, d_counts, m, h_counts);
+}
+
+// Signatures to the host: device batches of <= 2^24 keys in d_out.
+template <class Hash>
+static int host_sig_batches(bsdb_ctx *c, uint64_t n, uint64_t *h_sig, Hash &&hash) {
+    constexpr uint64_t B = 1ULL << 24;
+    int rc = grow(&c->d_out, &c->d_out_bytes, (size_t)std::min(n, B) * 16 + 16);
+    if (rc) return rc;
+    for (uint64_t k0 = 0; k0 < n; k0 += B) {
+        const uint64_t nk = std::min(B, n - k0);
+        if ((rc = hash(k0, nk, (uint64_t *)c->d_out))) return rc;
+        HIP_OK(hipMemcpyAsync(h_sig + 2 * k0, c->d_out, nk * 16, hipMemcpyDeviceToHost, c->stream));
+        HIP_OK(hipStreamSynchronize(c->stream));
     }
-    std::vector<uint32_t> tmp(m);
-    HIP_OK(hipMemcpyAsync(tmp.data(), d_counts, m * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-    HIP_OK(hipStreamSynchronize(s));
-    for (uint64_t b = 0; b < m; ++b) h_counts[b] += tmp[b];
     return BSDB_OK;
+}
+
+int bsdb_hash_fixed(bsdb_ctx *c, const uint8_t *h_keys, uint32_t key_len, uint64_t n, uint64_t seed,
+                    uint64_t *h_sig) {
+    if (!c || bad_key_len(key_len) || (n && (!h_keys || !h_sig))) return BSDB_EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    HIP_OK(hipSetDevice(c->device));
+    Ordered ord(c, c->stream);
+    return host_sig_batches(c, n, h_sig, [&](uint64_t k0, uint64_t nk, uint64_t *d) {
+        return host_hash_fixed_dev(c, h_keys + k0 * key_len, key_len, nk, seed, d);
+    });
 }
 
 int bsdb_hash_var(bsdb_ctx *c, const uint8_t *h_blob, const uint64_t *h_off, uint64_t n, uint64_t seed,
@@ -884,20 +1156,12 @@ int bsdb_hash_var(bsdb_ctx *c, const uint8_t *h_blob, const uint64_t *h_off, uin
     if (!c || (n && (!h_blob || !h_off || !h_sig))) return BSDB_EINVAL;
     std::lock_guard<std::mutex> g(c->mu);
     HIP_OK(hipSetDevice(c->device));
-    hipStream_t s = c->stream;
-    int rc = grow(&c->d_out, &c->d_out_bytes, (size_t)std::min(n, VAR_BATCH_KEYS) * 16 + 16);
-    if (rc) return rc;
-    std::vector<uint64_t> reb;
-    for (uint64_t k0 = 0; k0 < n;) {
-        const uint64_t k1 = var_batch_end(h_off, k0, n);
-        if ((rc = var_batch_upload(c, h_blob, h_off, k0, k1, reb, s))) return rc;
-        if ((rc = hash_impl(c, c->d_keys, c->d_off, h_off[k1] - h_off[k0], 0, k1 - k0, seed, (uint64_t *)c->d_out, s)))
-            return rc;
-        HIP_OK(hipMemcpyAsync(h_sig + 2 * k0, c->d_out, (k1 - k0) * 16, hipMemcpyDeviceToHost, s));
-        HIP_OK(hipStreamSynchronize(s));
-        k0 = k1;
-    }
-    return BSDB_OK;
+    Ordered ord(c, c->stream);
+    return host_sig_batches(c, n, h_sig, [&](uint64_t k0, uint64_t nk, uint64_t *d) {
+        return host_hash_var_dev(c, h_blob, h_off + k0, nk, seed, d);
+    });
 }
 
-}  // extern "C"
+
+#include "capi_comm.hip"
+#include "capi_mph.hip"

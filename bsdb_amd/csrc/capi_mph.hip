@@ -1,0 +1,440 @@
+// capi_mph.hip -- host-buffer full build (A5-A11 from host keys), the MPHF
+// object (A14 fields / A15 raw dump), batched lookup (F4) and the index
+// writer of BSDBWriter.buildIndex (A13, F2/F3).  Included by bsdb_capi.hip.
+//   W   = src/main/java/tech/bsdb/write/BSDBWriter.java
+//   GOV = src/main/java/it/unimi/dsi/sux4j/mph/GOVMinimalPerfectHashFunctionModified.java
+
+struct bsdb_mph {
+    bsdb_ctx *c = nullptr;
+    uint64_t n = 0, m = 0;
+    uint32_t width = 0;
+    uint64_t values_words = 0, sig_words = 0;
+    uint64_t *E = nullptr, *values = nullptr, *sigbits = nullptr;  // device
+};
+
+struct bsdb_index {
+    bsdb_mph *mph = nullptr;
+    bool approx = false;
+    uint64_t pass_size = 0, passes = 0, next_pass = 0, cur = UINT64_MAX;
+    FILE *f = nullptr, *fa = nullptr;
+    uint64_t *d_index = nullptr;  // the pass's slots (big-endian addresses)
+    uint8_t *d_index_a = nullptr; // approximate mode: the pass's 8-byte value slots
+};
+
+namespace {
+
+uint64_t mph_sig_words(uint64_t n, uint32_t width) { return width ? (n * width + 63) / 64 + 1 : 0; }
+
+void mph_release(bsdb_mph *p) {
+    if (!p) return;
+    if (p->c) (void)hipSetDevice(p->c->device);
+    (void)hipFree(p->E);
+    (void)hipFree(p->values);
+    (void)hipFree(p->sigbits);
+    delete p;
+}
+
+// A new mph on ctx's device with its arrays allocated (not initialised).
+int mph_alloc(bsdb_ctx *c, uint64_t n, uint32_t width, bsdb_mph **out) {
+    bsdb_mph *p = new (std::nothrow) bsdb_mph();
+    if (!p) return BSDB_ENOMEM;
+    p->c = c;
+    p->n = n;
+    p->m = n / BUCKET_SIZE + 1;
+    p->width = width;
+    p->values_words = bsdb_values_words(n);
+    p->sig_words = mph_sig_words(n, width);
+    if (hipMalloc(&p->E, (p->m + 1) * 8) != hipSuccess || hipMalloc(&p->values, p->values_words * 8) != hipSuccess ||
+        (width && hipMalloc(&p->sigbits, p->sig_words * 8) != hipSuccess)) {
+        mph_release(p);
+        return BSDB_ENOMEM;
+    }
+    *out = p;
+    return BSDB_OK;
+}
+
+// hash (host keys -> device signatures) + GOV build into a new mph
+template <class HashDev>
+int mph_build(bsdb_ctx *c, uint64_t n, uint32_t width, bsdb_mph **out, HashDev &&hash_dev) {
+    if (n / BUCKET_SIZE + 1 > 0x7FFFFFFFULL) return BSDB_EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    HIP_OK(hipSetDevice(c->device));
+    Ordered ord(c, c->stream);
+    bsdb_mph *p = nullptr;
+    int rc = mph_alloc(c, n, width, &p);
+    if (rc) return rc;
+    void *sig = nullptr;
+    if (hipMalloc(&sig, std::max<uint64_t>(n, 1) * 16) != hipSuccess) {
+        mph_release(p);
+        return BSDB_ENOMEM;
+    }
+    std::unique_ptr<void, DevFree> sig_guard(sig);
+    if ((rc = hash_dev((uint64_t *)sig)) ||
+        (rc = gov_build_impl(c, (const uint64_t *)sig, n, n, 0, p->m, 0, width, p->E, p->values, p->sigbits, c->stream,
+                             true))) {
+        (void)hipStreamSynchronize(c->stream);
+        mph_release(p);
+        return rc;
+    }
+    *out = p;
+    return BSDB_OK;
+}
+
+// getLong of host keys: per batch the signatures (slot buffer 6) and the
+// ranks (buffer 7), copied back into h_out on the compute stream.
+template <class Upload>
+int mph_lookup_host(bsdb_mph *p, uint64_t n, int check, int64_t *h_out, Upload &&upload_and_hash) {
+    bsdb_ctx *c = p->c;
+    const MphView v{p->E, p->values, p->sigbits, p->n, (uint32_t)(2 * p->m), p->width};
+    int rc = upload_and_hash.template run<true>(c, n, [&](FeedSlot &f, uint64_t k0, uint64_t k1, const uint64_t *d_sig) {
+        const uint64_t nk = k1 - k0;
+        int r2 = grow(&f.buf[7], &f.cap[7], nk * 8);
+        if (r2) return r2;
+        k_lookup<<<grid_for(c, nk), 256, 0, c->stream>>>(v, d_sig, nk, check, (int64_t *)f.buf[7]);
+        HIP_OK(hipMemcpyAsync(h_out + k0, f.buf[7], nk * 8, hipMemcpyDeviceToHost, c->stream));
+        return launch_status();
+    });
+    if (rc) return rc;
+    HIP_OK(hipStreamSynchronize(c->stream));
+    return BSDB_OK;
+}
+
+// Batched host keys -> device signatures in slot buffer 6, then `then`.
+struct FixedKeys {
+    const uint8_t *keys;
+    uint32_t key_len;
+    template <bool, class Then>
+    int run(bsdb_ctx *c, uint64_t n, Then &&then) const {
+        const uint64_t batch = fixed_batch(key_len, 128ULL << 20);
+        return feed_batches(
+            c, n, [&](uint64_t k0) { return std::min(n, k0 + batch); },
+            [&](FeedSlot &f, uint64_t k0, uint64_t k1) { return upload_fixed(c, f, keys, key_len, k0, k1); },
+            [&](FeedSlot &f, uint64_t k0, uint64_t k1) {
+                const uint64_t nk = k1 - k0;
+                int rc = grow(&f.buf[6], &f.cap[6], nk * 16);
+                if (rc) return rc;
+                if ((rc = hash_impl(c, (const uint8_t *)f.buf[0], nullptr, nk * key_len, key_len, nk, 0,
+                                    (uint64_t *)f.buf[6], c->stream)))
+                    return rc;
+                return then(f, k0, k1, (const uint64_t *)f.buf[6]);
+            });
+    }
+};
+
+struct VarKeys {
+    const uint8_t *blob;
+    const uint64_t *off;
+    template <bool, class Then>
+    int run(bsdb_ctx *c, uint64_t n, Then &&then) const {
+        return feed_batches(
+            c, n, [&](uint64_t k0) { return var_batch_end(off, k0, n); },
+            [&](FeedSlot &f, uint64_t k0, uint64_t k1) { return upload_var(c, f, blob, off, k0, k1); },
+            [&](FeedSlot &f, uint64_t k0, uint64_t k1) {
+                const uint64_t nk = k1 - k0;
+                int rc = grow(&f.buf[6], &f.cap[6], nk * 16);
+                if (rc) return rc;
+                if ((rc = hash_impl(c, (const uint8_t *)f.buf[0], (const uint64_t *)f.buf[1], off[k1] - off[k0], 0, nk, 0,
+                                    (uint64_t *)f.buf[6], c->stream)))
+                    return rc;
+                return then(f, k0, k1, (const uint64_t *)f.buf[6]);
+            });
+    }
+};
+
+// writeLBuffer (W:166-179): the first `bytes` of a device buffer to the file
+// in writes of at most 128 MiB
+int write_chunks(FILE *f, const void *d_src, uint64_t bytes, hipStream_t s) {
+    constexpr uint64_t CHUNK = 128ULL << 20;
+    std::vector<uint8_t> host((size_t)std::min(bytes, CHUNK));
+    for (uint64_t o = 0; o < bytes; o += CHUNK) {
+        const uint64_t k = std::min(CHUNK, bytes - o);
+        HIP_OK(hipMemcpyAsync(host.data(), (const uint8_t *)d_src + o, k, hipMemcpyDeviceToHost, s));
+        HIP_OK(hipStreamSynchronize(s));
+        if (fwrite(host.data(), 1, k, f) != k) return BSDB_EFILE;
+    }
+    return BSDB_OK;
+}
+
+// A13 per record batch: rank (checked getLong, W:135) -> slot of this pass
+template <class Keys>
+int index_put(bsdb_index *ix, const Keys &keys, uint64_t count, const uint64_t *h_addr, const uint64_t *h_value8,
+              const uint8_t *h_vlen) {
+    bsdb_mph *p = ix->mph;
+    bsdb_ctx *c = p->c;
+    if (ix->cur == UINT64_MAX) return BSDB_EINVAL;  // no pass begun
+    const MphView v{p->E, p->values, p->sigbits, p->n, (uint32_t)(2 * p->m), p->width};
+    const uint64_t start = ix->cur * ix->pass_size;
+    const uint64_t len = std::min(ix->pass_size, p->n - start);
+    return keys.template run<true>(c, count, [&](FeedSlot &f, uint64_t k0, uint64_t k1, const uint64_t *d_sig) {
+        const uint64_t nk = k1 - k0;
+        int rc;
+        if ((rc = grow(&f.buf[2], &f.cap[2], nk * 8)) || (rc = grow(&f.buf[7], &f.cap[7], nk * 8))) return rc;
+        // the record payloads go on the compute stream (they are not needed
+        // before the scatter, and it keeps the slot's buffers in one order)
+        HIP_OK(hipMemcpyAsync(f.buf[2], h_addr + k0, nk * 8, hipMemcpyHostToDevice, c->stream));
+        if (ix->approx) {
+            if ((rc = grow(&f.buf[3], &f.cap[3], nk * 8)) || (rc = grow(&f.buf[4], &f.cap[4], nk))) return rc;
+            HIP_OK(hipMemcpyAsync(f.buf[3], h_value8 + k0, nk * 8, hipMemcpyHostToDevice, c->stream));
+            HIP_OK(hipMemcpyAsync(f.buf[4], h_vlen + k0, nk, hipMemcpyHostToDevice, c->stream));
+        }
+        k_lookup<<<grid_for(c, nk), 256, 0, c->stream>>>(v, d_sig, nk, 1, (int64_t *)f.buf[7]);
+        k_index_scatter<<<grid_for(c, nk), 256, 0, c->stream>>>(
+            (const int64_t *)f.buf[7], (const uint64_t *)f.buf[2], nk, start, len, ix->d_index,
+            ix->approx ? (const uint64_t *)f.buf[3] : nullptr, ix->approx ? (const uint8_t *)f.buf[4] : nullptr,
+            ix->approx ? ix->d_index_a : nullptr);
+        return launch_status();
+    });
+}
+
+}  // namespace
+
+extern "C" {
+
+int bsdb_mph_build_fixed(bsdb_ctx *c, const uint8_t *h_keys, uint32_t key_len, uint64_t n, uint32_t width,
+                         bsdb_mph **out) {
+    if (!c || !out || bad_key_len(key_len) || width > 64 || (n && !h_keys)) return BSDB_EINVAL;
+    *out = nullptr;
+    return mph_build(c, n, width, out, [&](uint64_t *d_sig) { return host_hash_fixed_dev(c, h_keys, key_len, n, 0, d_sig); });
+}
+
+int bsdb_mph_build_var(bsdb_ctx *c, const uint8_t *h_blob, const uint64_t *h_off, uint64_t n, uint32_t width,
+                       bsdb_mph **out) {
+    if (!c || !out || width > 64 || (n && (!h_blob || !h_off))) return BSDB_EINVAL;
+    *out = nullptr;
+    return mph_build(c, n, width, out, [&](uint64_t *d_sig) { return host_hash_var_dev(c, h_blob, h_off, n, 0, d_sig); });
+}
+
+int bsdb_mph_info(const bsdb_mph *p, uint64_t *n, uint64_t *m, uint32_t *width, uint64_t *values_words,
+                  uint64_t *sig_words) {
+    if (!p) return BSDB_EINVAL;
+    if (n) *n = p->n;
+    if (m) *m = p->m;
+    if (width) *width = p->width;
+    if (values_words) *values_words = p->values_words;
+    if (sig_words) *sig_words = p->sig_words;
+    return BSDB_OK;
+}
+
+int bsdb_mph_export(bsdb_mph *p, uint64_t *h_E, uint64_t *h_values, uint64_t *h_sigbits) {
+    if (!p || !h_E || !h_values || (p->width && !h_sigbits)) return BSDB_EINVAL;
+    bsdb_ctx *c = p->c;
+    std::lock_guard<std::mutex> g(c->mu);
+    HIP_OK(hipSetDevice(c->device));
+    Ordered ord(c, c->stream);
+    HIP_OK(hipMemcpyAsync(h_E, p->E, (p->m + 1) * 8, hipMemcpyDeviceToHost, c->stream));
+    HIP_OK(hipMemcpyAsync(h_values, p->values, p->values_words * 8, hipMemcpyDeviceToHost, c->stream));
+    if (p->width) HIP_OK(hipMemcpyAsync(h_sigbits, p->sigbits, p->sig_words * 8, hipMemcpyDeviceToHost, c->stream));
+    HIP_OK(hipStreamSynchronize(c->stream));
+    return BSDB_OK;
+}
+
+int bsdb_mph_import(bsdb_ctx *c, uint64_t n, uint32_t width, const uint64_t *h_E, const uint64_t *h_values,
+                    const uint64_t *h_sigbits, bsdb_mph **out) {
+    if (!c || !out || !h_E || !h_values || width > 64 || (width && !h_sigbits) || n / BUCKET_SIZE + 1 > 0x7FFFFFFFULL)
+        return BSDB_EINVAL;
+    *out = nullptr;
+    std::lock_guard<std::mutex> g(c->mu);
+    HIP_OK(hipSetDevice(c->device));
+    Ordered ord(c, c->stream);
+    bsdb_mph *p = nullptr;
+    int rc = mph_alloc(c, n, width, &p);
+    if (rc) return rc;
+    if (hipMemcpyAsync(p->E, h_E, (p->m + 1) * 8, hipMemcpyHostToDevice, c->stream) != hipSuccess ||
+        hipMemcpyAsync(p->values, h_values, p->values_words * 8, hipMemcpyHostToDevice, c->stream) != hipSuccess ||
+        (width && hipMemcpyAsync(p->sigbits, h_sigbits, p->sig_words * 8, hipMemcpyHostToDevice, c->stream) != hipSuccess) ||
+        hipStreamSynchronize(c->stream) != hipSuccess) {
+        mph_release(p);
+        return BSDB_EIO;
+    }
+    *out = p;
+    return BSDB_OK;
+}
+
+// GOV.dump (GOV:592-619), read back by load_mph (mph.c:28-43)
+int bsdb_mph_dump(bsdb_mph *p, const char *path) {
+    if (!p || !path) return BSDB_EINVAL;
+    std::vector<uint64_t> E(p->m + 1), vals(p->values_words);
+    bsdb_ctx *c = p->c;
+    {
+        std::lock_guard<std::mutex> g(c->mu);
+        HIP_OK(hipSetDevice(c->device));
+        Ordered ord(c, c->stream);
+        HIP_OK(hipMemcpyAsync(E.data(), p->E, E.size() * 8, hipMemcpyDeviceToHost, c->stream));
+        HIP_OK(hipMemcpyAsync(vals.data(), p->values, vals.size() * 8, hipMemcpyDeviceToHost, c->stream));
+        HIP_OK(hipStreamSynchronize(c->stream));
+    }
+    FILE *f = fopen(path, "wb");
+    if (!f) return BSDB_EFILE;
+    const uint64_t head[4] = {p->n, 2 * p->m, 0 /* globalSeed, CBHS:209 */, p->m + 1};
+    const uint64_t nv = vals.size();
+    bool ok = fwrite(head, 8, 4, f) == 4 && fwrite(E.data(), 8, E.size(), f) == E.size() && fwrite(&nv, 8, 1, f) == 1 &&
+              fwrite(vals.data(), 8, vals.size(), f) == vals.size();
+    ok = (fclose(f) == 0) && ok;
+    return ok ? BSDB_OK : BSDB_EFILE;
+}
+
+int bsdb_mph_load(bsdb_ctx *c, const char *path, bsdb_mph **out) {
+    if (!c || !path || !out) return BSDB_EINVAL;
+    *out = nullptr;
+    FILE *f = fopen(path, "rb");
+    if (!f) return BSDB_EFILE;
+    uint64_t head[4];
+    std::vector<uint64_t> E, vals;
+    bool ok = fread(head, 8, 4, f) == 4;
+    const uint64_t n = head[0], m = n / BUCKET_SIZE + 1;
+    // the layout is only ours to read if it is a GOV over n keys: multiplier 2m, m+1 offsets
+    ok = ok && head[1] == 2 * m && head[2] == 0 && head[3] == m + 1 && m <= 0x7FFFFFFFULL;
+    if (ok) {
+        E.resize(m + 1);
+        ok = fread(E.data(), 8, E.size(), f) == E.size();
+    }
+    uint64_t nv = 0;
+    ok = ok && fread(&nv, 8, 1, f) == 1 && nv >= bsdb_values_words(n) && nv < (1ULL << 40);
+    if (ok) {
+        vals.resize(nv);
+        ok = fread(vals.data(), 8, nv, f) == nv;
+    }
+    fclose(f);
+    if (!ok) return BSDB_EFILE;
+    return bsdb_mph_import(c, n, 0, E.data(), vals.data(), nullptr, out);
+}
+
+int bsdb_mph_lookup_fixed(bsdb_mph *p, const uint8_t *h_keys, uint32_t key_len, uint64_t n, int check, int64_t *h_out) {
+    if (!p || bad_key_len(key_len) || (n && (!h_keys || !h_out))) return BSDB_EINVAL;
+    bsdb_ctx *c = p->c;
+    std::lock_guard<std::mutex> g(c->mu);
+    HIP_OK(hipSetDevice(c->device));
+    Ordered ord(c, c->stream);
+    return mph_lookup_host(p, n, check, h_out, FixedKeys{h_keys, key_len});
+}
+
+int bsdb_mph_lookup_var(bsdb_mph *p, const uint8_t *h_blob, const uint64_t *h_off, uint64_t n, int check,
+                        int64_t *h_out) {
+    if (!p || (n && (!h_blob || !h_off || !h_out))) return BSDB_EINVAL;
+    bsdb_ctx *c = p->c;
+    std::lock_guard<std::mutex> g(c->mu);
+    HIP_OK(hipSetDevice(c->device));
+    Ordered ord(c, c->stream);
+    return mph_lookup_host(p, n, check, h_out, VarKeys{h_blob, h_off});
+}
+
+int bsdb_mph_free(bsdb_mph *p) {
+    if (!p) return BSDB_EINVAL;
+    {
+        std::lock_guard<std::mutex> g(p->c->mu);
+        (void)hipSetDevice(p->c->device);
+        (void)hipStreamSynchronize(p->c->stream);
+    }
+    mph_release(p);
+    return BSDB_OK;
+}
+
+// ---- A13: the index writer ---------------------------------------------------
+int bsdb_index_open(bsdb_mph *p, int approximate, uint64_t pass_cache_bytes, const char *index_path,
+                    const char *index_a_path, bsdb_index **out, uint64_t *passes) {
+    if (!p || !index_path || !out || (approximate && !index_a_path) || (p->n && pass_cache_bytes < 8)) return BSDB_EINVAL;
+    *out = nullptr;
+    bsdb_index *ix = new (std::nothrow) bsdb_index();
+    if (!ix) return BSDB_ENOMEM;
+    ix->mph = p;
+    ix->approx = approximate != 0;
+    // W:112-118: passSize = min(n, passCacheSize / SLOT_SIZE), passes = ceil(n / passSize)
+    ix->pass_size = std::min(p->n, pass_cache_bytes / 8);
+    ix->passes = ix->pass_size ? (p->n + ix->pass_size - 1) / ix->pass_size : 0;
+    // W:124-127: both files are created (truncated), index_a.db even in exact mode
+    ix->f = fopen(index_path, "wb");
+    if (index_a_path) ix->fa = fopen(index_a_path, "wb");
+    bool ok = ix->f && (!index_a_path || ix->fa);
+    if (ok && ix->pass_size) {
+        std::lock_guard<std::mutex> g(p->c->mu);
+        ok = hipSetDevice(p->c->device) == hipSuccess && hipMalloc(&ix->d_index, ix->pass_size * 8) == hipSuccess &&
+             (!ix->approx || hipMalloc(&ix->d_index_a, ix->pass_size * 8) == hipSuccess);
+        if (!ok) {
+            bsdb_index_close(ix);
+            return BSDB_ENOMEM;
+        }
+    }
+    if (!ok) {
+        bsdb_index_close(ix);
+        return BSDB_EFILE;
+    }
+    if (passes) *passes = ix->passes;
+    *out = ix;
+    return BSDB_OK;
+}
+
+int bsdb_index_begin_pass(bsdb_index *ix, uint64_t pass) {
+    // passes are written to the files in order (W:129-150)
+    if (!ix || pass != ix->next_pass || pass >= ix->passes || ix->cur != UINT64_MAX) return BSDB_EINVAL;
+    bsdb_ctx *c = ix->mph->c;
+    std::lock_guard<std::mutex> g(c->mu);
+    HIP_OK(hipSetDevice(c->device));
+    Ordered ord(c, c->stream);
+    HIP_OK(hipMemsetAsync(ix->d_index, 0, ix->pass_size * 8, c->stream));
+    if (ix->approx) HIP_OK(hipMemsetAsync(ix->d_index_a, 0, ix->pass_size * 8, c->stream));
+    ix->cur = pass;
+    return BSDB_OK;
+}
+
+int bsdb_index_put_var(bsdb_index *ix, const uint8_t *h_blob, const uint64_t *h_off, uint64_t count,
+                       const uint64_t *h_addr, const uint64_t *h_value8, const uint8_t *h_vlen) {
+    if (!ix || (count && (!h_blob || !h_off || !h_addr || (ix->approx && (!h_value8 || !h_vlen))))) return BSDB_EINVAL;
+    bsdb_ctx *c = ix->mph->c;
+    std::lock_guard<std::mutex> g(c->mu);
+    HIP_OK(hipSetDevice(c->device));
+    Ordered ord(c, c->stream);
+    int rc = index_put(ix, VarKeys{h_blob, h_off}, count, h_addr, h_value8, h_vlen);
+    if (rc) return rc;
+    HIP_OK(hipStreamSynchronize(c->stream));  // the caller may reuse its buffers
+    return BSDB_OK;
+}
+
+int bsdb_index_put_fixed(bsdb_index *ix, const uint8_t *h_keys, uint32_t key_len, uint64_t count,
+                         const uint64_t *h_addr, const uint64_t *h_value8, const uint8_t *h_vlen) {
+    if (!ix || bad_key_len(key_len) || (count && (!h_keys || !h_addr || (ix->approx && (!h_value8 || !h_vlen)))))
+        return BSDB_EINVAL;
+    bsdb_ctx *c = ix->mph->c;
+    std::lock_guard<std::mutex> g(c->mu);
+    HIP_OK(hipSetDevice(c->device));
+    Ordered ord(c, c->stream);
+    int rc = index_put(ix, FixedKeys{h_keys, key_len}, count, h_addr, h_value8, h_vlen);
+    if (rc) return rc;
+    HIP_OK(hipStreamSynchronize(c->stream));
+    return BSDB_OK;
+}
+
+int bsdb_index_end_pass(bsdb_index *ix) {
+    if (!ix || ix->cur == UINT64_MAX) return BSDB_EINVAL;
+    bsdb_ctx *c = ix->mph->c;
+    std::lock_guard<std::mutex> g(c->mu);
+    HIP_OK(hipSetDevice(c->device));
+    Ordered ord(c, c->stream);
+    // W:147: the last pass writes only its lastPassSize slots
+    const uint64_t start = ix->cur * ix->pass_size, len = std::min(ix->pass_size, ix->mph->n - start);
+    int rc = write_chunks(ix->f, ix->d_index, len * 8, c->stream);
+    if (!rc && ix->approx) rc = write_chunks(ix->fa, ix->d_index_a, len * 8, c->stream);
+    if (rc) return rc;
+    ix->cur = UINT64_MAX;
+    ++ix->next_pass;
+    return BSDB_OK;
+}
+
+int bsdb_index_close(bsdb_index *ix) {
+    if (!ix) return BSDB_EINVAL;
+    bool ok = true;
+    if (ix->f) ok = fclose(ix->f) == 0 && ok;
+    if (ix->fa) ok = fclose(ix->fa) == 0 && ok;
+    if (ix->d_index || ix->d_index_a) {
+        std::lock_guard<std::mutex> g(ix->mph->c->mu);
+        (void)hipSetDevice(ix->mph->c->device);
+        (void)hipStreamSynchronize(ix->mph->c->stream);
+        (void)hipFree(ix->d_index);
+        (void)hipFree(ix->d_index_a);
+    }
+    // every pass written (W:129-150); a short close leaves short files
+    const bool complete = ix->next_pass == ix->passes;
+    delete ix;
+    return ok ? (complete ? BSDB_OK : BSDB_EINVAL) : BSDB_EFILE;
+}
+
+}  // extern "C"

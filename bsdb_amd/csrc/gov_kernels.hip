@@ -28,34 +28,54 @@
 namespace bsdb {
 
 constexpr int GS_THREADS = 1024;
-constexpr int GS_CMAX = 2048;    // keys per bucket handled (expected ~1500, sigma ~39)
+constexpr int GS_CMAX = 2048;    // keys per bucket solved in LDS (expected ~1500, sigma ~39)
 constexpr int GS_NVMAX = 2304;   // > vertex_offset span of GS_CMAX keys
-constexpr int GS_TINY = 12;
+constexpr int GS_TINY = 12;      // brute-force buckets (only in sets of < ~1500 keys)
 #ifndef GOV_PICK_REPS
 #define GOV_PICK_REPS 8  // FVS: pairs of heavy hinges taken per stuck cascade
-#endif      // brute-force buckets (only in sets of < ~1500 keys)
+#endif
 constexpr int GS_WMAX = (GS_CMAX + 1 + 63) / 64;  // words per bit-sliced row
+// Oversized buckets (adversarial or skewed key sets: > GS_CMAX keys, 14 sigma
+// above the mean for random keys) are solved by the same code with its state
+// in a per-workgroup slab of global memory, up to GB_CMAX keys.
+constexpr int GB_CMAX = 16384;
+constexpr int GB_THREADS = 256;  // sort of an oversized bucket
+// FVS: most heavy hinges of a block (a larger set falls back to Gauss-Jordan
+// over the whole block).  SolveArgs::fvs_max may lower it (tests force the
+// fallback with it); the result is the block's unique solution either way.
+constexpr uint32_t FVS_NH_MAX = 380;
 
-enum GovStatus : uint32_t { GOV_TOO_BIG = 1u, GOV_SEEDS = 2u, GOV_DUP = 4u };
+enum GovStatus : uint32_t { GOV_TOO_BIG = 1u, GOV_SEEDS = 2u, GOV_DUP = 4u, GOV_VERIFY = 8u };
 
 // ---- A5: signatures grouped by bucket, sorted by unsigned (sig0, sig1) -------
-__global__ __launch_bounds__(256) void k_bucket_count(const uint64_t *sig, uint64_t n, uint32_t mult, uint32_t *counts) {
+// A build covers the buckets [b0, b0 + nb) of a GOV structure over all the
+// keys (one GPU: b0 = 0, nb = m; a rank of the multi-GPU build, DESIGN.md
+// §6: its bucket range).  Eb = E + b0 holds GLOBAL offsets (e0 = the keys in
+// buckets below b0); the local signatures occupy positions E[b] - e0.
+__global__ __launch_bounds__(256) void k_bucket_count(const uint64_t *sig, uint64_t n, uint32_t mult, uint32_t b0,
+                                                      uint32_t *counts) {
     const uint64_t stride = (uint64_t)gridDim.x * 256;
     for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride)
-        atomicAdd(counts + bucket_of_w(w64(sig[2 * i]), mult), 1u);
+        atomicAdd(counts + (bucket_of_w(w64(sig[2 * i]), mult) - b0), 1u);
 }
 
-__global__ __launch_bounds__(256) void k_cursor_init(const uint64_t *E, uint64_t m, uint64_t *cursor) {
+// E[b0 + i] = e0 + local exclusive prefix (written by the scan at Eb)
+__global__ __launch_bounds__(256) void k_add_base(uint64_t *Eb, uint64_t cnt, uint64_t e0) {
     const uint64_t stride = (uint64_t)gridDim.x * 256;
-    for (uint64_t b = (uint64_t)blockIdx.x * 256 + threadIdx.x; b < m; b += stride) cursor[b] = E[b] & OFFSET_MASK;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < cnt; i += stride) Eb[i] += e0;
 }
 
-__global__ __launch_bounds__(256) void k_bucket_scatter(const uint64_t *sig, uint64_t n, uint32_t mult,
+__global__ __launch_bounds__(256) void k_cursor_init(const uint64_t *Eb, uint64_t nb, uint64_t e0, uint64_t *cursor) {
+    const uint64_t stride = (uint64_t)gridDim.x * 256;
+    for (uint64_t b = (uint64_t)blockIdx.x * 256 + threadIdx.x; b < nb; b += stride) cursor[b] = (Eb[b] & OFFSET_MASK) - e0;
+}
+
+__global__ __launch_bounds__(256) void k_bucket_scatter(const uint64_t *sig, uint64_t n, uint32_t mult, uint32_t b0,
                                                         unsigned long long *cursor, uint64_t *out) {
     const uint64_t stride = (uint64_t)gridDim.x * 256;
     for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
         const ulonglong2 s = reinterpret_cast<const ulonglong2 *>(sig)[i];
-        const uint64_t pos = atomicAdd(cursor + bucket_of_w(w64(s.x), mult), 1ULL);
+        const uint64_t pos = atomicAdd(cursor + (bucket_of_w(w64(s.x), mult) - b0), 1ULL);
         reinterpret_cast<ulonglong2 *>(out)[pos] = s;
     }
 }
@@ -64,15 +84,13 @@ __device__ __forceinline__ bool sig_less(ulonglong2 a, ulonglong2 b) { return a.
 
 // Bitonic sort of one bucket in LDS (padded with all-ones sentinels) +
 // duplicate check on neighbours (CBHS:969-972).
-__global__ __launch_bounds__(256) void k_bucket_sort(uint64_t *sig, const uint64_t *E, uint64_t m, uint32_t *status) {
+__global__ __launch_bounds__(256) void k_bucket_sort(uint64_t *sig, const uint64_t *Eb, uint64_t nb, uint64_t e0,
+                                                     uint32_t *status) {
     __shared__ ulonglong2 s[GS_CMAX];
-    for (uint64_t b = blockIdx.x; b < m; b += gridDim.x) {
-        const uint64_t lo = E[b] & OFFSET_MASK, hi = E[b + 1] & OFFSET_MASK;
+    for (uint64_t b = blockIdx.x; b < nb; b += gridDim.x) {
+        const uint64_t lo = (Eb[b] & OFFSET_MASK) - e0, hi = (Eb[b + 1] & OFFSET_MASK) - e0;
         const uint32_t cnt = (uint32_t)(hi - lo);
-        if (cnt > GS_CMAX) {
-            if (threadIdx.x == 0) atomicOr(status, (uint32_t)GOV_TOO_BIG);
-            continue;
-        }
+        if (cnt > GS_CMAX) continue;  // k_bucket_sort_big
         uint32_t p2 = 1;
         while (p2 < cnt) p2 <<= 1;
         ulonglong2 *g = reinterpret_cast<ulonglong2 *>(sig) + lo;
@@ -104,15 +122,75 @@ __global__ __launch_bounds__(256) void k_bucket_sort(uint64_t *sig, const uint64
     }
 }
 
+// Oversized buckets (> GS_CMAX keys): list them (status[3] counts them; a
+// bucket over GB_CMAX keys cannot be solved and raises GOV_TOO_BIG).
+__global__ __launch_bounds__(256) void k_big_list(const uint64_t *Eb, uint64_t nb, uint32_t *status, uint32_t *list,
+                                                  uint32_t cap) {
+    const uint64_t stride = (uint64_t)gridDim.x * 256;
+    for (uint64_t b = (uint64_t)blockIdx.x * 256 + threadIdx.x; b < nb; b += stride) {
+        const uint64_t cnt = (Eb[b + 1] & OFFSET_MASK) - (Eb[b] & OFFSET_MASK);
+        if (cnt <= (uint64_t)GS_CMAX) continue;
+        if (cnt > (uint64_t)GB_CMAX) {
+            atomicOr(status, (uint32_t)GOV_TOO_BIG);
+            continue;
+        }
+        const uint32_t i = atomicAdd(status + 3, 1u);
+        if (i < cap) list[i] = (uint32_t)b;
+    }
+}
+
+// The same bitonic sort + duplicate check for the listed oversized buckets, in
+// a per-workgroup global slab of GB_CMAX entries (padded with sentinels).
+__global__ __launch_bounds__(GB_THREADS) void k_bucket_sort_big(uint64_t *sig, const uint64_t *Eb, uint64_t e0,
+                                                                const uint32_t *list, uint32_t nbig, ulonglong2 *slab,
+                                                                uint32_t *status) {
+    ulonglong2 *s = slab + (size_t)blockIdx.x * GB_CMAX;
+    for (uint32_t li = blockIdx.x; li < nbig; li += gridDim.x) {
+        const uint32_t b = list[li];
+        const uint64_t lo = (Eb[b] & OFFSET_MASK) - e0, hi = (Eb[b + 1] & OFFSET_MASK) - e0;
+        const uint32_t cnt = (uint32_t)(hi - lo);
+        uint32_t p2 = 1;
+        while (p2 < cnt) p2 <<= 1;
+        ulonglong2 *g = reinterpret_cast<ulonglong2 *>(sig) + lo;
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < p2; i += GB_THREADS) s[i] = i < cnt ? g[i] : make_ulonglong2(~0ULL, ~0ULL);
+        __syncthreads();
+        for (uint32_t k = 2; k <= p2; k <<= 1) {
+            for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+                for (uint32_t i = threadIdx.x; i < p2; i += GB_THREADS) {
+                    const uint32_t l = i ^ j;
+                    if (l > i) {
+                        const ulonglong2 a = s[i], c = s[l];
+                        const bool up = (i & k) == 0;
+                        if (up ? sig_less(c, a) : sig_less(a, c)) {
+                            s[i] = c;
+                            s[l] = a;
+                        }
+                    }
+                }
+                __syncthreads();
+            }
+        }
+        bool dup = false;
+        for (uint32_t i = threadIdx.x; i < cnt; i += GB_THREADS) {
+            g[i] = s[i];
+            if (i && s[i].x == s[i - 1].x && s[i].y == s[i - 1].y) dup = true;
+        }
+        if (dup) atomicOr(status, (uint32_t)GOV_DUP);
+    }
+}
+
 // ---- A8: per-bucket solve --------------------------------------------------
 struct SolveArgs {
-    const uint64_t *sig;  // sorted signatures
-    uint64_t m;
-    uint64_t *E;          // in: offsets; out: | seed << 56
-    uint64_t *values;     // zeroed 2-bit value array
-    uint64_t *scratch;    // per workgroup: 2 * GS_CMAX * GS_WMAX words
+    const uint64_t *sig;  // sorted signatures of buckets [b0, m), the first at global offset e0
+    uint64_t m;           // end of the bucket range
+    uint64_t *E;          // in: offsets; out: | seed << 56 (global bucket index)
+    uint64_t *values;     // zeroed 2-bit value array (global vertex positions)
+    uint64_t *scratch;    // per workgroup: solve_scratch_words<SolveLds>() words
     uint32_t *status;
     uint64_t *prof;       // optional per-workgroup phase cycle counters [grid][GP_N] (BSDB_GOV_PROFILE)
+    uint32_t fvs_max;     // heavy-set limit, <= FVS_NH_MAX
+    uint64_t b0, e0;      // first bucket of the range, keys before it
 };
 
 // phase counters (cycles, or counts for the GP_N_* slots)
@@ -120,26 +198,41 @@ enum GovProf { GP_EDGES, GP_PEEL, GP_GREEDY, GP_BFS, GP_TARJAN, GP_SINGLE, GP_DE
                GP_N_SEEDS, GP_N_BFS, GP_N_BFS_POPS, GP_N_DENSE_ROWS, GP_N_DENSE_MAX, GP_N_CORE, GP_N_BLOCKS, GP_N_BIG_ROWS,
                GP_N_SCC_SWEEPS, GP_N_SMALL_S, GP_FVS_SEL, GP_FVS_FORMS, GP_FVS_GJ, GP_N };
 
-struct SolveLds {
-    uint16_t e[3 * GS_CMAX];
-    uint32_t deg[GS_NVMAX];
-    uint32_t xe[GS_NVMAX];
-    uint32_t claim[GS_CMAX];
-    int16_t hinge[GS_CMAX];
-    int16_t round_of[GS_CMAX];
-    int16_t vowner[GS_NVMAX];
-    uint8_t xval[GS_NVMAX];
+// Solver state for buckets of up to CMAX_ keys: LDS for GS_CMAX, a global
+// slab per workgroup for GB_CMAX (same code; indices fit int16 either way).
+template <int CMAX_>
+struct SolveLdsT {
+    static constexpr int CMAX = CMAX_;
+    static constexpr int NVMAX = CMAX_ + CMAX_ / 8;  // > vertex_offset span of CMAX keys (281/256)
+    static constexpr int WMAX = (CMAX_ + 1 + 63) / 64;
+    // hsys doubles as the FVS selection's reverse CSR (3*CMAX int16 + CMAX u32)
+    static constexpr int HSYS_WORDS = 2 * 6 * 256 > (10 * CMAX_ + 7) / 8 ? 2 * 6 * 256 : (10 * CMAX_ + 7) / 8;
+    static_assert(CMAX_ < 32767, "int16 edge indices");
+    uint16_t e[3 * CMAX];
+    uint32_t deg[NVMAX];
+    uint32_t xe[NVMAX];
+    uint32_t claim[CMAX];
+    int16_t hinge[CMAX];
+    int16_t round_of[CMAX];
+    int16_t vowner[NVMAX];
+    uint8_t xval[NVMAX];
     // orientation BFS / Tarjan (not live together)
-    int16_t a0[GS_CMAX], a1[GS_CMAX], a2[GS_CMAX], a3[GS_CMAX];
-    uint8_t b0[GS_NVMAX], b1[GS_CMAX];
-    int16_t dep[3 * GS_CMAX];   // Tarjan: owner of edge k's i-th non-hinge vertex, or -1
-    int16_t members[GS_CMAX];   // components, in emission order
-    int16_t comp_end[GS_CMAX];  // end (exclusive) of component c in members
-    int16_t col_of[GS_CMAX];
-    uint64_t prow[2 * GS_WMAX]; // pivot row
-    uint64_t hsys[2 * 6 * 256]; // a heavy-hinge system of <= 255 unknowns, word-major (stride 256)
+    int16_t a0[CMAX], a1[CMAX], a2[CMAX], a3[CMAX];
+    uint8_t b0[NVMAX], b1[CMAX];
+    int16_t dep[3 * CMAX];   // Tarjan: owner of edge k's i-th non-hinge vertex, or -1
+    int16_t members[CMAX];   // components, in emission order
+    int16_t comp_end[CMAX];  // end (exclusive) of component c in members
+    int16_t col_of[CMAX];
+    uint64_t prow[2 * WMAX]; // pivot row
+    uint64_t hsys[HSYS_WORDS]; // a heavy-hinge system of <= 255 unknowns, word-major (stride 256)
     uint32_t ncomp, flag, pivot, rounds, chg, nleft, nscc, qtail;
 };
+using SolveLds = SolveLdsT<GS_CMAX>;
+using SolveBig = SolveLdsT<GB_CMAX>;
+static_assert(SolveLds::NVMAX == GS_NVMAX && SolveLds::WMAX == GS_WMAX, "LDS layout");
+// per-workgroup global scratch of the dense phase (bit-sliced rows, forms)
+template <class Lds>
+constexpr size_t solve_scratch_words() { return (size_t)2 * Lds::CMAX * Lds::WMAX; }
 
 __device__ __forceinline__ void gf3_add(uint64_t &x1, uint64_t &x2, uint64_t y1, uint64_t y2) {
     const uint64_t a1 = x1, a2 = x2;
@@ -162,34 +255,44 @@ struct PhaseClock {
     __device__ void max(int slot, uint64_t v) { if (acc && threadIdx.x == 0 && v > acc[slot]) acc[slot] = v; }
 };
 
-// In-place exclusive scan of a[0..n) (n <= 3 * GS_THREADS) by the whole
-// workgroup; wsum: 16 words of LDS scratch.  Ends with a barrier.
+// In-place exclusive scan of a[0..n) by the whole workgroup, 3 * GS_THREADS
+// entries per round; wsum: 16 words of scratch.  Ends with a barrier.
 __device__ void wg_excl_scan3(uint32_t *a, uint32_t n, uint32_t *wsum) {
-    const uint32_t tid = threadIdx.x, i0 = 3 * tid;
-    const uint32_t c0 = i0 < n ? a[i0] : 0, c1 = i0 + 1 < n ? a[i0 + 1] : 0, c2 = i0 + 2 < n ? a[i0 + 2] : 0;
-    const uint32_t tot = c0 + c1 + c2;
-    uint32_t inc = tot;
+    const uint32_t tid = threadIdx.x;
+    uint32_t carry = 0;
+    for (uint32_t r0 = 0; r0 < n; r0 += 3 * GS_THREADS) {
+        const uint32_t i0 = r0 + 3 * tid;
+        const uint32_t c0 = i0 < n ? a[i0] : 0, c1 = i0 + 1 < n ? a[i0 + 1] : 0, c2 = i0 + 2 < n ? a[i0 + 2] : 0;
+        const uint32_t tot = c0 + c1 + c2;
+        uint32_t inc = tot;
 #pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t o = (uint32_t)__shfl_up((int)inc, d, 64);
-        if ((tid & 63) >= (uint32_t)d) inc += o;
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t o = (uint32_t)__shfl_up((int)inc, d, 64);
+            if ((tid & 63) >= (uint32_t)d) inc += o;
+        }
+        if ((tid & 63) == 63) wsum[tid >> 6] = inc;
+        __syncthreads();
+        uint32_t base = carry, all = carry;
+        for (uint32_t w = 0; w < GS_THREADS / 64; ++w) {
+            const uint32_t s = wsum[w];
+            if (w < (tid >> 6)) base += s;
+            all += s;
+        }
+        const uint32_t ex = base + inc - tot;
+        __syncthreads();
+        if (i0 < n) a[i0] = ex;
+        if (i0 + 1 < n) a[i0 + 1] = ex + c0;
+        if (i0 + 2 < n) a[i0 + 2] = ex + c0 + c1;
+        carry = all;
     }
-    if ((tid & 63) == 63) wsum[tid >> 6] = inc;
-    __syncthreads();
-    uint32_t base = 0;
-    for (uint32_t w = 0; w < (tid >> 6); ++w) base += wsum[w];
-    const uint32_t ex = base + inc - tot;
-    __syncthreads();
-    if (i0 < n) a[i0] = ex;
-    if (i0 + 1 < n) a[i0 + 1] = ex + c0;
-    if (i0 + 2 < n) a[i0 + 2] = ex + c0 + c1;
     __syncthreads();
 }
 
 // Tries local seed j on bucket (sig, cnt, nv).  Returns (WG-uniform) true on
 // success with L.xval / L.vowner describing the solution.
-__device__ bool try_seed(SolveLds &L, const ulonglong2 *sig, uint32_t cnt, uint32_t nv, uint64_t seed_bits,
-                         uint64_t *scr, PhaseClock &pc) {
+template <class Lds>
+__device__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t cnt, uint32_t nv, uint64_t seed_bits,
+                         uint64_t *scr, PhaseClock &pc, uint32_t fvs_max) {
     const int tid = threadIdx.x;
     pc.start();
     pc.add(GP_N_SEEDS, 1);
@@ -638,10 +741,10 @@ __device__ bool try_seed(SolveLds &L, const ulonglong2 *sig, uint32_t cnt, uint3
         for (uint32_t i = tid; i < sz; i += GS_THREADS) L.col_of[L.members[beg + i]] = (int16_t)i;
         __syncthreads();
         // Rows live word-major in the workgroup's scratch: plane q (the two
-        // bit planes of GF(3)) of word w of row rr at scr[(2w + q) * GS_CMAX
+        // bit planes of GF(3)) of word w of row rr at scr[(2w + q) * Lds::CMAX
         // + rr], so a wave's 64 rows read 64 consecutive words (row-major
         // rows 2W words apart cost a 64-byte sector per lane).
-        auto X = [&](uint32_t rr, uint32_t w, uint32_t q) -> uint64_t & { return scr[(size_t)(2 * w + q) * GS_CMAX + rr]; };
+        auto X = [&](uint32_t rr, uint32_t w, uint32_t q) -> uint64_t & { return scr[(size_t)(2 * w + q) * Lds::CMAX + rr]; };
         uint8_t *colval = L.b0;  // (Tarjan's arrays are dead here)
         auto HS = [&](uint32_t rr, uint32_t w, uint32_t q) -> uint64_t & { return L.hsys[(2 * w + q) * 256 + rr]; };
         // Gauss-Jordan on rows 0..n-1 of X (n equations, n unknowns, the
@@ -737,9 +840,10 @@ __device__ bool try_seed(SolveLds &L, const ulonglong2 *sig, uint32_t cnt, uint3
         // and the forms are evaluated.  Block elimination by a triangular
         // part with unit-or-two diagonal: the same unique solution, singular
         // exactly when the block is.
-        constexpr uint32_t FVS_MIN = 96, FVS_NH_MAX = 380, FW = 6;  // <= 6 words per form / heavy row
-        constexpr size_t V0 = (size_t)16 * GS_CMAX;          // affine forms, past that region
-        auto V = [&](uint32_t i, uint32_t w, uint32_t q) -> uint64_t & { return scr[V0 + (size_t)(2 * w + q) * GS_CMAX + i]; };
+        constexpr uint32_t FVS_MIN = 96, FW = 6;  // <= 6 words per form / heavy row
+        static_assert(FVS_NH_MAX + 1 <= 64 * FW, "heavy columns + the constant column must fit FW words");
+        constexpr size_t V0 = (size_t)16 * Lds::CMAX;          // affine forms, past that region
+        auto V = [&](uint32_t i, uint32_t w, uint32_t q) -> uint64_t & { return scr[V0 + (size_t)(2 * w + q) * Lds::CMAX + i]; };
         bool solved = false;
         if (sz >= FVS_MIN) {
             uint32_t *st = L.xe, *indeg = L.claim;  // 0 open, 1 formed, 2 heavy (dead arrays)
@@ -768,8 +872,8 @@ __device__ bool try_seed(SolveLds &L, const ulonglong2 *sig, uint32_t cnt, uint3
             // member's level is 1 + its dependencies' highest (heavy: 0):
             // the forms are evaluated level by level.
             uint32_t *roff = L.deg;                                        // reverse CSR offsets
-            int16_t *rev = reinterpret_cast<int16_t *>(L.hsys);            // 3 * GS_CMAX dependents
-            uint32_t *pend = reinterpret_cast<uint32_t *>(L.hsys) + 3 * GS_CMAX / 2;  // unplaced deps
+            int16_t *rev = reinterpret_cast<int16_t *>(L.hsys);            // 3 * Lds::CMAX dependents
+            uint32_t *pend = reinterpret_cast<uint32_t *>(L.hsys) + 3 * Lds::CMAX / 2;  // unplaced deps
             int16_t *queue = L.a3;
             for (uint32_t i = tid; i <= sz; i += GS_THREADS) roff[i] = 0;
             if (tid == 0) L.qtail = 0;
@@ -786,7 +890,7 @@ __device__ bool try_seed(SolveLds &L, const ulonglong2 *sig, uint32_t cnt, uint3
                 pend[i] = np;
             }
             __syncthreads();
-            wg_excl_scan3(roff, sz + 1, L.xe + GS_CMAX);
+            wg_excl_scan3(roff, sz + 1, L.xe + Lds::CMAX);
             for (uint32_t d = tid; d < sz; d += GS_THREADS) indeg[d] = roff[d];
             __syncthreads();
             for (uint32_t i = tid; i < sz; i += GS_THREADS)
@@ -837,7 +941,10 @@ __device__ bool try_seed(SolveLds &L, const ulonglong2 *sig, uint32_t cnt, uint3
                         qt = L.qtail;
                     }
                     if (qt >= sz) break;  // every member placed (each enters the queue once)
-                    if (nh >= FVS_NH_MAX) {
+                    // a pick adds up to 2 heavy hinges: the heavy set stays
+                    // <= fvs_max, so forms and heavy rows (constant column
+                    // at nH) fit FW words
+                    if (nh + 2 > fvs_max) {
                         fb = true;
                         break;
                     }
@@ -845,7 +952,7 @@ __device__ bool try_seed(SolveLds &L, const ulonglong2 *sig, uint32_t cnt, uint3
                     // best candidates turn heavy at once: any feedback vertex
                     // set gives the same unique solution (and is singular
                     // exactly when the block is); half the stuck cascades.
-                    for (int rep = 0; rep < GOV_PICK_REPS; ++rep) {
+                    for (int rep = 0; rep < GOV_PICK_REPS && nh + 2 <= fvs_max; ++rep) {
                         uint32_t key = 0, key2 = 0;
                         for (uint32_t q0 = 0; q0 * 64 < sz; q0 += 8) {
                             uint32_t sv[8], dv[8];
@@ -971,7 +1078,7 @@ __device__ bool try_seed(SolveLds &L, const ulonglong2 *sig, uint32_t cnt, uint3
                     rinfo[i] = (int16_t)(((h + 3 * 64 - cst) % 3) | (cf == 2 ? 4u : 0u));
                 }
                 __syncthreads();
-                wg_excl_scan3(roff, r + 1, L.xe + GS_CMAX);  // (16 words past st[]; xe holds GS_NVMAX)
+                wg_excl_scan3(roff, r + 1, L.xe + Lds::CMAX);  // (16 words past st[]; xe holds Lds::NVMAX)
                 for (uint32_t R = tid; R < r; R += GS_THREADS) rcur[R] = roff[R];
                 __syncthreads();
                 for (uint32_t i = tid; i < sz; i += GS_THREADS)
@@ -1130,9 +1237,52 @@ __device__ bool try_seed(SolveLds &L, const ulonglong2 *sig, uint32_t cnt, uint3
     return true;
 }
 
+// Solves bucket b with state L (LDS or a global slab) and stores its values
+// and local seed.  Workgroup-uniform.
+template <class Lds>
+__device__ void solve_bucket(Lds &L, const SolveArgs &a, uint64_t b, uint64_t *scr, PhaseClock &pc) {
+    const uint64_t lo = a.E[b] & OFFSET_MASK, hi = a.E[b + 1] & OFFSET_MASK;
+    const uint32_t cnt = (uint32_t)(hi - lo);
+    const uint64_t vo = vertex_offset(lo);
+    const uint32_t nv = (uint32_t)(vertex_offset(hi) - vo);
+    if (cnt == 0) return;
+    if (cnt > (uint32_t)Lds::CMAX || nv > (uint32_t)Lds::NVMAX) {
+        if (threadIdx.x == 0) atomicOr(a.status, (uint32_t)GOV_TOO_BIG);
+        return;
+    }
+    const ulonglong2 *sig = reinterpret_cast<const ulonglong2 *>(a.sig) + (lo - a.e0);
+    uint32_t j = 0;
+    for (; j < 256; ++j)
+        if (try_seed(L, sig, cnt, nv, (uint64_t)j << 56, scr, pc, a.fvs_max)) break;
+    pc.start();
+    if (j == 256) {
+        if (threadIdx.x == 0) atomicOr(a.status, (uint32_t)GOV_SEEDS);
+        return;
+    }
+    // values: hinge -> xval or 3, other vertices 0; words shared with the
+    // neighbouring buckets are OR-ed
+    const uint64_t w0 = vo >> 5, w1 = (vo + nv + 31) >> 5;
+    for (uint64_t w = w0 + threadIdx.x; w < w1; w += GS_THREADS) {
+        uint64_t word = 0;
+        for (uint32_t t = 0; t < 32; ++t) {
+            const uint64_t pos = w * 32 + t;
+            if (pos < vo || pos >= vo + nv) continue;
+            const uint32_t v = (uint32_t)(pos - vo);
+            const uint32_t val = L.vowner[v] >= 0 ? (L.xval[v] ? L.xval[v] : 3u) : 0u;
+            word |= (uint64_t)val << (2 * t);
+        }
+        const bool inner = w * 32 >= vo && (w + 1) * 32 <= vo + nv;
+        if (inner) a.values[w] = word;
+        else if (word) atomicOr((unsigned long long *)(a.values + w), (unsigned long long)word);
+    }
+    if (threadIdx.x == 0) a.E[b] |= (uint64_t)j << 56;
+    __syncthreads();
+    pc.lap(GP_STORE);
+}
+
 __global__ __launch_bounds__(GS_THREADS) void k_gov_solve(SolveArgs a) {
     __shared__ SolveLds L;
-    uint64_t *scr = a.scratch + (size_t)blockIdx.x * 2 * GS_CMAX * GS_WMAX;
+    uint64_t *scr = a.scratch + (size_t)blockIdx.x * solve_scratch_words<SolveLds>();
     PhaseClock pc{a.prof ? a.prof + (size_t)blockIdx.x * GP_N : nullptr, 0};
     // buckets from a queue (status[2], zeroed with the status word): seed
     // retries make per-bucket cost uneven, a static stride left the slowest
@@ -1142,45 +1292,75 @@ __global__ __launch_bounds__(GS_THREADS) void k_gov_solve(SolveArgs a) {
         __syncthreads();
         if (threadIdx.x == 0) next_b = atomicAdd(a.status + 2, 1u);
         __syncthreads();
-        const uint64_t b = next_b;
+        const uint64_t b = a.b0 + next_b;
         if (b >= a.m) break;
-        const uint64_t lo = a.E[b] & OFFSET_MASK, hi = a.E[b + 1] & OFFSET_MASK;
-        const uint32_t cnt = (uint32_t)(hi - lo);
-        const uint64_t vo = vertex_offset(lo);
-        const uint32_t nv = (uint32_t)(vertex_offset(hi) - vo);
-        if (cnt == 0) continue;
-        if (cnt > GS_CMAX || nv > GS_NVMAX) {
-            if (threadIdx.x == 0) atomicOr(a.status, (uint32_t)GOV_TOO_BIG);
+        const uint64_t cnt = (a.E[b + 1] & OFFSET_MASK) - (a.E[b] & OFFSET_MASK);
+        if (cnt > (uint64_t)GS_CMAX) continue;  // k_gov_solve_big
+        solve_bucket(L, a, b, scr, pc);
+    }
+}
+
+// The oversized buckets of k_big_list: one per workgroup at a time, solver
+// state in a global slab (slabs[blockIdx.x]), dense scratch after it.
+__global__ __launch_bounds__(GS_THREADS) void k_gov_solve_big(SolveArgs a, const uint32_t *list, uint32_t nbig,
+                                                              uint8_t *slabs, size_t slab_bytes) {
+    SolveBig &L = *reinterpret_cast<SolveBig *>(slabs + (size_t)blockIdx.x * slab_bytes);
+    uint64_t *scr = reinterpret_cast<uint64_t *>(slabs + (size_t)blockIdx.x * slab_bytes + ((sizeof(SolveBig) + 255) & ~(size_t)255));
+    PhaseClock pc{nullptr, 0};
+    for (uint32_t li = blockIdx.x; li < nbig; li += gridDim.x) solve_bucket(L, a, a.b0 + list[li], scr, pc);
+}
+
+// bytes of one k_gov_solve_big workgroup slab (state + dense scratch)
+constexpr size_t big_slab_bytes() {
+    return ((sizeof(SolveBig) + 255) & ~(size_t)255) + solve_scratch_words<SolveBig>() * 8;
+}
+
+// ---- checks and E4 ownership -------------------------------------------------
+// bsdb_set_verify: every local key's rank lies in [e0, e0 + n) and is hit once
+// (bitmap of n bits, zeroed); with n keys that is a bijection onto the range.
+__global__ __launch_bounds__(256) void k_verify_ranks(MphView v, const uint64_t *sig, uint64_t n, uint64_t e0,
+                                                      unsigned long long *bitmap, uint32_t *status) {
+    const uint64_t stride = (uint64_t)gridDim.x * 256;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
+        const ulonglong2 s = reinterpret_cast<const ulonglong2 *>(sig)[i];
+        const uint64_t r = mph_rank(v, s.x, s.y) - e0;
+        if (r >= n) {
+            atomicOr(status, (uint32_t)GOV_VERIFY);
             continue;
         }
-        const ulonglong2 *sig = reinterpret_cast<const ulonglong2 *>(a.sig) + lo;
-        uint32_t j = 0;
-        for (; j < 256; ++j)
-            if (try_seed(L, sig, cnt, nv, (uint64_t)j << 56, scr, pc)) break;
-        pc.start();
-        if (j == 256) {
-            if (threadIdx.x == 0) atomicOr(a.status, (uint32_t)GOV_SEEDS);
-            continue;
-        }
-        // values: hinge -> xval or 3, other vertices 0; words shared with the
-        // neighbouring buckets are OR-ed
-        const uint64_t w0 = vo >> 5, w1 = (vo + nv + 31) >> 5;
-        for (uint64_t w = w0 + threadIdx.x; w < w1; w += GS_THREADS) {
-            uint64_t word = 0;
-            for (uint32_t t = 0; t < 32; ++t) {
-                const uint64_t pos = w * 32 + t;
-                if (pos < vo || pos >= vo + nv) continue;
-                const uint32_t v = (uint32_t)(pos - vo);
-                const uint32_t val = L.vowner[v] >= 0 ? (L.xval[v] ? L.xval[v] : 3u) : 0u;
-                word |= (uint64_t)val << (2 * t);
-            }
-            const bool inner = w * 32 >= vo && (w + 1) * 32 <= vo + nv;
-            if (inner) a.values[w] = word;
-            else if (word) atomicOr((unsigned long long *)(a.values + w), (unsigned long long)word);
-        }
-        if (threadIdx.x == 0) a.E[b] |= (uint64_t)j << 56;
-        __syncthreads();
-        pc.lap(GP_STORE);
+        const unsigned long long bit = 1ULL << (r & 63);
+        if (atomicOr(bitmap + (r >> 6), bit) & bit) atomicOr(status, (uint32_t)GOV_VERIFY);
+    }
+}
+
+// Rank g of G owns buckets [g*m/G, (g+1)*m/G): the owner of bucket b is
+// floor(((b+1)*G - 1) / m).
+__device__ __forceinline__ uint32_t owner_of(uint32_t b, uint64_t m, uint32_t G) {
+    return (uint32_t)((((uint64_t)b + 1) * G - 1) / m);
+}
+
+constexpr int OWN_MAXR = 64;
+
+__global__ __launch_bounds__(256) void k_owner_count(const uint64_t *sig, uint64_t n, uint32_t mult, uint64_t m,
+                                                     uint32_t G, unsigned long long *counts) {
+    __shared__ uint32_t h[OWN_MAXR];
+    if (threadIdx.x < OWN_MAXR) h[threadIdx.x] = 0;
+    __syncthreads();
+    const uint64_t stride = (uint64_t)gridDim.x * 256;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride)
+        atomicAdd(&h[owner_of(bucket_of_w(w64(sig[2 * i]), mult), m, G)], 1u);
+    __syncthreads();
+    if (threadIdx.x < G && h[threadIdx.x]) atomicAdd(counts + threadIdx.x, (unsigned long long)h[threadIdx.x]);
+}
+
+// cursor[g] starts at rank g's offset in the output
+__global__ __launch_bounds__(256) void k_owner_scatter(const uint64_t *sig, uint64_t n, uint32_t mult, uint64_t m,
+                                                       uint32_t G, unsigned long long *cursor, uint64_t *out) {
+    const uint64_t stride = (uint64_t)gridDim.x * 256;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
+        const ulonglong2 s = reinterpret_cast<const ulonglong2 *>(sig)[i];
+        const uint64_t pos = atomicAdd(cursor + owner_of(bucket_of_w(w64(s.x), mult), m, G), 1ULL);
+        reinterpret_cast<ulonglong2 *>(out)[pos] = s;
     }
 }
 

@@ -19,7 +19,9 @@ LIB_PATH = os.path.join(HERE, "libbsdb_mi355x.so")
 HEADER = os.path.join(os.path.dirname(HERE), "include", "bsdb_mi355x.h")
 
 BSDB_OK = 0
-ERRORS = {-22: "EINVAL", -12: "ENOMEM", -5: "EIO", -19: "ENODEV", -17: "EDUP", -34: "ESEEDS", -7: "E2BIG"}
+ERRORS = {-22: "EINVAL", -12: "ENOMEM", -5: "EIO", -19: "ENODEV", -17: "EDUP", -34: "ESEEDS", -7: "E2BIG",
+          -70: "ECOMM", -9: "EFILE", -74: "EVERIFY"}
+COMM_ID_BYTES = 128
 
 # (name, restype, argtypes) -- kept in the order of include/bsdb_mi355x.h
 _vp, _u64, _u32, _i = C.c_void_p, C.c_uint64, C.c_uint32, C.c_int
@@ -39,6 +41,9 @@ SIGNATURES = [
     ("bsdb_dev_index_scatter", _i, [_vp, _vp, _vp, _u64, _u64, _u64, _vp, _vp, _vp, _vp, _vp]),
     ("bsdb_values_words", _u64, [_u64]),
     ("bsdb_dev_gov_build", _i, [_vp, _vp, _u64, _u32, _vp, _vp, _vp, _vp]),
+    ("bsdb_dev_gov_build_range", _i, [_vp, _vp, _u64, _u64, _u64, _u64, _u64, _u32, _vp, _vp, _vp, _vp]),
+    ("bsdb_dev_partition_owners", _i, [_vp, _vp, _u64, _u64, _i, _vp, _vp, _vp]),
+    ("bsdb_set_verify", _i, [_vp, _i]),
     ("bsdb_set_histogram_mode", _i, [_vp, _i]),
     ("bsdb_set_frontend", _i, [_vp, _i]),
     ("bsdb_set_chunk_keys", _i, [_vp, _u64]),
@@ -51,6 +56,32 @@ SIGNATURES = [
     ("bsdb_hash_var", _i, [_vp, _vp, _vp, _u64, _u64, _vp]),
     ("bsdb_dev_gen_keys13", _i, [_vp, _u64, _u64, _vp, _vp]),
     ("bsdb_dev_gen_keys_var", _i, [_vp, _u64, _u64, _vp, _vp, _u64, _vp]),
+    ("bsdb_comm_unique_id", _i, [_vp]),
+    ("bsdb_comm_init", _i, [_vp, _i, _i, _vp]),
+    ("bsdb_dev_histogram_finalize", _i, [_vp, _vp, _u64, _u64, _vp, _vp]),
+    ("bsdb_dev_allreduce_u64", _i, [_vp, _vp, _u64, _vp]),
+    ("bsdb_multi_open", _i, [_i, _vp, C.POINTER(_vp)]),
+    ("bsdb_multi_close", _i, [_vp]),
+    ("bsdb_multi_size", _i, [_vp]),
+    ("bsdb_multi_ctx", _i, [_vp, _i, C.POINTER(_vp)]),
+    ("bsdb_multi_histogram_fixed", _i, [_vp, _vp, _u32, _u64, _u64, _vp]),
+    ("bsdb_multi_histogram_var", _i, [_vp, _vp, _vp, _u64, _u64, _vp]),
+    ("bsdb_mph_build_fixed", _i, [_vp, _vp, _u32, _u64, _u32, C.POINTER(_vp)]),
+    ("bsdb_mph_build_var", _i, [_vp, _vp, _vp, _u64, _u32, C.POINTER(_vp)]),
+    ("bsdb_mph_info", _i, [_vp, C.POINTER(_u64), C.POINTER(_u64), C.POINTER(_u32), C.POINTER(_u64), C.POINTER(_u64)]),
+    ("bsdb_mph_export", _i, [_vp, _vp, _vp, _vp]),
+    ("bsdb_mph_import", _i, [_vp, _u64, _u32, _vp, _vp, _vp, C.POINTER(_vp)]),
+    ("bsdb_mph_dump", _i, [_vp, C.c_char_p]),
+    ("bsdb_mph_load", _i, [_vp, C.c_char_p, C.POINTER(_vp)]),
+    ("bsdb_mph_lookup_fixed", _i, [_vp, _vp, _u32, _u64, _i, _vp]),
+    ("bsdb_mph_lookup_var", _i, [_vp, _vp, _vp, _u64, _i, _vp]),
+    ("bsdb_mph_free", _i, [_vp]),
+    ("bsdb_index_open", _i, [_vp, _i, _u64, C.c_char_p, C.c_char_p, C.POINTER(_vp), C.POINTER(_u64)]),
+    ("bsdb_index_begin_pass", _i, [_vp, _u64]),
+    ("bsdb_index_put_var", _i, [_vp, _vp, _vp, _u64, _vp, _vp, _vp]),
+    ("bsdb_index_put_fixed", _i, [_vp, _vp, _u32, _u64, _vp, _vp, _vp]),
+    ("bsdb_index_end_pass", _i, [_vp]),
+    ("bsdb_index_close", _i, [_vp]),
 ]
 
 HIST_AUTO, HIST_PARTITIONED, HIST_ATOMIC = 0, 1, 2
@@ -219,6 +250,84 @@ class Context:
             _stream(stream)))
         return E, values, sigbits
 
+    def gov_build_range(self, sig, n_global: int, b_lo: int, b_hi: int, e_lo: int, width: int, E, values, sigbits=None,
+                        stream=None):
+        """E4: one rank's bucket range [b_lo, b_hi) into FULL-size zeroed arrays."""
+        _check("bsdb_dev_gov_build_range", lib().bsdb_dev_gov_build_range(
+            self._h, _ptr(sig), sig.shape[0], n_global, b_lo, b_hi, e_lo, width, _ptr(E), _ptr(values),
+            _ptr(sigbits) if sigbits is not None else None, _stream(stream)))
+
+    def partition_owners(self, sig, m: int, nranks: int, out=None, stream=None):
+        """Signatures grouped by owning rank (bucket ranges); returns (out, counts)."""
+        import torch
+        import numpy as np
+        n = sig.shape[0]
+        if out is None:
+            out = torch.empty((max(n, 1), 2), dtype=torch.int64, device=sig.device)[:n]
+        counts = np.zeros(nranks, np.uint64)
+        _check("bsdb_dev_partition_owners", lib().bsdb_dev_partition_owners(
+            self._h, _ptr(sig), n, m, nranks, _ptr(out), counts.ctypes.data, _stream(stream)))
+        return out, [int(x) for x in counts]
+
+    def set_verify(self, on: bool):
+        _check("bsdb_set_verify", lib().bsdb_set_verify(self._h, 1 if on else 0))
+
+    # ---- B4: the histogram collective (RCCL) inside the library
+    @staticmethod
+    def comm_unique_id() -> bytes:
+        buf = C.create_string_buffer(COMM_ID_BYTES)
+        _check("bsdb_comm_unique_id", lib().bsdb_comm_unique_id(buf))
+        return buf.raw
+
+    def comm_init(self, nranks: int, rank: int, uid: bytes):
+        buf = C.create_string_buffer(bytes(uid), COMM_ID_BYTES)
+        _check("bsdb_comm_init", lib().bsdb_comm_init(self._h, nranks, rank, buf))
+
+    def histogram_finalize(self, counts, n_total: int, out=None, stream=None):
+        """All-reduce of the local counts over RCCL + scan -> E (every rank)."""
+        import torch
+        m = counts.numel()
+        if out is None:
+            out = torch.empty(m + 1, dtype=torch.int64, device=counts.device)
+        _check("bsdb_dev_histogram_finalize", lib().bsdb_dev_histogram_finalize(
+            self._h, _ptr(counts), m, n_total, _ptr(out), _stream(stream)))
+        return out
+
+    def allreduce_u64(self, buf, stream=None):
+        _check("bsdb_dev_allreduce_u64", lib().bsdb_dev_allreduce_u64(self._h, _ptr(buf), buf.numel(), _stream(stream)))
+
+    # ---- A14/A15/F4: a device-resident MPHF built from host keys
+    def mph_build_fixed(self, keys_np, key_len: int, width: int) -> "Mph":
+        import numpy as np
+        keys_np = np.ascontiguousarray(keys_np, np.uint8)
+        h = C.c_void_p()
+        _check("bsdb_mph_build_fixed", lib().bsdb_mph_build_fixed(
+            self._h, keys_np.ctypes.data, key_len, keys_np.size // key_len, width, C.byref(h)))
+        return Mph(h, self)
+
+    def mph_build_var(self, blob_np, off_np, width: int) -> "Mph":
+        blob_np, off_np, n = self._var_host_args(blob_np, off_np)
+        h = C.c_void_p()
+        _check("bsdb_mph_build_var", lib().bsdb_mph_build_var(
+            self._h, blob_np.ctypes.data, off_np.ctypes.data, n, width, C.byref(h)))
+        return Mph(h, self)
+
+    def mph_import(self, n: int, width: int, E, values, sigbits=None) -> "Mph":
+        import numpy as np
+        E = np.ascontiguousarray(E, np.uint64)
+        values = np.ascontiguousarray(values, np.uint64)
+        sb = np.ascontiguousarray(sigbits, np.uint64) if sigbits is not None else None
+        h = C.c_void_p()
+        _check("bsdb_mph_import", lib().bsdb_mph_import(
+            self._h, n, width, E.ctypes.data, values.ctypes.data, sb.ctypes.data if sb is not None else None,
+            C.byref(h)))
+        return Mph(h, self)
+
+    def mph_load(self, path: str) -> "Mph":
+        h = C.c_void_p()
+        _check("bsdb_mph_load", lib().bsdb_mph_load(self._h, path.encode(), C.byref(h)))
+        return Mph(h, self)
+
     # ---- A11-A13: MPHF evaluation over (E, values[, checksum bits])
     def lookup(self, sig, n: int, E, values, width: int = 0, sigbits=None, check: bool = True, out=None,
                stream=None):
@@ -260,9 +369,13 @@ class Context:
         return blob, off
 
     def gen_keys13(self, first: int, n: int, out=None, stream=None):
+        """13*n key bytes (a view of a 16-B-padded allocation when `out` is
+        None, so keys.numel() // 13 == n)."""
         import torch
         if out is None:
-            out = torch.empty(13 * n + 16, dtype=torch.uint8, device=f"cuda:{self.device}")
+            out = torch.empty(13 * n + 16, dtype=torch.uint8, device=f"cuda:{self.device}")[: 13 * n]
+        elif out.numel() < 13 * n:
+            raise ValueError("out holds fewer than 13*n bytes")
         _check("bsdb_dev_gen_keys13", lib().bsdb_dev_gen_keys13(self._h, first, n, _ptr(out), _stream(stream)))
         return out
 
@@ -316,3 +429,173 @@ class Context:
         _check("bsdb_hash_var", lib().bsdb_hash_var(
             self._h, blob_np.ctypes.data, off_np.ctypes.data, n, seed & (2**64 - 1), out.ctypes.data))
         return out[:n]
+
+
+class Mph:
+    """A GOV MPHF resident on one device (``bsdb_mph``)."""
+
+    def __init__(self, h, ctx: Context):
+        self._h = h
+        self.ctx = ctx  # keeps the context alive
+
+    def close(self):
+        if self._h:
+            _check("bsdb_mph_free", lib().bsdb_mph_free(self._h))
+            self._h = C.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def info(self):
+        n, m, vw, sw = C.c_uint64(), C.c_uint64(), C.c_uint64(), C.c_uint64()
+        w = C.c_uint32()
+        _check("bsdb_mph_info", lib().bsdb_mph_info(self._h, C.byref(n), C.byref(m), C.byref(w), C.byref(vw),
+                                                    C.byref(sw)))
+        return {"n": n.value, "num_buckets": m.value, "width": w.value, "values_words": vw.value,
+                "sig_words": sw.value}
+
+    def export(self):
+        """(E u64[m+1], values u64[], sigbits u64[] or None) -- the fields of
+        GOVMinimalPerfectHashFunctionModified (GOV:284-313)."""
+        import numpy as np
+        i = self.info()
+        E = np.zeros(i["num_buckets"] + 1, np.uint64)
+        vals = np.zeros(i["values_words"], np.uint64)
+        sb = np.zeros(i["sig_words"], np.uint64) if i["width"] else None
+        _check("bsdb_mph_export", lib().bsdb_mph_export(self._h, E.ctypes.data, vals.ctypes.data,
+                                                        sb.ctypes.data if sb is not None else None))
+        return E, vals, sb
+
+    def dump(self, path: str):
+        _check("bsdb_mph_dump", lib().bsdb_mph_dump(self._h, path.encode()))
+
+    def lookup_fixed(self, keys_np, key_len: int, check: bool = True):
+        import numpy as np
+        keys_np = np.ascontiguousarray(keys_np, np.uint8)
+        n = keys_np.size // key_len
+        out = np.zeros(max(n, 1), np.int64)
+        _check("bsdb_mph_lookup_fixed", lib().bsdb_mph_lookup_fixed(
+            self._h, keys_np.ctypes.data, key_len, n, 1 if check else 0, out.ctypes.data))
+        return out[:n]
+
+    def lookup_var(self, blob_np, off_np, check: bool = True):
+        import numpy as np
+        blob_np, off_np, n = Context._var_host_args(blob_np, off_np)
+        out = np.zeros(max(n, 1), np.int64)
+        _check("bsdb_mph_lookup_var", lib().bsdb_mph_lookup_var(
+            self._h, blob_np.ctypes.data, off_np.ctypes.data, n, 1 if check else 0, out.ctypes.data))
+        return out[:n]
+
+    def write_index(self, index_path: str, index_a_path: Optional[str], approximate: bool, pass_cache_bytes: int,
+                    feed):
+        """BSDBWriter.buildIndex (W:107-155): for every pass, ``feed(put)``
+        must call ``put(keys..., addr, value8, vlen)`` for every record (the
+        kv.db scan).  Returns the number of passes."""
+        return IndexWriter(self, index_path, index_a_path, approximate, pass_cache_bytes).run(feed)
+
+
+class IndexWriter:
+    """``bsdb_index``: index.db / index_a.db of BSDBWriter.buildIndex."""
+
+    def __init__(self, mph: Mph, index_path: str, index_a_path: Optional[str], approximate: bool,
+                 pass_cache_bytes: int):
+        self.mph = mph
+        self.approx = approximate
+        self._h = C.c_void_p()
+        p = C.c_uint64()
+        _check("bsdb_index_open", lib().bsdb_index_open(
+            mph._h, 1 if approximate else 0, pass_cache_bytes, index_path.encode(),
+            index_a_path.encode() if index_a_path else None, C.byref(self._h), C.byref(p)))
+        self.passes = p.value
+
+    def begin_pass(self, i: int):
+        _check("bsdb_index_begin_pass", lib().bsdb_index_begin_pass(self._h, i))
+
+    def end_pass(self):
+        _check("bsdb_index_end_pass", lib().bsdb_index_end_pass(self._h))
+
+    def put_fixed(self, keys_np, key_len: int, addr_np, value8_np=None, vlen_np=None):
+        import numpy as np
+        keys_np = np.ascontiguousarray(keys_np, np.uint8)
+        addr_np = np.ascontiguousarray(addr_np, np.uint64)
+        v8 = np.ascontiguousarray(value8_np, np.uint64) if value8_np is not None else None
+        vl = np.ascontiguousarray(vlen_np, np.uint8) if vlen_np is not None else None
+        _check("bsdb_index_put_fixed", lib().bsdb_index_put_fixed(
+            self._h, keys_np.ctypes.data, key_len, addr_np.size, addr_np.ctypes.data,
+            v8.ctypes.data if v8 is not None else None, vl.ctypes.data if vl is not None else None))
+
+    def put_var(self, blob_np, off_np, addr_np, value8_np=None, vlen_np=None):
+        import numpy as np
+        blob_np, off_np, n = Context._var_host_args(blob_np, off_np)
+        addr_np = np.ascontiguousarray(addr_np, np.uint64)
+        v8 = np.ascontiguousarray(value8_np, np.uint64) if value8_np is not None else None
+        vl = np.ascontiguousarray(vlen_np, np.uint8) if vlen_np is not None else None
+        _check("bsdb_index_put_var", lib().bsdb_index_put_var(
+            self._h, blob_np.ctypes.data, off_np.ctypes.data, n, addr_np.ctypes.data,
+            v8.ctypes.data if v8 is not None else None, vl.ctypes.data if vl is not None else None))
+
+    def close(self):
+        if self._h:
+            rc = lib().bsdb_index_close(self._h)
+            self._h = C.c_void_p()
+            _check("bsdb_index_close", rc)
+
+    def run(self, feed):
+        try:
+            for i in range(self.passes):
+                self.begin_pass(i)
+                feed(self)
+                self.end_pass()
+        finally:
+            self.close()
+        return self.passes
+
+
+class Multi:
+    """``bsdb_multi``: every listed device of this process + one RCCL communicator."""
+
+    def __init__(self, ndev: int, devices=None):
+        self._h = C.c_void_p()
+        arr = (C.c_int * ndev)(*devices) if devices is not None else None
+        _check("bsdb_multi_open", lib().bsdb_multi_open(ndev, arr, C.byref(self._h)))
+
+    def close(self):
+        if self._h:
+            _check("bsdb_multi_close", lib().bsdb_multi_close(self._h))
+            self._h = C.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def size(self) -> int:
+        return int(lib().bsdb_multi_size(self._h))
+
+    def histogram_fixed(self, keys_np, key_len: int, seed: int = 0):
+        """E[0..m] of host keys sharded over the devices (one all-reduce)."""
+        import numpy as np
+        keys_np = np.ascontiguousarray(keys_np, np.uint8)
+        n = keys_np.size // key_len
+        E = np.zeros(n // 1500 + 2, np.uint64)
+        _check("bsdb_multi_histogram_fixed", lib().bsdb_multi_histogram_fixed(
+            self._h, keys_np.ctypes.data, key_len, n, seed & (2**64 - 1), E.ctypes.data))
+        return E
+
+    def histogram_var(self, blob_np, off_np, seed: int = 0):
+        import numpy as np
+        blob_np, off_np, n = Context._var_host_args(blob_np, off_np)
+        E = np.zeros(n // 1500 + 2, np.uint64)
+        _check("bsdb_multi_histogram_var", lib().bsdb_multi_histogram_var(
+            self._h, blob_np.ctypes.data, off_np.ctypes.data, n, seed & (2**64 - 1), E.ctypes.data))
+        return E

@@ -22,9 +22,19 @@
  *   var    a byte blob of blob_bytes plus offsets[n+1] (u64); key i = blob[off[i] .. off[i+1]).
  *          No read goes past blob_bytes.
  *
- * Thread safety: calls on one context are serialised by the context.  put()
- * is concurrent in the reference (W:75, Builder.java:144-160); callers batch
- * per thread and submit through one context or one context per thread.
+ * Thread safety: calls on one context are serialised by the context's lock,
+ * and the context orders its own work across streams: a call that uses the
+ * context's workspace on a stream other than the previous call's first waits
+ * (hipStreamWaitEvent) for the previous call's work.  put() is concurrent in
+ * the reference (W:75, Builder.java:144-160); callers batch per thread and
+ * submit through one shared context or one context per thread.
+ *
+ * Object handles (all opaque, passed to Java as jlong like native.c:50-59's
+ * mph*, but every one has a matching free/close):
+ *   bsdb_ctx    one HIP device: stream, workspace, host staging, RCCL rank
+ *   bsdb_mph    a GOV MPHF resident on one device (E, 2-bit values, checksum bits)
+ *   bsdb_index  the index.db / index_a.db writer of BSDBWriter.buildIndex
+ *   bsdb_multi  one context per device of this process + an RCCL communicator
  */
 #ifndef BSDB_MI355X_H
 #define BSDB_MI355X_H
@@ -36,16 +46,19 @@
 extern "C" {
 #endif
 
-#define BSDB_ABI_VERSION 1
+#define BSDB_ABI_VERSION 2
 
 /* Return codes (negative errno-style). */
 #define BSDB_OK          0
-#define BSDB_EINVAL    (-22)  /* bad argument (null pointer, key_len 0/255+, n too large) */
+#define BSDB_EINVAL    (-22)  /* bad argument (null pointer, key_len 0 or > 255, n too large) */
 #define BSDB_ENOMEM    (-12)  /* device allocation failed                                  */
 #define BSDB_EIO        (-5)  /* HIP runtime / kernel launch error                         */
 #define BSDB_ENODEV    (-19)  /* no such HIP device                                        */
 #define BSDB_EDUP      (-17)  /* duplicate 128-bit signature (CBHS:969-972, GOV:471-473)   */
 #define BSDB_ESEEDS    (-34)  /* a bucket exhausted its 255 local seeds (GOV:431)          */
+#define BSDB_ECOMM     (-70)  /* RCCL unavailable or a collective failed                   */
+#define BSDB_EFILE     (-9)   /* file open/read/write failed (index / dump files)          */
+#define BSDB_EVERIFY   (-74)  /* a built MPHF failed its on-device bijection check         */
 
 typedef struct bsdb_ctx bsdb_ctx;
 
@@ -131,6 +144,30 @@ uint64_t bsdb_values_words(uint64_t n);
 int bsdb_dev_gov_build(bsdb_ctx *ctx, const uint64_t *d_sig, uint64_t n, uint32_t width, uint64_t *d_E,
                        uint64_t *d_values, uint64_t *d_sigbits, void *stream);
 
+/* E4: the same build restricted to the buckets [b_lo, b_hi) of a GOV structure
+ * over n_global keys (one rank of the multi-GPU build).  d_sig
+ * holds exactly the n_local signatures whose bucket lies in the range (any
+ * order); e_lo = keys in buckets below b_lo.  d_E (num_buckets(n_global)+1),
+ * d_values (bsdb_values_words(n_global)) and d_sigbits ((n_global*width+63)/64
+ * + 1) are FULL-size arrays zeroed by the caller; the call writes E[b_lo..b_hi)
+ * (plus E[m] on the last range), the 2-bit fields of the range's vertices and
+ * the checksum fields of its ranks, and nothing else.  Fields of different
+ * ranges are disjoint bits, so summing the ranks' arrays (one RCCL all-reduce
+ * or reduce, ncclSum) assembles the global structure. */
+int bsdb_dev_gov_build_range(bsdb_ctx *ctx, const uint64_t *d_sig, uint64_t n_local, uint64_t n_global,
+                             uint64_t b_lo, uint64_t b_hi, uint64_t e_lo, uint32_t width, uint64_t *d_E,
+                             uint64_t *d_values, uint64_t *d_sigbits, void *stream);
+/* E4 ownership: rank g of `nranks` owns buckets [g*m/nranks, (g+1)*m/nranks)
+ * (m = num_buckets; the bucket is monotone in sig0, CBHS:129-138).  Groups the n
+ * signatures of d_sig by owning rank into d_out (rank 0's first; order within a
+ * rank unspecified) and writes the per-rank counts to h_counts[nranks]
+ * (synchronises). */
+int bsdb_dev_partition_owners(bsdb_ctx *ctx, const uint64_t *d_sig, uint64_t n, uint64_t num_buckets, int nranks,
+                              uint64_t *d_out, uint64_t *h_counts, void *stream);
+/* Debug/test option: after every GOV build, look every key up again on the
+ * device and check the ranks form a permutation of [0, n) (BSDB_EVERIFY if not). */
+int bsdb_set_verify(bsdb_ctx *ctx, int enable);
+
 /* Histogram path selection for bsdb_dev_histogram_* (benchmarks/tests):
  *   0 = auto (partitioned two-pass), 1 = partitioned two-pass, 2 = direct atomics. */
 int bsdb_set_histogram_mode(bsdb_ctx *ctx, int mode);
@@ -185,6 +222,108 @@ int bsdb_dev_gen_keys13(bsdb_ctx *ctx, uint64_t first, uint64_t n, uint8_t *d_ke
  * offsets[n] <= blob_cap (synchronises).  Bench/test input generator only. */
 int bsdb_dev_gen_keys_var(bsdb_ctx *ctx, uint64_t first, uint64_t n, uint64_t *d_offsets, uint8_t *d_blob,
                           uint64_t blob_cap, void *stream);
+
+/* ---------------------------------------------------------------------------
+ * B4: the one collective of the histogram stage, inside
+ * this library.  RCCL is loaded at first use (dlopen librccl.so.1; BSDB_ECOMM
+ * when absent).  Per-process ranks (one JVM or one torchrun rank per GPU):
+ * rank 0 creates the 128-byte id, the host ships it to the other ranks over
+ * its own channel, every rank calls bsdb_comm_init with it.
+ * bsdb_dev_histogram_finalize then all-reduces the local counts over xGMI --
+ * packed as u16 pairs (m/2 u32 words, 17.6 MB at C4), redone as u32 only if a
+ * count does not fit -- and scans them into E[0..m] (every rank the same E);
+ * it checks E[m] == n_total (synchronises; BSDB_ECOMM on mismatch).  d_counts
+ * holds the global counts afterwards.
+ * ------------------------------------------------------------------------- */
+#define BSDB_COMM_ID_BYTES 128
+int bsdb_comm_unique_id(uint8_t *id /* [BSDB_COMM_ID_BYTES] */);
+int bsdb_comm_init(bsdb_ctx *ctx, int nranks, int rank, const uint8_t *id);
+int bsdb_dev_histogram_finalize(bsdb_ctx *ctx, uint32_t *d_counts, uint64_t num_buckets, uint64_t n_total,
+                                uint64_t *d_E, void *stream);
+/* Sum-all-reduce of u64 words on the context's communicator (assembles the
+ * disjoint fields of bsdb_dev_gov_build_range outputs; BSDB_ECOMM without one). */
+int bsdb_dev_allreduce_u64(bsdb_ctx *ctx, uint64_t *d_buf, uint64_t count, void *stream);
+
+/* ---------------------------------------------------------------------------
+ * B4: all the devices of one process (the reference's build runs in ONE JVM,
+ * SURVEY.md §2.1), one bsdb_ctx per device and an RCCL communicator over them
+ * (ncclCommInitAll).  devices == NULL means 0..ndev-1.  The host-buffer calls
+ * shard the keys in input order over the devices (one host thread per device,
+ * each copying over its own PCIe link), histogram the shards, all-reduce the
+ * counts with ONE collective and return E[0..m] (u64, offsets only) in h_E.
+ * ------------------------------------------------------------------------- */
+typedef struct bsdb_multi bsdb_multi;
+int bsdb_multi_open(int ndev, const int *devices, bsdb_multi **out);
+int bsdb_multi_close(bsdb_multi *mc);
+int bsdb_multi_size(const bsdb_multi *mc);
+int bsdb_multi_ctx(bsdb_multi *mc, int i, bsdb_ctx **out);
+int bsdb_multi_histogram_fixed(bsdb_multi *mc, const uint8_t *h_keys, uint32_t key_len, uint64_t n, uint64_t seed,
+                               uint64_t *h_E);
+int bsdb_multi_histogram_var(bsdb_multi *mc, const uint8_t *h_blob, const uint64_t *h_off, uint64_t n,
+                             uint64_t seed, uint64_t *h_E);
+
+/* ---------------------------------------------------------------------------
+ * A14/A15 + F1/F4 from host buffers: a GOV MPHF built on and resident on one
+ * device (the Java side fills GOVMinimalPerfectHashFunctionModified's fields
+ * from bsdb_mph_export and stores it with BinIO.storeObject, W:99-105;
+ * INTEGRATION.md).  Keys as in bsdb_hash_*; seed 0 (CBHS:209).
+ *   build     hash -> sort -> solve -> sign (width = hash.checksum.bits)
+ *   info      n, num_buckets, width, words of the values / checksum arrays
+ *   export    D2H: E[num_buckets+1] (offset | seed << 56), values words,
+ *             checksum words (h_sigbits may be NULL when width == 0)
+ *   import    H2D of the same arrays (e.g. from a loaded hash.db)
+ *   dump/load the raw layout of GOV.dump (GOV:592-619) read by the
+ *             reference's own load_mph (mph.c:28-43): native-endian u64
+ *             n, multiplier, globalSeed, len(E), E[], len(array), array[];
+ *             no checksum bits (load gives width 0)
+ *   lookup    getLong (GOV:528-532, 557-569) of host keys: rank or -1
+ *             (check != 0: range and checksum test; 0: unchecked rank)
+ * ------------------------------------------------------------------------- */
+typedef struct bsdb_mph bsdb_mph;
+int bsdb_mph_build_fixed(bsdb_ctx *ctx, const uint8_t *h_keys, uint32_t key_len, uint64_t n, uint32_t width,
+                         bsdb_mph **out);
+int bsdb_mph_build_var(bsdb_ctx *ctx, const uint8_t *h_blob, const uint64_t *h_off, uint64_t n, uint32_t width,
+                       bsdb_mph **out);
+int bsdb_mph_info(const bsdb_mph *mph, uint64_t *n, uint64_t *num_buckets, uint32_t *width, uint64_t *values_words,
+                  uint64_t *sig_words);
+int bsdb_mph_export(bsdb_mph *mph, uint64_t *h_E, uint64_t *h_values, uint64_t *h_sigbits);
+int bsdb_mph_import(bsdb_ctx *ctx, uint64_t n, uint32_t width, const uint64_t *h_E, const uint64_t *h_values,
+                    const uint64_t *h_sigbits, bsdb_mph **out);
+int bsdb_mph_dump(bsdb_mph *mph, const char *path);
+int bsdb_mph_load(bsdb_ctx *ctx, const char *path, bsdb_mph **out);
+int bsdb_mph_lookup_fixed(bsdb_mph *mph, const uint8_t *h_keys, uint32_t key_len, uint64_t n, int check,
+                          int64_t *h_out);
+int bsdb_mph_lookup_var(bsdb_mph *mph, const uint8_t *h_blob, const uint64_t *h_off, uint64_t n, int check,
+                        int64_t *h_out);
+int bsdb_mph_free(bsdb_mph *mph);
+
+/* ---------------------------------------------------------------------------
+ * A13 + F2/F3: BSDBWriter.buildIndex (W:107-155, writeLBuffer W:166-179).
+ * open: passSize = min(n, pass_cache_bytes / 8) slots, passes = ceil(n /
+ *   passSize) (W:112-118); creates/truncates index_path and index_a_path
+ *   (the reference creates index_a.db even in exact mode, W:126; with
+ *   index_a_path NULL it is not touched).  For each pass the caller feeds
+ *   every record of the kv.db scan (KVWriter.forEach, W:134) with
+ *   put_{var,fixed}: the key is looked up on the device (getLong, checked),
+ *   and a record whose rank r lies in the pass writes the big-endian address
+ *   (REVERSE_ORDER, Common.java:61) at slot r - rangeStart and, in approximate
+ *   mode, the first min(len, 8) value bytes (value8 little-endian = the byte
+ *   order in the record; a shorter value leaves its slot tail zero -- the
+ *   reference leaves it unspecified, W:141).  end_pass writes the pass's slots
+ *   in writes of <= 128 MiB.  Record buffers: key blob + offsets (or fixed
+ *   keys), addr[count], and for approximate mode value8[count] + vlen[count]
+ *   (min(value length, 8)).  Uploads are double-buffered on two streams.
+ * ------------------------------------------------------------------------- */
+typedef struct bsdb_index bsdb_index;
+int bsdb_index_open(bsdb_mph *mph, int approximate, uint64_t pass_cache_bytes, const char *index_path,
+                    const char *index_a_path, bsdb_index **out, uint64_t *passes);
+int bsdb_index_begin_pass(bsdb_index *ix, uint64_t pass);
+int bsdb_index_put_var(bsdb_index *ix, const uint8_t *h_blob, const uint64_t *h_off, uint64_t count,
+                       const uint64_t *h_addr, const uint64_t *h_value8, const uint8_t *h_vlen);
+int bsdb_index_put_fixed(bsdb_index *ix, const uint8_t *h_keys, uint32_t key_len, uint64_t count,
+                         const uint64_t *h_addr, const uint64_t *h_value8, const uint8_t *h_vlen);
+int bsdb_index_end_pass(bsdb_index *ix);
+int bsdb_index_close(bsdb_index *ix);
 
 #ifdef __cplusplus
 }

@@ -202,6 +202,49 @@ void bo_gen_keys13(uint64_t first, uint64_t n, uint8_t *out) {
     }
 }
 
+/* Config C5 generator (the device's k_gen_var_len / k_gen_var_fill restated):
+ * floor(CDF(r) * 2^64) of Zipf(s = 1.1) over ranks r = 1..57, r = 1..56. */
+static const uint64_t ZIPF_CDF[56] = {
+    0x415ff50621eab000ULL, 0x5fdf8ea4661c1800ULL, 0x7365cc48cd422800ULL, 0x81a02c160ca0d800ULL,
+    0x8cc1c51827e0f000ULL, 0x95dd881c0eabb000ULL, 0x9d8d9c8bd387d800ULL, 0xa430d6d3c06da800ULL,
+    0xaa0593efa19cb800ULL, 0xaf36f652f272a000ULL, 0xb3e4079390b42800ULL, 0xb823d5bdeb558000ULL,
+    0xbc07f52bb16ae800ULL, 0xbf9e197287e21000ULL, 0xc2f123c939aa0800ULL, 0xc609db869ad6f800ULL,
+    0xc8ef6f73a3a9d800ULL, 0xcba7d2952de20000ULL, 0xce38001f766e2000ULL, 0xd0a42e21797a3800ULL,
+    0xd2eff3ea03b6c000ULL, 0xd51e678ba501e800ULL, 0xd73234d900b38000ULL, 0xd92daf816c491000ULL,
+    0xdb12e17da86ff800ULL, 0xdce396a9b5e6c000ULL, 0xdea1662ec6fe5800ULL, 0xe04dba370d317800ULL,
+    0xe1e9d64761753000ULL, 0xe376dc8509ffe800ULL, 0xe4f5d21dcfad2800ULL, 0xe667a2fc93d9d000ULL,
+    0xe7cd24eb876f7000ULL, 0xe9271a3e3b92e800ULL, 0xea76341874c6f000ULL, 0xebbb14628b26f800ULL,
+    0xecf64f78eaa7d000ULL, 0xee286da1bdeba000ULL, 0xef51ec51cc50e000ULL, 0xf0733f47f9ee2000ULL,
+    0xf18cd1858f189800ULL, 0xf29f062863636800ULL, 0xf3aa392b30515800ULL, 0xf4aec00f9fea5000ULL,
+    0xf5acea751b007800ULL, 0xf6a5029ee3f44800ULL, 0xf7974deba8448800ULL, 0xf8840d40614fb000ULL,
+    0xf96b7d68184c6800ULL, 0xfa4dd769e82e0000ULL, 0xfb2b50d667f27000ULL, 0xfc041c0d7f209800ULL,
+    0xfcd8687d83bcc000ULL, 0xfda862dc63a64800ULL, 0xfe74355b824d6000ULL, 0xff3c07d6de49e800ULL};
+
+uint32_t bo_varkey_len(uint64_t i) {
+    const uint64_t u = bo_splitmix64(i ^ 0xB5DB0005ULL);
+    uint32_t r = 0;
+    for (int t = 0; t < 56; t++) r += u >= ZIPF_CDF[t];
+    return 8 + r;
+}
+
+static uint32_t gen_varkey(uint64_t i, uint8_t *d) {
+    const uint32_t len = bo_varkey_len(i);
+    for (int b = 0; b < 8; b++) d[b] = (uint8_t)(i >> (56 - 8 * b));
+    for (uint32_t j = 8; j < len; j += 8) {
+        const uint64_t w = bo_splitmix64(((i << 3) + ((j - 8) >> 3)) ^ 0xB5DB0005A5A5A5A5ULL);
+        for (uint32_t b = 0; b < 8 && j + b < len; b++) d[j + b] = (uint8_t)(w >> (8 * b));
+    }
+    return len;
+}
+
+void bo_gen_keys_var(uint64_t first, uint64_t n, uint64_t *offsets, uint8_t *blob) {
+    offsets[0] = 0;
+    for (uint64_t k = 0; k < n; k++) {
+        const uint32_t len = blob ? gen_varkey(first + k, blob + offsets[k]) : bo_varkey_len(first + k);
+        offsets[k + 1] = offsets[k] + len;
+    }
+}
+
 /* ---- threaded CPU baseline --------------------------------------------- */
 typedef struct { uint64_t first, lo, hi; uint8_t *out; } gen_job;
 static void *mt_gen_only(void *arg) {
@@ -286,6 +329,23 @@ double bo_histogram_gen13_mt(uint64_t first, uint64_t n, uint64_t seed, uint64_t
 double bo_histogram_fixed_mt(const uint8_t *keys, uint32_t key_len, uint64_t n, uint64_t seed,
                              uint64_t m, uint32_t *counts, int threads) {
     return run_mt(mt_fixed, keys, key_len, 0, n, seed, m, counts, threads);
+}
+
+static void *mt_genvar(void *arg) {
+    mt_job *j = (mt_job *)arg;
+    uint8_t k[72];
+    uint64_t t[4];
+    for (uint64_t i = j->lo; i < j->hi; i++) {
+        const uint32_t len = gen_varkey(j->first + i, k);
+        bo_spooky_short(k, len, j->seed, t);
+        j->local[bo_bucket(t[0], j->m)]++;
+    }
+    return NULL;
+}
+
+double bo_histogram_genvar_mt(uint64_t first, uint64_t n, uint64_t seed, uint64_t m, uint32_t *counts,
+                              int threads) {
+    return run_mt(mt_genvar, NULL, 0, first, n, seed, m, counts, threads);
 }
 
 /* ---- A12 lookup ---------------------------------------------------------- */
@@ -703,4 +763,165 @@ int bo_gov_build(const uint64_t *sig_in, uint64_t n, uint32_t sig_width, uint64_
 /* Batch lookup with or without the checksum test. */
 void bo_lookup_batch(const bo_mph *m, const uint64_t *sig, uint64_t n, int check, int64_t *out) {
     for (uint64_t i = 0; i < n; i++) out[i] = check ? bo_lookup(m, sig + 2 * i) : bo_lookup_nocheck(m, sig + 2 * i);
+}
+
+/* ---- threaded forms (CPU full-build baseline; same results) -------------- */
+typedef struct {
+    int kind;  /* 0 hash13, 1 lookups, 2 bucket counts, 3 scatter, 4 solve, 5 sign */
+    const uint8_t *keys; uint32_t key_len; uint64_t seed;
+    const uint64_t *sig; uint64_t lo, hi; uint64_t *out64; int64_t *outi; int check;
+    const bo_mph *mp; uint64_t m; uint32_t *local; uint64_t *cursor; uint64_t *sorted;
+    uint64_t *E; uint64_t *values; int32_t *ws; uint8_t *vals; int rc;
+    uint32_t width; uint64_t *sigs;
+} gv_job;
+
+static void run_jobs(gv_job *jobs, int threads, void *(*fn)(void *)) {
+    pthread_t tid[256];
+    for (int t = 0; t < threads; t++) pthread_create(&tid[t], NULL, fn, &jobs[t]);
+    for (int t = 0; t < threads; t++) pthread_join(tid[t], NULL);
+}
+
+static void *gv_worker(void *arg) {
+    gv_job *j = (gv_job *)arg;
+    uint64_t t4[4];
+    switch (j->kind) {
+    case 0:
+        for (uint64_t i = j->lo; i < j->hi; i++) {
+            bo_spooky_short(j->keys + i * j->key_len, j->key_len, j->seed, t4);
+            j->out64[2 * i] = t4[0];
+            j->out64[2 * i + 1] = t4[1];
+        }
+        break;
+    case 1:
+        for (uint64_t i = j->lo; i < j->hi; i++)
+            j->outi[i] = j->check ? bo_lookup(j->mp, j->sig + 2 * i) : bo_lookup_nocheck(j->mp, j->sig + 2 * i);
+        break;
+    case 2:
+        for (uint64_t i = j->lo; i < j->hi; i++) j->local[bo_bucket(j->sig[2 * i], j->m)]++;
+        break;
+    case 3:
+        for (uint64_t i = j->lo; i < j->hi; i++) {
+            const uint64_t p = j->cursor[bo_bucket(j->sig[2 * i], j->m)]++;
+            j->sorted[2 * p] = j->sig[2 * i];
+            j->sorted[2 * p + 1] = j->sig[2 * i + 1];
+        }
+        break;
+    case 4:  /* buckets [lo, hi): sort, duplicate check, solve (GOV:405-440) */
+        for (uint64_t b = j->lo; b < j->hi && !j->rc; b++) {
+            const uint64_t lo = j->E[b] & (~0ULL >> 8), hi = j->E[b + 1] & (~0ULL >> 8);
+            qsort(j->sorted + 2 * lo, hi - lo, 16, cmp_sig);
+            for (uint64_t i = lo + 1; i < hi; i++)
+                if (j->sorted[2 * i] == j->sorted[2 * i - 2] && j->sorted[2 * i + 1] == j->sorted[2 * i - 1]) j->rc = -1;
+            if (j->rc) break;
+            const uint64_t vo = bo_vertex_offset(lo);
+            const uint32_t nv = (uint32_t)(bo_vertex_offset(hi) - vo);
+            uint64_t s = 0;
+            for (; s < 256; s++)
+                if (!solve_bucket(j->sorted + 2 * lo, (uint32_t)(hi - lo), nv, s << 56, j->vals, j->ws)) break;
+            if (s == 256) { j->rc = -2; break; }
+            j->E[b] |= s << 56;  /* (E[b+1]'s offset bits are all another range reads) */
+            for (uint32_t v = 0; v < nv; v++)
+                if (j->vals[v]) __atomic_fetch_or(&j->values[(vo + v) >> 5], (uint64_t)j->vals[v] << (2 * ((vo + v) & 31)), __ATOMIC_RELAXED);
+        }
+        break;
+    case 5: {
+        const uint64_t mask = j->width == 64 ? ~0ULL : (1ULL << j->width) - 1;
+        for (uint64_t i = j->lo; i < j->hi; i++) {
+            const uint64_t r = (uint64_t)bo_lookup_nocheck(j->mp, j->sorted + 2 * i);
+            const uint64_t v = j->sorted[2 * i] & mask, bit = r * j->width, w = bit >> 6;
+            const unsigned off = (unsigned)(bit & 63);
+            if (v) {
+                __atomic_fetch_or(&j->sigs[w], v << off, __ATOMIC_RELAXED);
+                if (off + j->width > 64) __atomic_fetch_or(&j->sigs[w + 1], v >> (64 - off), __ATOMIC_RELAXED);
+            }
+        }
+        break;
+    }
+    }
+    return NULL;
+}
+
+static int clamp_threads(int threads) { return threads < 1 ? 1 : threads > 256 ? 256 : threads; }
+
+void bo_hash_fixed_mt(const uint8_t *keys, uint32_t key_len, uint64_t n, uint64_t seed, uint64_t *sig, int threads) {
+    threads = clamp_threads(threads);
+    gv_job jobs[256];
+    for (int t = 0; t < threads; t++)
+        jobs[t] = (gv_job){.kind = 0, .keys = keys, .key_len = key_len, .seed = seed, .lo = n * t / threads,
+                           .hi = n * (t + 1) / threads, .out64 = sig};
+    run_jobs(jobs, threads, gv_worker);
+}
+
+void bo_lookup_batch_mt(const bo_mph *mp, const uint64_t *sig, uint64_t n, int check, int64_t *out, int threads) {
+    threads = clamp_threads(threads);
+    gv_job jobs[256];
+    for (int t = 0; t < threads; t++)
+        jobs[t] = (gv_job){.kind = 1, .sig = sig, .lo = n * t / threads, .hi = n * (t + 1) / threads, .outi = out,
+                           .check = check, .mp = mp};
+    run_jobs(jobs, threads, gv_worker);
+}
+
+int bo_gov_build_mt(const uint64_t *sig, uint64_t n, uint32_t sig_width, uint64_t *E, uint64_t *values,
+                    uint64_t values_words, uint64_t *signatures, uint64_t sig_words, int threads, double *seconds) {
+    threads = clamp_threads(threads);
+    const double t0 = now_s();
+    const uint64_t m = bo_num_buckets(n);
+    gv_job jobs[256];
+    uint64_t *sorted = (uint64_t *)malloc((n ? n : 1) * 16);
+    uint32_t *local = (uint32_t *)calloc((size_t)threads * m, 4);
+    uint64_t *cursor = (uint64_t *)malloc((size_t)threads * m * 8);
+    /* A6 histogram, per thread slice */
+    for (int t = 0; t < threads; t++)
+        jobs[t] = (gv_job){.kind = 2, .sig = sig, .lo = n * t / threads, .hi = n * (t + 1) / threads, .m = m,
+                           .local = local + (size_t)t * m};
+    run_jobs(jobs, threads, gv_worker);
+    memset(E, 0, (m + 1) * 8);
+    for (uint64_t b = 0; b < m; b++) {
+        uint64_t acc = E[b];
+        for (int t = 0; t < threads; t++) {
+            cursor[(size_t)t * m + b] = acc;
+            acc += local[(size_t)t * m + b];
+        }
+        E[b + 1] = acc;
+    }
+    /* bucket order (stable per thread slice; each bucket is sorted next) */
+    for (int t = 0; t < threads; t++)
+        jobs[t] = (gv_job){.kind = 3, .sig = sig, .lo = n * t / threads, .hi = n * (t + 1) / threads, .m = m,
+                           .cursor = cursor + (size_t)t * m, .sorted = sorted};
+    run_jobs(jobs, threads, gv_worker);
+    free(local);
+    free(cursor);
+    memset(values, 0, values_words * 8);
+    uint32_t maxc = 0;
+    for (uint64_t b = 0; b < m; b++) if (E[b + 1] - E[b] > maxc) maxc = (uint32_t)(E[b + 1] - E[b]);
+    const uint32_t maxnv = (uint32_t)(bo_vertex_offset(maxc) + 4);
+    /* bucket ranges of ~n/threads keys each */
+    uint64_t b0 = 0;
+    for (int t = 0; t < threads; t++) {
+        uint64_t b1 = b0;
+        const uint64_t target = n * (t + 1) / threads;
+        while (b1 < m && (t == threads - 1 || E[b1] < target)) b1++;
+        jobs[t] = (gv_job){.kind = 4, .lo = b0, .hi = b1, .E = E, .values = values, .sorted = sorted,
+                           .ws = (int32_t *)malloc(solve_ws_words(maxc + 1, maxnv + 1) * 4 + 64),
+                           .vals = (uint8_t *)malloc(maxnv + 1)};
+        b0 = b1;
+    }
+    run_jobs(jobs, threads, gv_worker);
+    int rc = 0;
+    for (int t = 0; t < threads; t++) {
+        if (jobs[t].rc == -1 || (jobs[t].rc && !rc)) rc = jobs[t].rc;
+        free(jobs[t].ws);
+        free(jobs[t].vals);
+    }
+    if (!rc && sig_width) {
+        memset(signatures, 0, sig_words * 8);
+        bo_mph mp = {n, 2 * m, 0, m, E, values, 0, NULL};
+        for (int t = 0; t < threads; t++)
+            jobs[t] = (gv_job){.kind = 5, .lo = n * t / threads, .hi = n * (t + 1) / threads, .mp = &mp,
+                               .sorted = sorted, .width = sig_width, .sigs = signatures};
+        run_jobs(jobs, threads, gv_worker);
+    }
+    free(sorted);
+    if (seconds) *seconds = now_s() - t0;
+    return rc;
 }

@@ -54,6 +54,15 @@ void bo_gen_keys13_mt(uint64_t first, uint64_t n, uint8_t *out, int threads);
  * the CPU baseline leg.  Returns elapsed seconds. */
 double bo_histogram_gen13_mt(uint64_t first, uint64_t n, uint64_t seed, uint64_t num_buckets,
                              uint32_t *counts, int threads);
+/* Config C5 keys: key i has length 8 + r, r drawn
+ * Zipf(1.1) over 8..64 by inverse CDF on splitmix64(i ^ 0xB5DB0005); bytes
+ * 0-7 = i big-endian (BaseTest.java:16-24); tail word w = splitmix64(((i<<3)
+ * + w) ^ 0xB5DB0005A5A5A5A5) little-endian.  len() gives the length; gen
+ * writes offsets[n+1] (from 0) and, with blob != NULL, the key bytes. */
+uint32_t bo_varkey_len(uint64_t i);
+void bo_gen_keys_var(uint64_t first, uint64_t n, uint64_t *offsets, uint8_t *blob);
+double bo_histogram_genvar_mt(uint64_t first, uint64_t n, uint64_t seed, uint64_t num_buckets, uint32_t *counts,
+                              int threads);
 /* Multi-threaded histogram over a resident fixed-length key blob. */
 double bo_histogram_fixed_mt(const uint8_t *keys, uint32_t key_len, uint64_t n, uint64_t seed,
                              uint64_t num_buckets, uint32_t *counts, int threads);
@@ -88,6 +97,15 @@ int bo_gov_build(const uint64_t *sig /* 2n, any order */, uint64_t n, uint32_t s
                  uint64_t *E, uint64_t *values, uint64_t values_words,
                  uint64_t *signatures, uint64_t sig_words);
 uint64_t bo_values_words(uint64_t n);    /* words of the 2-bit value array */
+/* The same build, threads over bucket ranges (identical output: every bucket
+ * is solved exactly as by bo_gov_build).  Also the CPU full-build baseline
+ * ("port") of bench.py.  Returns as bo_gov_build; *seconds = elapsed. */
+int bo_gov_build_mt(const uint64_t *sig, uint64_t n, uint32_t sig_width, uint64_t *E, uint64_t *values,
+                    uint64_t values_words, uint64_t *signatures, uint64_t sig_words, int threads, double *seconds);
+/* Threaded lookups (bench / large tests). */
+void bo_lookup_batch_mt(const bo_mph *m, const uint64_t *sig, uint64_t n, int check, int64_t *out, int threads);
+/* Threaded signatures of 13-byte keys (full-build baseline input). */
+void bo_hash_fixed_mt(const uint8_t *keys, uint32_t key_len, uint64_t n, uint64_t seed, uint64_t *sig, int threads);
 void bo_lookup_batch(const bo_mph *m, const uint64_t *sig, uint64_t n, int check, int64_t *out);
 
 #ifdef __cplusplus

@@ -69,6 +69,15 @@ def lib() -> C.CDLL:
             L.bo_gov_build.restype = C.c_int
         if hasattr(L, "bo_lookup_batch"):
             L.bo_lookup_batch.argtypes = [C.POINTER(BoMph), _u64p, C.c_uint64, C.c_int, C.POINTER(C.c_int64)]
+        L.bo_gov_build_mt.argtypes = [_u64p, C.c_uint64, C.c_uint32, _u64p, _u64p, C.c_uint64, _u64p, C.c_uint64,
+                                      C.c_int, C.POINTER(C.c_double)]
+        L.bo_gov_build_mt.restype = C.c_int
+        L.bo_lookup_batch_mt.argtypes = [C.POINTER(BoMph), _u64p, C.c_uint64, C.c_int, C.POINTER(C.c_int64), C.c_int]
+        L.bo_hash_fixed_mt.argtypes = [_u8p, C.c_uint32, C.c_uint64, C.c_uint64, _u64p, C.c_int]
+        L.bo_varkey_len.argtypes = [C.c_uint64]; L.bo_varkey_len.restype = C.c_uint32
+        L.bo_gen_keys_var.argtypes = [C.c_uint64, C.c_uint64, _u64p, _u8p]
+        L.bo_histogram_genvar_mt.argtypes = [C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64, _u32p, C.c_int]
+        L.bo_histogram_genvar_mt.restype = C.c_double
         _lib = L
     return _lib
 
@@ -232,3 +241,93 @@ def lookup_batch(sig: np.ndarray, n: int, E: np.ndarray, values: np.ndarray, wid
     lib().bo_lookup_batch(C.byref(mp), _p(sig, _u64p), sig.shape[0], 1 if check else 0,
                           out.ctypes.data_as(C.POINTER(C.c_int64)))
     return out[: sig.shape[0]]
+
+
+# ------------------------------------------------- threaded forms, C5 keys
+def cpu_threads() -> int:
+    """CPUs this process may actually use: the affinity mask, capped by a
+    cgroup CPU quota when one is set (the GPU box's os.cpu_count() shows the
+    whole machine, its quota is lower)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(int(quota) // int(period))))
+    except (OSError, ValueError):
+        pass
+    return max(1, n)
+
+
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def gov_build_mt(sig: np.ndarray, width: int, threads: int):
+    """bo_gov_build over bucket ranges on `threads` threads: (rc, E, values,
+    sigbits, seconds), identical to gov_build."""
+    sig = np.ascontiguousarray(sig, np.uint64).reshape(-1, 2)
+    n = sig.shape[0]
+    m = num_buckets(n)
+    E = np.zeros(m + 1, np.uint64)
+    vw = int(lib().bo_values_words(n))
+    values = np.zeros(vw, np.uint64)
+    sw = (n * width + 63) // 64 + 1
+    sigbits = np.zeros(sw, np.uint64)
+    dt = C.c_double()
+    rc = lib().bo_gov_build_mt(_p(sig, _u64p), n, width, _p(E, _u64p), _p(values, _u64p), vw, _p(sigbits, _u64p), sw,
+                               threads, C.byref(dt))
+    return rc, E, values, sigbits, dt.value
+
+
+def lookup_batch_mt(sig: np.ndarray, n: int, E: np.ndarray, values: np.ndarray, width: int = 0, sigbits=None,
+                    check: bool = True, threads: int = 1) -> np.ndarray:
+    sig = np.ascontiguousarray(sig, np.uint64).reshape(-1, 2)
+    m = E.size - 1
+    sb = sigbits if sigbits is not None else np.zeros(1, np.uint64)
+    mp = BoMph(n, 2 * m, 0, m, _p(E, _u64p), _p(values, _u64p), width, _p(sb, _u64p))
+    out = np.zeros(max(sig.shape[0], 1), np.int64)
+    lib().bo_lookup_batch_mt(C.byref(mp), _p(sig, _u64p), sig.shape[0], 1 if check else 0,
+                             out.ctypes.data_as(C.POINTER(C.c_int64)), threads)
+    return out[: sig.shape[0]]
+
+
+def hash_fixed_mt(keys: np.ndarray, key_len: int, threads: int, seed: int = 0) -> np.ndarray:
+    keys = np.ascontiguousarray(keys, np.uint8).reshape(-1)
+    n = keys.size // key_len
+    sig = np.zeros(2 * max(n, 1), np.uint64)
+    lib().bo_hash_fixed_mt(_p(keys, _u8p), key_len, n, seed, _p(sig, _u64p), threads)
+    return sig[: 2 * n].reshape(n, 2)
+
+
+def gen_keys_var(first: int, n: int):
+    """Config C5 keys [first, first+n): (blob u8, offsets u64[n+1])."""
+    off = np.zeros(n + 1, np.uint64)
+    lib().bo_gen_keys_var(first, n, _p(off, _u64p), None)
+    blob = np.zeros(max(int(off[-1]), 1), np.uint8)
+    lib().bo_gen_keys_var(first, n, _p(off, _u64p), _p(blob, _u8p))
+    return blob[: int(off[-1])], off
+
+
+def varkey_len(i: int) -> int:
+    return int(lib().bo_varkey_len(i))
+
+
+def histogram_genvar_mt(first: int, n: int, m: int, threads: int, seed: int = 0):
+    counts = np.zeros(m, np.uint32)
+    dt = lib().bo_histogram_genvar_mt(first, n, seed, m, _p(counts, _u32p), threads)
+    return counts, dt
+
+
+def splitmix64_np(x: np.ndarray) -> np.ndarray:
+    """bo_splitmix64 over a u64 array (wrapping arithmetic)."""
+    with np.errstate(over="ignore"):
+        z = np.asarray(x, np.uint64) + np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        return z ^ (z >> np.uint64(31))

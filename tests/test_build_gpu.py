@@ -1,0 +1,328 @@
+"""GPU: the host-buffer full build, the MPHF object, the index writer, the
+oversized-bucket and FVS-limit solver paths, the range build of the
+multi-GPU design (E4) and the RCCL collective inside the C ABI (B4) -- all
+through include/bsdb_mi355x.h, against the CPU oracle (and, for the raw
+dump, the reference's own load_mph / mph_get_byte_array)."""
+import os
+
+import numpy as np
+import pytest
+
+import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+THREADS = O.cpu_threads()
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from bsdb_amd import Context
+    c = Context(0)
+    yield c
+    c.close()
+
+
+def dev(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+def u64(t):
+    return t.cpu().numpy().view(np.uint64)
+
+
+def oracle_build(keys, L, width):
+    sig = O.hash_fixed_mt(keys, L, THREADS)
+    rc, E, vals, sb, _ = O.gov_build_mt(sig, width, THREADS)
+    assert rc == 0
+    return sig, E, vals, sb
+
+
+def test_mph_build_fixed_matches_oracle(ctx):
+    """C1 shape: 1e6 13-byte keys, hash.checksum.bits = 4, from host memory."""
+    n, width = 1_000_000, 4
+    keys = O.gen_keys13(0, n)
+    sig, E, vals, sb = oracle_build(keys, 13, width)
+    with ctx.mph_build_fixed(keys, 13, width) as mph:
+        info = mph.info()
+        assert info["n"] == n and info["num_buckets"] == n // 1500 + 1 and info["width"] == width
+        dE, dv, ds = mph.export()
+        np.testing.assert_array_equal(dE, E)
+        np.testing.assert_array_equal(dv, vals)
+        np.testing.assert_array_equal(ds[: sb.size], sb)
+        # getLong of every key (checked) is a bijection, equal to the oracle's
+        r = mph.lookup_fixed(keys, 13)
+        assert np.array_equal(np.sort(r), np.arange(n))
+        np.testing.assert_array_equal(r, O.lookup_batch_mt(sig, n, E, vals, width, sb, True, THREADS))
+
+
+def test_mph_build_var_and_absent_keys(ctx):
+    blob, off = O.gen_keys_var(0, 300_000)
+    sig = O.hash_var(blob, off)
+    rc, E, vals, sb, _ = O.gov_build_mt(sig, 16, THREADS)
+    assert rc == 0
+    with ctx.mph_build_var(blob, off, 16) as mph:
+        dE, dv, ds = mph.export()
+        np.testing.assert_array_equal(dE, E)
+        np.testing.assert_array_equal(dv, vals)
+        np.testing.assert_array_equal(ds[: sb.size], sb)
+        # keys outside the set: checked lookups agree with the oracle's (-1 or a false positive)
+        ablob, aoff = O.gen_keys_var(10_000_000, 50_000)
+        got = mph.lookup_var(ablob, aoff, check=True)
+        exp = O.lookup_batch(O.hash_var(ablob, aoff), sig.shape[0], E, vals, 16, sb, True)
+        np.testing.assert_array_equal(got, exp)
+        assert (got == -1).mean() > 0.99  # 2^-16 false positives
+
+
+def test_dump_is_read_by_reference_load_mph(ctx, tmp_path):
+    """A15: bsdb_mph_dump writes GOV.dump's layout (GOV:592-619); the
+    reference's own load_mph + mph_get_byte_array (mph.c:28-43, 86-96) read it
+    back and return the device's unchecked ranks."""
+    R = O.ref_lib()
+    if R is None:
+        pytest.skip("oracle/_ref not built")
+    keys = [str(i).encode() for i in range(200_000)]  # NativeTest-style ASCII keys
+    off = np.zeros(len(keys) + 1, np.uint64)
+    off[1:] = np.cumsum([len(k) for k in keys])
+    blob = np.frombuffer(b"".join(keys), np.uint8)
+    path = str(tmp_path / "hash.dump")
+    with ctx.mph_build_var(blob, off, 12) as mph:
+        mph.dump(path)
+        ranks = mph.lookup_var(blob, off, check=False)
+        with ctx.mph_load(path) as back:
+            assert back.info()["width"] == 0
+            np.testing.assert_array_equal(back.lookup_var(blob, off, check=False), ranks)
+            e1, v1, _ = back.export()
+            e0, v0, _ = mph.export()
+            np.testing.assert_array_equal(e1, e0)
+            np.testing.assert_array_equal(v1, v0)
+    fd = os.open(path, os.O_RDONLY)
+    try:
+        rm = R.load_mph(fd)
+    finally:
+        os.close(fd)
+    got = np.array([R.mph_get_byte_array(rm, k, len(k)) for k in keys[:20_000]], np.int64)
+    np.testing.assert_array_equal(got, ranks[:20_000])
+    assert np.array_equal(np.sort(ranks), np.arange(len(keys)))
+
+
+def test_import_roundtrip(ctx):
+    keys = O.gen_keys13(7, 100_000)
+    sig, E, vals, sb = oracle_build(keys, 13, 8)
+    with ctx.mph_import(100_000, 8, E, vals, sb) as mph:
+        np.testing.assert_array_equal(mph.lookup_fixed(keys, 13), O.lookup_batch(sig, 100_000, E, vals, 8, sb))
+        e, v, s = mph.export()
+        assert np.array_equal(e, E) and np.array_equal(v, vals) and np.array_equal(s, sb)
+
+
+def records(first, n):
+    """Synthetic kv.db scan: addr, the first 8 value bytes, min(value len, 8)."""
+    i = np.arange(first, first + n, dtype=np.uint64)
+    addr = np.uint64(0x1000) + np.uint64(48) * i
+    value8 = O.splitmix64_np(np.uint64(0xB5DB0002) + i)
+    vlen = (8 - (i % np.uint64(11)).astype(np.int64)).clip(1, 8).astype(np.uint8)  # some values shorter than 8 B
+    return addr, value8, vlen
+
+
+def expected_index(ranks, addr, value8, vlen, n):
+    """W:129-145 restated: index slot r = big-endian addr; index_a slot r =
+    the first min(len, 8) value bytes (zero tail)."""
+    idx = np.zeros(n, ">u8")
+    idx[ranks] = addr
+    va = np.zeros((n, 8), np.uint8)
+    vb = value8.view(np.uint8).reshape(-1, 8)
+    keep = np.arange(8)[None, :] < vlen[:, None]
+    va[ranks] = np.where(keep, vb, 0)
+    return idx.tobytes(), va.tobytes()
+
+
+@pytest.mark.parametrize("approx,pass_cache", [(False, 1 << 30), (False, 8 * 70_001), (True, 8 * 99_999),
+                                               (True, 8 * 300_000)])
+def test_index_writer(ctx, tmp_path, approx, pass_cache):
+    """A13: index.db / index_a.db bytes of BSDBWriter.buildIndex, one pass or
+    several (passSize = passCache/8), records fed per pass in batches."""
+    n = 300_000
+    keys = O.gen_keys13(100, n)
+    sig, E, vals, sb = oracle_build(keys, 13, 4)
+    addr, value8, vlen = records(0, n)
+    ranks = O.lookup_batch(sig, n, E, vals, 4, sb)
+    exp_idx, exp_a = expected_index(ranks, addr, value8, vlen, n)
+    ip, ap = str(tmp_path / "index.db"), str(tmp_path / "index_a.db")
+    order = np.random.default_rng(5).permutation(n)  # the scan order does not matter
+    with ctx.mph_build_fixed(keys, 13, 4) as mph:
+        def feed(w):
+            for lo in range(0, n, 64_000):
+                sel = order[lo: lo + 64_000]
+                w.put_fixed(keys.reshape(n, 13)[sel], 13, addr[sel], value8[sel] if approx else None,
+                            vlen[sel] if approx else None)
+        passes = mph.write_index(ip, ap, approx, pass_cache, feed)
+    assert passes == -(-n // min(n, pass_cache // 8))
+    assert open(ip, "rb").read() == exp_idx
+    assert os.path.exists(ap)  # created even in exact mode (W:126)
+    assert open(ap, "rb").read() == (exp_a if approx else b"")
+
+
+def test_index_writer_var_keys(ctx, tmp_path):
+    blob, off = O.gen_keys_var(3, 120_000)
+    n = 120_000
+    sig = O.hash_var(blob, off)
+    rc, E, vals, sb, _ = O.gov_build_mt(sig, 4, THREADS)
+    addr, value8, vlen = records(3, n)
+    exp_idx, exp_a = expected_index(O.lookup_batch(sig, n, E, vals, 4, sb), addr, value8, vlen, n)
+    ip, ap = str(tmp_path / "i.db"), str(tmp_path / "a.db")
+    with ctx.mph_build_var(blob, off, 4) as mph:
+        mph.write_index(ip, ap, True, 8 * 50_000, lambda w: w.put_var(blob, off, addr, value8, vlen))
+    assert open(ip, "rb").read() == exp_idx and open(ap, "rb").read() == exp_a
+
+
+def skewed_keys(n_total, big, rng_seed=3):
+    """n_total 13-byte keys of which `big` fall into bucket 0 of
+    m = n_total/1500+1 (crafted by rejection: bucket 0 of 2 or 3 holds a third
+    of the hash space)."""
+    m = n_total // 1500 + 1
+    rng = np.random.default_rng(rng_seed)
+    cand = rng.integers(0, 256, 13 * 20 * n_total, dtype=np.uint8)
+    sig = O.hash_fixed(cand, 13)
+    b = np.array([O.bucket(int(s), m) for s in sig[:, 0]])
+    k = cand.reshape(-1, 13)
+    return np.concatenate([k[b == 0][:big], k[b != 0][: n_total - big]]).reshape(-1)
+
+
+@pytest.mark.parametrize("n_total,big", [(3001, 2100), (4500, 4000)])
+def test_oversized_bucket_matches_oracle(ctx, n_total, big):
+    """A bucket over the LDS solver's 2048 keys goes to the global-memory
+    solver (no BSDB_E2BIG), bit-identical to the oracle."""
+    keys = skewed_keys(n_total, big)
+    sig = O.hash_fixed(keys, 13)
+    rc, E, vals, sb = O.gov_build(sig, 4)
+    assert rc == 0 and int(E[1] & np.uint64((1 << 56) - 1)) == big
+    E_d, v_d, s_d = ctx.gov_build(dev(sig.view(np.int64)), 4)
+    np.testing.assert_array_equal(u64(E_d), E)
+    np.testing.assert_array_equal(u64(v_d), vals)
+    np.testing.assert_array_equal(u64(s_d)[: sb.size], sb)
+
+
+def test_fvs_limit_fallback_is_identical(ctx, monkeypatch):
+    """the heavy set never exceeds its limit; forcing a tiny limit
+    (the whole-block Gauss-Jordan fallback) changes nothing in the output."""
+    keys = O.gen_keys13(11, 400_000)
+    sig = O.hash_fixed_mt(keys, 13, THREADS)
+    rc, E, vals, sb, _ = O.gov_build_mt(sig, 4, THREADS)
+    for lim in ("6", "40"):
+        monkeypatch.setenv("BSDB_GOV_FVS_MAX", lim)
+        E_d, v_d, s_d = ctx.gov_build(dev(sig.view(np.int64)), 4)
+        np.testing.assert_array_equal(u64(E_d), E)
+        np.testing.assert_array_equal(u64(v_d), vals)
+
+
+def test_verify_option(ctx):
+    keys = O.gen_keys13(12, 200_000)
+    sig = dev(O.hash_fixed(keys, 13).view(np.int64))
+    ctx.set_verify(True)
+    try:
+        ctx.gov_build(sig, 4)  # raises BSDB_EVERIFY on a non-bijective result
+    finally:
+        ctx.set_verify(False)
+
+
+def test_range_builds_sum_to_full_build(ctx):
+    """E4: each rank builds its bucket range into zeroed full-size arrays; the
+    sum of the ranks' arrays (what one RCCL sum-reduce does) is the full build."""
+    n, width, G = 600_000, 5, 3
+    keys = O.gen_keys13(21, n)
+    sig = O.hash_fixed_mt(keys, 13, THREADS)
+    rc, E, vals, sb, _ = O.gov_build_mt(sig, width, THREADS)
+    m = n // 1500 + 1
+    grouped, counts = ctx.partition_owners(dev(sig.view(np.int64)), m, G)
+    assert sum(counts) == n
+    b_of = np.array([O.bucket(int(s), m) for s in sig[:, 0]], np.int64)
+    own = ((b_of + 1) * G - 1) // m
+    assert counts == [int((own == g).sum()) for g in range(G)]
+    Es = torch.zeros(m + 1, dtype=torch.int64, device="cuda")
+    Vs = torch.zeros(int(O.lib().bo_values_words(n)), dtype=torch.int64, device="cuda")
+    Ss = torch.zeros((n * width + 63) // 64 + 1, dtype=torch.int64, device="cuda")
+    e_lo = 0
+    for g in range(G):
+        b_lo, b_hi = g * m // G, (g + 1) * m // G
+        part = grouped[e_lo: e_lo + counts[g]].contiguous()
+        got = u64(part)
+        assert np.all((own[np.isin(sig[:, 0], got[:, 0])] == g))
+        Er = torch.zeros_like(Es); Vr = torch.zeros_like(Vs); Sr = torch.zeros_like(Ss)
+        ctx.gov_build_range(part, n, b_lo, b_hi, e_lo, width, Er, Vr, Sr)
+        Es += Er; Vs += Vr; Ss += Sr
+        e_lo += counts[g]
+    np.testing.assert_array_equal(u64(Es), E)
+    np.testing.assert_array_equal(u64(Vs), vals)
+    np.testing.assert_array_equal(u64(Ss)[: sb.size], sb)
+
+
+def test_rccl_finalize_single_rank(ctx):
+    """B4: the histogram all-reduce + scan inside the library (RCCL, one rank)."""
+    from bsdb_amd.native import Context
+    uid = Context.comm_unique_id()
+    ctx.comm_init(1, 0, uid)
+    n = 3_000_000
+    keys = ctx.gen_keys13(0, n)
+    m = n // 1500 + 1
+    counts = ctx.histogram_fixed(keys, 13, m)
+    E = ctx.histogram_finalize(counts, n)
+    np.testing.assert_array_equal(u64(E), O.edge_offsets(O.histogram_fixed(O.gen_keys13(0, n), 13, m)))
+    # counts over 65535 (one key repeated) take the u32 path
+    big = torch.zeros(10, dtype=torch.int32, device="cuda")
+    big[3] = 70_000; big[7] = 65_535; big[8] = 1
+    E2 = ctx.histogram_finalize(big, 135_536)
+    np.testing.assert_array_equal(u64(E2), O.edge_offsets(big.cpu().numpy().view(np.uint32)))
+    # allreduce_u64 on one rank is the identity
+    x = torch.arange(5, dtype=torch.int64, device="cuda")
+    ctx.allreduce_u64(x)
+    assert x.tolist() == [0, 1, 2, 3, 4]
+
+
+def test_multi_device_context_one_gpu():
+    """B4: bsdb_multi (ncclCommInitAll) over this box's one GPU."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from bsdb_amd.native import Multi
+    n = 2_000_003
+    keys = O.gen_keys13(5, n)
+    with Multi(1) as mc:
+        assert mc.size() == 1
+        E = mc.histogram_fixed(keys, 13)
+    np.testing.assert_array_equal(E, O.edge_offsets(O.histogram_fixed(keys, 13, n // 1500 + 1)))
+    blob, off = O.gen_keys_var(0, 400_000)
+    with Multi(1) as mc:
+        E = mc.histogram_var(blob, off)
+    np.testing.assert_array_equal(E, O.edge_offsets(O.histogram_var(blob, off, 400_000 // 1500 + 1)))
+
+
+def test_calls_on_two_streams_are_ordered(ctx):
+    """two dev calls on different streams share the workspace; the
+    context orders them (the second waits for the first)."""
+    n = 4_000_000
+    m = n // 1500 + 1
+    ka, kb = ctx.gen_keys13(0, n), ctx.gen_keys13(n, n)
+    sa, sb = torch.cuda.Stream(), torch.cuda.Stream()
+    ca = torch.zeros(m, dtype=torch.int32, device="cuda")
+    cb = torch.zeros(m, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    for _ in range(3):
+        ctx.histogram_fixed(ka, 13, m, counts=ca, stream=sa)
+        ctx.histogram_fixed(kb, 13, m, counts=cb, stream=sb)
+    torch.cuda.synchronize()
+    ea = O.histogram_fixed(O.gen_keys13(0, n), 13, m).astype(np.int64) * 3
+    eb = O.histogram_fixed(O.gen_keys13(n, n), 13, m).astype(np.int64) * 3
+    np.testing.assert_array_equal(ca.cpu().numpy(), ea)
+    np.testing.assert_array_equal(cb.cpu().numpy(), eb)
+
+
+def test_fixed_key_len_validated(ctx):
+    from bsdb_amd.native import BsdbError
+    keys = ctx.gen_keys13(0, 10)
+    for L in (0, 256):
+        with pytest.raises(BsdbError):
+            ctx.histogram_fixed(keys, L, 10, n=1)
+    assert ctx.gen_keys13(0, 1000).numel() == 13_000  # no padding key

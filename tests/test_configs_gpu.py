@@ -1,0 +1,200 @@
+"""GPU: every BASELINE.json config at its own size (SURVEY.md §8 sizes),
+through the C ABI, against the CPU oracle (C restatement pinned to the
+reference's spooky.c/mph.c) -- whole arrays where the oracle finishes in
+about a minute on the box's cores, size-independent properties and samples
+where it does not.
+
+  C2  1e8 x 13 B, exact index, cb = 4      full host-buffer build + index.db
+  C3  1e9 x 13 B, index.approximate = true  full build + index.db/index_a.db
+  C4  13 193 787 549 x 13 B (README shape)  full-size histogram == oracle
+  C5  4e9 var-len 8-64 B Zipf, cb = 16      full-size histogram == oracle,
+                                            cb = 16 build on a sample
+"""
+import os
+import shutil
+import tempfile
+import threading
+
+import numpy as np
+import pytest
+
+import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+THREADS = O.cpu_threads()
+README_N = 13_193_787_549
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from bsdb_amd import Context
+    c = Context(0)
+    yield c
+    c.close()
+    torch.cuda.empty_cache()
+
+
+def u64(t):
+    return t.cpu().numpy().view(np.uint64)
+
+
+def in_background(fn, *args):
+    """Runs an oracle call (ctypes releases the GIL) beside the GPU work."""
+    box = {}
+    th = threading.Thread(target=lambda: box.setdefault("r", fn(*args)))
+    th.start()
+    return th, box
+
+
+@pytest.mark.timeout(900)
+def test_c4_full_size_histogram_equals_oracle(ctx):
+    n, m = README_N, README_N // 1500 + 1
+    th, box = in_background(O.histogram_gen13_mt, 0, n, m, THREADS)
+    keys = ctx.gen_keys13(0, n)                      # 171.5 GB in HBM
+    counts = ctx.histogram_fixed(keys, 13, m)
+    E = ctx.edge_offsets(counts)
+    sig = ctx.hash_fixed(keys[: 13 * 100_000], 13)
+    torch.cuda.synchronize()
+    got_counts, got_E = counts.cpu().numpy().view(np.uint32), u64(E)
+    tail = keys[13 * (n - 100_000):].cpu().numpy()
+    del keys, counts, E
+    torch.cuda.empty_cache()
+    assert ctx.fallback_count() == 0
+    assert int(got_E[-1]) == n
+    np.testing.assert_array_equal(u64(sig), O.hash_fixed(O.gen_keys13(0, 100_000), 13))
+    np.testing.assert_array_equal(tail, O.gen_keys13(n - 100_000, 100_000))
+    th.join()
+    exp, _ = box["r"]
+    np.testing.assert_array_equal(got_counts, exp)      # the whole 35 MB histogram
+    np.testing.assert_array_equal(got_E, O.edge_offsets(exp))
+
+
+@pytest.mark.timeout(900)
+def test_c5_full_size_histogram_equals_oracle(ctx):
+    n, m = 4_000_000_000, 4_000_000_000 // 1500 + 1
+    th, box = in_background(O.histogram_genvar_mt, 0, n, m, THREADS)
+    blob, off = ctx.gen_keys_var(0, n)               # ~103 GB: offsets + blob
+    binned = ctx.histogram_var(blob, off, m)
+    ctx.set_histogram_mode(2)
+    try:
+        atomic = ctx.histogram_var(blob, off, m)
+    finally:
+        ctx.set_histogram_mode(0)
+    torch.cuda.synchronize()
+    head_off = u64(off[:10_001])
+    head = blob[: int(head_off[-1])].cpu().numpy()
+    b_np, a_np = binned.cpu().numpy().view(np.uint32), atomic.cpu().numpy().view(np.uint32)
+    del blob, off, binned, atomic
+    torch.cuda.empty_cache()
+    assert ctx.fallback_count() == 0
+    assert int(b_np.astype(np.uint64).sum()) == n
+    np.testing.assert_array_equal(b_np, a_np)
+    eb, eo = O.gen_keys_var(0, 10_000)                 # the device generator is the C5 recipe
+    np.testing.assert_array_equal(head_off, eo)
+    np.testing.assert_array_equal(head, eb)
+    th.join()
+    exp, _ = box["r"]
+    np.testing.assert_array_equal(b_np, exp)
+
+
+@pytest.mark.timeout(600)
+def test_c5_checksum16_build_on_a_sample(ctx):
+    """cb = 16 (C5's hash.checksum.bits) on the first 2e6 C5 keys, device
+    path end to end (generator -> hash -> GOV build -> sign) vs the oracle."""
+    n = 2_000_000
+    blob, off = ctx.gen_keys_var(0, n)
+    sig = ctx.hash_var(blob, off)
+    E, vals, sb = ctx.gov_build(sig, 16)
+    hb, ho = O.gen_keys_var(0, n)
+    osig = O.hash_var(hb, ho)
+    np.testing.assert_array_equal(u64(sig), osig)
+    rc, oE, ov, osb, _ = O.gov_build_mt(osig, 16, THREADS)
+    assert rc == 0
+    np.testing.assert_array_equal(u64(E), oE)
+    np.testing.assert_array_equal(u64(vals), ov)
+    np.testing.assert_array_equal(u64(sb)[: osb.size], osb)
+
+
+def big_tmp(tmp_path, need_bytes):
+    """A directory with room for the index files (tmp, else /dev/shm)."""
+    for d in (str(tmp_path), "/dev/shm"):
+        if os.path.isdir(d) and shutil.disk_usage(d).free > need_bytes * 1.25:
+            return tempfile.mkdtemp(dir=d)
+    pytest.skip(f"no {need_bytes / 1e9:.0f} GB of scratch space for the index files")
+
+
+def records(first, n):
+    i = np.arange(first, first + n, dtype=np.uint64)
+    addr = np.uint64(0x1000) + np.uint64(48) * i      # SimpleCompact record = 1+2+13+32 B
+    value8 = O.splitmix64_np(np.uint64(0xB5DB0002) + i)  # first 8 bytes of the 32-B value (D2)
+    return addr, value8, np.full(n, 8, np.uint8)
+
+
+def full_build_and_index(ctx, tmp_path, n, width, approx, pass_cache):
+    keys = O.gen_keys13_mt(0, n, THREADS)
+    ctx.set_verify(True)  # on-device check: every key's rank, a permutation of [0, n)
+    try:
+        mph = ctx.mph_build_fixed(keys, 13, width)
+    finally:
+        ctx.set_verify(False)
+    addr, value8, vlen = records(0, n)
+    d = big_tmp(tmp_path, 8 * n * (2 if approx else 1))
+    ip, ap = os.path.join(d, "index.db"), os.path.join(d, "index_a.db")
+    B = 50_000_000
+
+    def feed(w):
+        for lo in range(0, n, B):
+            hi = min(n, lo + B)
+            w.put_fixed(keys[13 * lo: 13 * hi], 13, addr[lo:hi], value8[lo:hi] if approx else None,
+                        vlen[lo:hi] if approx else None)
+    passes = mph.write_index(ip, ap, approx, pass_cache, feed)
+    assert passes == -(-n // min(n, pass_cache // 8))
+    return keys, mph, addr, value8, ip, ap
+
+
+@pytest.mark.timeout(900)
+def test_c2_exact_full_build_1e8(ctx, tmp_path):
+    n, width = 100_000_000, 4
+    keys, mph, addr, _, ip, ap = full_build_and_index(ctx, tmp_path, n, width, False, 1 << 30)
+    E, vals, sb = mph.export()
+    # every key: the device's checked getLong == the oracle's lookup on the exported structure
+    ranks = mph.lookup_fixed(keys, 13)
+    sig = O.hash_fixed_mt(keys, 13, THREADS)
+    np.testing.assert_array_equal(ranks, O.lookup_batch_mt(sig, n, E, vals, width, sb, True, THREADS))
+    assert np.array_equal(np.bincount(ranks, minlength=n), np.ones(n, np.int64))
+    # index.db == the W:129-145 restatement, byte for byte; index_a.db empty
+    exp = np.zeros(n, ">u8")
+    exp[ranks] = addr
+    assert os.path.getsize(ip) == 8 * n
+    assert np.array_equal(np.fromfile(ip, ">u8"), exp)
+    assert os.path.getsize(ap) == 0
+    mph.close()
+    shutil.rmtree(os.path.dirname(ip), ignore_errors=True)
+
+
+@pytest.mark.timeout(900)
+def test_c3_approx_full_build_1e9(ctx, tmp_path):
+    n, width = 1_000_000_000, 4
+    # the reference default -ps 1024 (MiB): passSize 2^27 slots, 8 passes (SURVEY.md §8 sizes)
+    keys, mph, addr, value8, ip, ap = full_build_and_index(ctx, tmp_path, n, width, True, 1 << 30)
+    assert os.path.getsize(ip) == 8 * n and os.path.getsize(ap) == 8 * n
+    E, vals, sb = mph.export()
+    rng = np.random.default_rng(33)
+    s = np.sort(rng.choice(n, 200_000, replace=False))
+    skeys = keys.reshape(n, 13)[s].reshape(-1)
+    ssig = O.hash_fixed(skeys, 13)
+    r = O.lookup_batch_mt(ssig, n, E, vals, width, sb, True, THREADS)
+    np.testing.assert_array_equal(mph.lookup_fixed(skeys, 13), r)
+    assert r.min() >= 0 and np.unique(r).size == r.size
+    idx = np.memmap(ip, ">u8", mode="r")
+    ida = np.memmap(ap, "<u8", mode="r")
+    np.testing.assert_array_equal(np.asarray(idx[r]), addr[s])
+    np.testing.assert_array_equal(np.asarray(ida[r]), value8[s])
+    del idx, ida
+    mph.close()
+    shutil.rmtree(os.path.dirname(ip), ignore_errors=True)
