@@ -25,7 +25,7 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-from bsdb_amd.distributed import global_histogram, shard  # noqa: E402
+from bsdb_amd.distributed import shard  # noqa: E402
 
 README_N = 13_193_787_549     # README.md:50-60 record count
 KEY_LEN = 13
@@ -33,11 +33,16 @@ HBM_PEAK_GBS = 8000.0         # MI355X_MICROARCH.md chip table: 8.0 TB/s HBM3E
 
 
 
+def _oracle():
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    return O
+
+
 def cpu_baseline(m: int, target_s: float, threads: int):
     """The oracle's multi-threaded hash+bucket+histogram on resident 13-byte keys
     (same key recipe, same m), timed on this box's host cores; bounded sample."""
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import oracle as O
+    O = _oracle()
     calib_n = 4_000_000
     keys = O.gen_keys13_mt(0, calib_n, threads)
     _, dt = O.histogram_fixed_mt(keys, KEY_LEN, m, threads)
@@ -55,9 +60,66 @@ def cpu_baseline(m: int, target_s: float, threads: int):
             break
     del keys
     return {"value": total_keys / total_s, "unit": "keys/s", "cores": threads, "kind": "port",
+            "cpu_model": O.cpu_model(), "os_cpu_count": os.cpu_count(),
             "sample": f"{passes} pass(es) over {n} resident 13-byte keys (first {n} of the workload's key recipe), "
-                      f"m={m}, {total_s:.1f} s of CPU work, {threads} threads, "
-                      f"oracle bo_histogram_fixed_mt (C restatement pinned to the reference's spooky.c)"}
+                      f"m={m}, {total_s:.1f} s of CPU work, {threads} threads (every CPU this process may use: "
+                      f"affinity capped by the cgroup quota; os.cpu_count() = {os.cpu_count()} counts the whole "
+                      f"machine), oracle bo_histogram_fixed_mt (C restatement pinned to the reference's spooky.c)"}
+
+
+def full_build_gpu(ctx, n: int, width: int, reps: int):
+    """Full build on the device, keys resident in HBM: hash -> GOV build
+    (bucket sort, per-bucket solve, sign with `width` checksum bits) ->
+    getLong of every key -> index scatter (W:129-145).  keys/s over the
+    median run, per-stage device time."""
+    import torch
+    keys = ctx.gen_keys13(0, n)
+    addr = torch.arange(n, dtype=torch.int64, device="cuda")
+    index = torch.empty(n, dtype=torch.int64, device="cuda")
+    runs = []
+    for _ in range(reps + 1):
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+        ev[0].record()
+        sig = ctx.hash_fixed(keys, 13)
+        ev[1].record()
+        E, vals, sb = ctx.gov_build(sig, width)
+        ev[2].record()
+        rank = ctx.lookup(sig, n, E, vals, width, sb, check=True)
+        ctx.index_scatter(rank, addr, 0, n, index)
+        ev[3].record()
+        torch.cuda.synchronize()
+        runs.append([ev[i].elapsed_time(ev[i + 1]) for i in range(3)])
+        del sig, E, vals, sb, rank
+    runs = sorted(runs[1:], key=sum)
+    hash_ms, gov_ms, index_ms = runs[len(runs) // 2]
+    total = hash_ms + gov_ms + index_ms
+    del keys, addr, index
+    torch.cuda.empty_cache()
+    return {"n_keys": n, "checksum_bits": width, "keys_per_s": n / (total / 1e3), "ms": total,
+            "stage_ms": {"hash": hash_ms, "gov_build_sort_solve_sign": gov_ms, "lookup_index_scatter": index_ms}}
+
+
+def full_build_cpu(n: int, width: int, threads: int):
+    """The same stages on the host cores: oracle hash, bo_gov_build_mt (threads
+    over bucket ranges), lookups and the index scatter ("port")."""
+    import time as _t
+    import numpy as np
+    O = _oracle()
+    keys = O.gen_keys13_mt(0, n, threads)
+    t0 = _t.perf_counter()
+    sig = O.hash_fixed_mt(keys, 13, threads)
+    t1 = _t.perf_counter()
+    rc, E, vals, sb, _ = O.gov_build_mt(sig, width, threads)
+    t2 = _t.perf_counter()
+    rank = O.lookup_batch_mt(sig, n, E, vals, width, sb, True, threads)
+    index = np.zeros(n, ">u8")
+    index[rank] = np.arange(n, dtype=np.uint64)
+    t3 = _t.perf_counter()
+    assert rc == 0
+    return {"n_keys": n, "checksum_bits": width, "keys_per_s": n / (t3 - t0), "ms": (t3 - t0) * 1e3,
+            "cores": threads, "kind": "port", "cpu_model": O.cpu_model(),
+            "stage_ms": {"hash": (t1 - t0) * 1e3, "gov_build_sort_solve_sign": (t2 - t1) * 1e3,
+                         "lookup_index_scatter": (t3 - t2) * 1e3}}
 
 
 def main():
@@ -70,7 +132,8 @@ def main():
     ap.add_argument("--chunk", type=int, default=0, help="keys per partitioned chunk (0 = default)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every CPU this process may use")
+    ap.add_argument("--no-full-build", action="store_true", help="skip the full-build figures")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="collective backend (nccl = RCCL over xGMI; gloo only to rehearse N ranks on one GPU)")
     args = ap.parse_args()
@@ -92,9 +155,18 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
         else:
             dist.init_process_group("gloo")
+    if args.cpu_threads <= 0:
+        args.cpu_threads = _oracle().cpu_threads()
 
     from bsdb_amd import Context
     ctx = Context(dev)
+    if world > 1 and args.backend == "nccl":
+        # the one collective runs inside the C ABI (bsdb_dev_histogram_finalize,
+        # RCCL over xGMI); the 128-byte communicator id travels over the
+        # process group once, outside the timed region
+        obj = [Context.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        ctx.comm_init(world, rank, obj[0])
     if args.mode:
         ctx.set_histogram_mode(args.mode)
     if args.chunk:
@@ -124,9 +196,15 @@ def main():
             h = counts.cpu()
             dist.all_reduce(h)
             counts.copy_(h)
+            ctx.edge_offsets(counts, out=E)
+        elif world > 1:
+            counts.zero_()
+            ctx.histogram_fixed(keys, KEY_LEN, m, counts=counts, n=nloc)
+            ctx.histogram_finalize(counts, n, out=E)   # RCCL all-reduce + scan, E[m] == n checked
         else:
-            global_histogram(lambda c: ctx.histogram_fixed(keys, KEY_LEN, m, counts=c, n=nloc), counts)
-        ctx.edge_offsets(counts, out=E)
+            counts.zero_()
+            ctx.histogram_fixed(keys, KEY_LEN, m, counts=counts, n=nloc)
+            ctx.edge_offsets(counts, out=E)
 
     for _ in range(args.warmup):
         step()
@@ -174,6 +252,17 @@ def main():
             except Exception:
                 traffic = None
         log(f"timed {args.steps} steps: {dt * 1e3 / args.steps:.2f} ms/step")
+    full = None
+    if rank == 0 and world == 1 and not args.no_full_build:
+        # the rest of the build beside the histogram
+        # stage: GPU at C2 and C1 size, the CPU port at C1 size
+        del keys
+        torch.cuda.empty_cache()
+        full = {"gpu_c2": full_build_gpu(ctx, 100_000_000, 4, 2), "gpu_c1": full_build_gpu(ctx, 1_000_000, 4, 3)}
+        if not args.no_cpu:
+            full["cpu_c1"] = full_build_cpu(1_000_000, 4, args.cpu_threads)
+        log("full-build figures done")
+    if rank == 0:
         cpu = None
         if not args.no_cpu:
             cpu = cpu_baseline(m, args.cpu_seconds, args.cpu_threads)
@@ -192,8 +281,9 @@ def main():
             "dtype": "u64",
             "data": "synthetic (SURVEY.md §8(d) D2 13-byte keys, generated in HBM before timing)",
             "config": {
-                "workload": "BASELINE config 4: README dataset shape, 13-byte keys, exact index, "
-                            "hash.checksum.bits=4; hash -> bucket -> histogram -> edge offsets",
+                "workload": "BASELINE config 4 (README dataset shape, 13-byte keys), histogram stage: "
+                            "SpookyHash-short -> bucket -> bucket-occupancy histogram -> edge offsets "
+                            "(edgeOffsetAndSeed); the solve/sign/index stages are the full_build figures",
                 "n_keys": n, "key_bytes": KEY_LEN, "num_buckets": m,
                 "keys_per_gpu": nloc if world == 1 else f"~{n // world}",
                 "parallelism": f"key-shard x{world}" + ((" + RCCL all-reduce(histogram)" if args.backend == "nccl"
@@ -211,10 +301,12 @@ def main():
             "kernel_ms_per_step": {"pass1": p1_ms / args.steps, "pass2": p2_ms / args.steps,
                                    "edge_offsets": sc_ms / args.steps},
             "cpu_baseline": cpu,
+            "full_build": full,
             "check": {"E[m]==n": ok},
         }
         print(json.dumps(line), flush=True)
-    del keys
+    if "keys" in locals():
+        del keys
     ctx.close()
     if world > 1:
         dist.destroy_process_group()

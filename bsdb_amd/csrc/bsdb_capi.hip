@@ -878,10 +878,10 @@ int bsdb_dev_gov_build_range(bsdb_ctx *c, const uint64_t *d_sig, uint64_t n_loca
     return gov_build_impl(c, d_sig, n_local, n_global, b_lo, b_hi, e_lo, width, d_E, d_values, d_sigbits, s, false);
 }
 
-int bsdb_dev_partition_owners(bsdb_ctx *c, const uint64_t *d_sig, uint64_t n, uint64_t m, int nranks,
-                              uint64_t *d_out, uint64_t *h_counts, void *stream) {
+int bsdb_dev_partition_owners(bsdb_ctx *c, const uint64_t *d_sig, const uint64_t *d_payload, uint64_t n, uint64_t m,
+                              int nranks, uint64_t *d_out, uint64_t *d_payload_out, uint64_t *h_counts, void *stream) {
     if (!c || nranks < 1 || nranks > OWN_MAXR || m == 0 || m > 0x7FFFFFFFULL || !h_counts ||
-        (n && (!d_sig || !d_out)) || !aligned16(d_sig) || !aligned16(d_out))
+        (n && (!d_sig || !d_out)) || !aligned16(d_sig) || !aligned16(d_out) || (!d_payload != !d_payload_out))
         return BSDB_EINVAL;
     std::lock_guard<std::mutex> g(c->mu);
     HIP_OK(hipSetDevice(c->device));
@@ -903,7 +903,9 @@ int bsdb_dev_partition_owners(bsdb_ctx *c, const uint64_t *d_sig, uint64_t n, ui
         h_counts[g2] = cnt[g2];
     }
     HIP_OK(hipMemcpyAsync(cur, start, nranks * 8, hipMemcpyHostToDevice, s));
-    if (n) k_owner_scatter<<<grid_for(c, n), 256, 0, s>>>(d_sig, n, (uint32_t)(2 * m), m, (uint32_t)nranks, cur, d_out);
+    if (n)
+        k_owner_scatter<<<grid_for(c, n), 256, 0, s>>>(d_sig, d_payload, n, (uint32_t)(2 * m), m, (uint32_t)nranks, cur,
+                                                       d_out, d_payload_out);
     if ((rc = launch_status())) return rc;
     HIP_OK(hipStreamSynchronize(s));  // start[] is a stack buffer
     return BSDB_OK;

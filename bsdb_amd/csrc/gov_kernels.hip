@@ -1354,13 +1354,16 @@ __global__ __launch_bounds__(256) void k_owner_count(const uint64_t *sig, uint64
 }
 
 // cursor[g] starts at rank g's offset in the output
-__global__ __launch_bounds__(256) void k_owner_scatter(const uint64_t *sig, uint64_t n, uint32_t mult, uint64_t m,
-                                                       uint32_t G, unsigned long long *cursor, uint64_t *out) {
+__global__ __launch_bounds__(256) void k_owner_scatter(const uint64_t *sig, const uint64_t *payload, uint64_t n,
+                                                       uint32_t mult, uint64_t m, uint32_t G,
+                                                       unsigned long long *cursor, uint64_t *out,
+                                                       uint64_t *payload_out) {
     const uint64_t stride = (uint64_t)gridDim.x * 256;
     for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
         const ulonglong2 s = reinterpret_cast<const ulonglong2 *>(sig)[i];
         const uint64_t pos = atomicAdd(cursor + owner_of(bucket_of_w(w64(s.x), mult), m, G), 1ULL);
         reinterpret_cast<ulonglong2 *>(out)[pos] = s;
+        if (payload) payload_out[pos] = payload[i];
     }
 }
 

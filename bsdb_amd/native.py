@@ -42,7 +42,7 @@ SIGNATURES = [
     ("bsdb_values_words", _u64, [_u64]),
     ("bsdb_dev_gov_build", _i, [_vp, _vp, _u64, _u32, _vp, _vp, _vp, _vp]),
     ("bsdb_dev_gov_build_range", _i, [_vp, _vp, _u64, _u64, _u64, _u64, _u64, _u32, _vp, _vp, _vp, _vp]),
-    ("bsdb_dev_partition_owners", _i, [_vp, _vp, _u64, _u64, _i, _vp, _vp, _vp]),
+    ("bsdb_dev_partition_owners", _i, [_vp, _vp, _vp, _u64, _u64, _i, _vp, _vp, _vp, _vp]),
     ("bsdb_set_verify", _i, [_vp, _i]),
     ("bsdb_set_histogram_mode", _i, [_vp, _i]),
     ("bsdb_set_frontend", _i, [_vp, _i]),
@@ -257,17 +257,19 @@ class Context:
             self._h, _ptr(sig), sig.shape[0], n_global, b_lo, b_hi, e_lo, width, _ptr(E), _ptr(values),
             _ptr(sigbits) if sigbits is not None else None, _stream(stream)))
 
-    def partition_owners(self, sig, m: int, nranks: int, out=None, stream=None):
-        """Signatures grouped by owning rank (bucket ranges); returns (out, counts)."""
+    def partition_owners(self, sig, m: int, nranks: int, payload=None, stream=None):
+        """Signatures (and one int64 payload per key) grouped by owning rank
+        (bucket ranges); returns (sig_out, payload_out or None, counts)."""
         import torch
         import numpy as np
         n = sig.shape[0]
-        if out is None:
-            out = torch.empty((max(n, 1), 2), dtype=torch.int64, device=sig.device)[:n]
+        out = torch.empty((max(n, 1), 2), dtype=torch.int64, device=sig.device)[:n]
+        pout = torch.empty(max(n, 1), dtype=torch.int64, device=sig.device)[:n] if payload is not None else None
         counts = np.zeros(nranks, np.uint64)
         _check("bsdb_dev_partition_owners", lib().bsdb_dev_partition_owners(
-            self._h, _ptr(sig), n, m, nranks, _ptr(out), counts.ctypes.data, _stream(stream)))
-        return out, [int(x) for x in counts]
+            self._h, _ptr(sig), _ptr(payload) if payload is not None else None, n, m, nranks, _ptr(out),
+            _ptr(pout) if pout is not None else None, counts.ctypes.data, _stream(stream)))
+        return out, pout, [int(x) for x in counts]
 
     def set_verify(self, on: bool):
         _check("bsdb_set_verify", lib().bsdb_set_verify(self._h, 1 if on else 0))

@@ -1,0 +1,165 @@
+"""Host-side mirror of the reference's BSDBWriter (the drop-in seam, B1/B2).
+
+``BSDBWriter`` keeps the reference constructor's arguments and the call
+sequence put* -> build() = buildHash() + buildIndex(), and produces the same
+file set in ``base_path`` (src/main/java/tech/bsdb/write/BSDBWriter.java, "W"):
+
+  kv.db.<p>          records [kLen u8][vLen u16 BE][key][value] of
+                     SimpleCompactKVWriter (SimpleCompactKVWriter.java:36-42;
+                     the kv.db format is out of scope, this is the minimal
+                     writer that produces the record addresses the index needs:
+                     addr = p << 56 | byte offset, :62-73)
+  config.properties  the keys BSDBWriter sets (W:54-58) + record statistics
+  hash.dump          the MPHF in GOV.dump's raw layout (GOV:592-619), the
+                     layout the reference's own load_mph reads (mph.c:28-43);
+                     hash.db itself is a Java-serialized object that the Java
+                     host writes from the same arrays
+  index.db           big-endian record address per rank (W:107-155)
+  index_a.db         approximate mode: first <= 8 value bytes per rank;
+                     created empty otherwise (W:126)
+
+Every compute step is the C ABI (bsdb_mph_build_var, bsdb_index_*): no CPU
+fallback.  ``put`` is per record as in the reference; ``put_batch`` takes a
+whole key blob at once.
+"""
+from __future__ import annotations
+
+import os
+from typing import Optional
+
+import numpy as np
+
+from .native import Context, Mph
+
+SLOT_SIZE = 8          # Common.java SLOT_SIZE
+MAX_KEY_SIZE = 255     # Common.java MAX_KEY_SIZE
+RECORD_HEADER = 3      # Common.java RECORD_HEADER_SIZE
+
+
+class BSDBWriter:
+    def __init__(self, base_path: str, tmp_dir: Optional[str] = None, checksum_bits: int = 4,
+                 pass_cache_size: int = 1 << 30, compact: bool = True, compress: bool = False,
+                 compress_block_size: int = 8192, shared_dict_size: int = 0, approximate_mode: bool = False,
+                 partitions: int = 1, device: int = 0):
+        if compress or not compact:
+            raise NotImplementedError("only the compact kv.db layout is mirrored (kv.db formats are out of scope)")
+        self.base = base_path
+        os.makedirs(base_path, exist_ok=True)
+        self.checksum_bits = checksum_bits
+        self.pass_cache_size = pass_cache_size
+        self.approximate = approximate_mode
+        self.partitions = partitions
+        self.compress_block_size = compress_block_size
+        self._keys: list = []
+        self._values: list = []
+        self._batches: list = []  # (blob, offsets, value8, vlen, value bytes total)
+        self.ctx = Context(device)
+
+    # W:75-89
+    def put(self, key: bytes, value: bytes):
+        if key is None or value is None:
+            raise RuntimeError("currently null key/value is not support.")
+        if not 0 < len(key) <= MAX_KEY_SIZE:
+            raise ValueError("key length must be 1..255 bytes")
+        self._keys.append(bytes(key))
+        self._values.append(bytes(value))
+
+    def put_batch(self, blob: np.ndarray, offsets: np.ndarray, values: list):
+        """Keys blob[offsets[i]:offsets[i+1]] with values[i] (bytes each)."""
+        off = np.ascontiguousarray(offsets, np.uint64)
+        lens = np.diff(off)
+        if lens.size and (lens.min() == 0 or lens.max() > MAX_KEY_SIZE):
+            raise ValueError("key length must be 1..255 bytes")
+        if len(values) != lens.size:
+            raise ValueError("one value per key")
+        self._batches.append((np.ascontiguousarray(blob, np.uint8), off, list(values)))
+
+    def _records(self):
+        """All records as (key blob, offsets, values list)."""
+        blobs, offs, vals, base = [], [np.zeros(1, np.uint64)], [], 0
+        if self._keys:
+            lens = np.fromiter((len(k) for k in self._keys), np.uint64, len(self._keys))
+            blobs.append(np.frombuffer(b"".join(self._keys), np.uint8))
+            offs.append(np.cumsum(lens, dtype=np.uint64))
+            vals += self._values
+            base = int(offs[-1][-1])
+        for blob, off, v in self._batches:
+            blobs.append(blob[int(off[0]): int(off[-1])])
+            offs.append(off[1:] - off[0] + np.uint64(base))
+            vals += v
+            base += int(off[-1] - off[0])
+        blob = np.concatenate(blobs) if blobs else np.zeros(0, np.uint8)
+        return blob, np.concatenate(offs), vals
+
+    def _write_kv(self, blob, off, vals):
+        """kv.db.<p>: record i goes to partition i % partitions; returns addresses."""
+        n = off.size - 1
+        addr = np.zeros(n, np.uint64)
+        files = [open(os.path.join(self.base, f"kv.db.{p}"), "wb") for p in range(self.partitions)]
+        pos = [0] * self.partitions
+        try:
+            for i in range(n):
+                p = i % self.partitions
+                k = blob[int(off[i]): int(off[i + 1])].tobytes()
+                v = vals[i]
+                files[p].write(bytes([len(k)]) + len(v).to_bytes(2, "big") + k + v)
+                addr[i] = (p << 56) | pos[p]
+                pos[p] += RECORD_HEADER + len(k) + len(v)
+        finally:
+            for f in files:
+                f.close()
+        return addr
+
+    def _write_config(self, off, vals):
+        n = off.size - 1
+        klen = np.diff(off)
+        vlen = np.fromiter((len(v) for v in vals), np.int64, n)
+        props = {
+            "kv.compressed": "false", "kv.compact": "true", "kv.compress.block.size": self.compress_block_size,
+            "index.approximate": str(self.approximate).lower(), "hash.checksum.bits": self.checksum_bits,
+            "kv.count": n, "kv.key.len.max": int(klen.max()) if n else 0,
+            "kv.key.len.avg": float(klen.mean()) if n else 0.0, "kv.value.len.max": int(vlen.max()) if n else 0,
+            "kv.value.len.avg": float(vlen.mean()) if n else 0.0,
+        }
+        with open(os.path.join(self.base, "config.properties"), "w") as f:
+            for k, v in props.items():
+                f.write(f"{k} = {v}\n")
+
+    # W:91-97
+    def build(self):
+        blob, off, vals = self._records()
+        self._addr = self._write_kv(blob, off, vals)
+        self._write_config(off, vals)
+        self._blob, self._off, self._vals = blob, off, vals
+        mph = self.build_hash()
+        self.build_index(mph)
+        return mph
+
+    # W:99-105
+    def build_hash(self) -> Mph:
+        mph = self.ctx.mph_build_var(self._blob, self._off, self.checksum_bits)
+        mph.dump(os.path.join(self.base, "hash.dump"))
+        return mph
+
+    # W:107-155
+    def build_index(self, mph: Mph, batch: int = 1 << 22):
+        n = self._off.size - 1
+        value8 = np.zeros(n, np.uint64)
+        vlen = np.zeros(n, np.uint8)
+        if self.approximate:
+            for i, v in enumerate(self._vals):
+                head = v[:8]
+                value8[i] = int.from_bytes(head, "little")
+                vlen[i] = len(head)
+        off = self._off
+
+        def feed(w):  # one kv.db scan per pass (W:134)
+            for lo in range(0, n, batch):
+                hi = min(n, lo + batch)
+                w.put_var(self._blob, off[lo: hi + 1], self._addr[lo:hi], value8[lo:hi] if self.approximate else None,
+                          vlen[lo:hi] if self.approximate else None)
+        return mph.write_index(os.path.join(self.base, "index.db"), os.path.join(self.base, "index_a.db"),
+                               self.approximate, self.pass_cache_size, feed)
+
+    def close(self):
+        self.ctx.close()

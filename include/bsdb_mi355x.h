@@ -160,10 +160,12 @@ int bsdb_dev_gov_build_range(bsdb_ctx *ctx, const uint64_t *d_sig, uint64_t n_lo
 /* E4 ownership: rank g of `nranks` owns buckets [g*m/nranks, (g+1)*m/nranks)
  * (m = num_buckets; the bucket is monotone in sig0, CBHS:129-138).  Groups the n
  * signatures of d_sig by owning rank into d_out (rank 0's first; order within a
- * rank unspecified) and writes the per-rank counts to h_counts[nranks]
- * (synchronises). */
-int bsdb_dev_partition_owners(bsdb_ctx *ctx, const uint64_t *d_sig, uint64_t n, uint64_t num_buckets, int nranks,
-                              uint64_t *d_out, uint64_t *h_counts, void *stream);
+ * rank unspecified) together with one u64 payload per key (the record address
+ * of the index stage; d_payload / d_payload_out may be NULL), and writes the
+ * per-rank counts to h_counts[nranks] (synchronises). */
+int bsdb_dev_partition_owners(bsdb_ctx *ctx, const uint64_t *d_sig, const uint64_t *d_payload, uint64_t n,
+                              uint64_t num_buckets, int nranks, uint64_t *d_out, uint64_t *d_payload_out,
+                              uint64_t *h_counts, void *stream);
 /* Debug/test option: after every GOV build, look every key up again on the
  * device and check the ranks form a permutation of [0, n) (BSDB_EVERIFY if not). */
 int bsdb_set_verify(bsdb_ctx *ctx, int enable);

@@ -105,6 +105,11 @@ uint32_t bo_bucket(uint64_t sig0, uint64_t num_buckets) {
     return (uint32_t)(prod >> 64);
 }
 
+/* bucket of every signature (batched GOV:559) */
+void bo_bucket_batch(const uint64_t *sig, uint64_t n, uint64_t num_buckets, uint32_t *out) {
+    for (uint64_t i = 0; i < n; i++) out[i] = bo_bucket(sig[2 * i], num_buckets);
+}
+
 /* GOV:155-162,315-317 -- OFFSET_MASK = 2^56-1, C_TIMES_256 = floor(1.10*256) = 281. */
 uint64_t bo_vertex_offset(uint64_t eos) { return ((eos & (~0ULL >> 8)) * 281) >> 8; }
 
@@ -773,6 +778,7 @@ typedef struct {
     const bo_mph *mp; uint64_t m; uint32_t *local; uint64_t *cursor; uint64_t *sorted;
     uint64_t *E; uint64_t *values; int32_t *ws; uint8_t *vals; int rc;
     uint32_t width; uint64_t *sigs;
+    uint64_t b0, e0;  /* range build: first bucket, keys before it */
 } gv_job;
 
 static void run_jobs(gv_job *jobs, int threads, void *(*fn)(void *)) {
@@ -797,24 +803,25 @@ static void *gv_worker(void *arg) {
             j->outi[i] = j->check ? bo_lookup(j->mp, j->sig + 2 * i) : bo_lookup_nocheck(j->mp, j->sig + 2 * i);
         break;
     case 2:
-        for (uint64_t i = j->lo; i < j->hi; i++) j->local[bo_bucket(j->sig[2 * i], j->m)]++;
+        for (uint64_t i = j->lo; i < j->hi; i++) j->local[bo_bucket(j->sig[2 * i], j->m) - j->b0]++;
         break;
     case 3:
         for (uint64_t i = j->lo; i < j->hi; i++) {
-            const uint64_t p = j->cursor[bo_bucket(j->sig[2 * i], j->m)]++;
+            const uint64_t p = j->cursor[bo_bucket(j->sig[2 * i], j->m) - j->b0]++;
             j->sorted[2 * p] = j->sig[2 * i];
             j->sorted[2 * p + 1] = j->sig[2 * i + 1];
         }
         break;
     case 4:  /* buckets [lo, hi): sort, duplicate check, solve (GOV:405-440) */
         for (uint64_t b = j->lo; b < j->hi && !j->rc; b++) {
-            const uint64_t lo = j->E[b] & (~0ULL >> 8), hi = j->E[b + 1] & (~0ULL >> 8);
+            const uint64_t glo = j->E[b] & (~0ULL >> 8), ghi = j->E[b + 1] & (~0ULL >> 8);
+            const uint64_t lo = glo - j->e0, hi = ghi - j->e0;  /* positions in the range's sorted array */
             qsort(j->sorted + 2 * lo, hi - lo, 16, cmp_sig);
             for (uint64_t i = lo + 1; i < hi; i++)
                 if (j->sorted[2 * i] == j->sorted[2 * i - 2] && j->sorted[2 * i + 1] == j->sorted[2 * i - 1]) j->rc = -1;
             if (j->rc) break;
-            const uint64_t vo = bo_vertex_offset(lo);
-            const uint32_t nv = (uint32_t)(bo_vertex_offset(hi) - vo);
+            const uint64_t vo = bo_vertex_offset(glo);
+            const uint32_t nv = (uint32_t)(bo_vertex_offset(ghi) - vo);
             uint64_t s = 0;
             for (; s < 256; s++)
                 if (!solve_bucket(j->sorted + 2 * lo, (uint32_t)(hi - lo), nv, s << 56, j->vals, j->ws)) break;
@@ -861,47 +868,53 @@ void bo_lookup_batch_mt(const bo_mph *mp, const uint64_t *sig, uint64_t n, int c
     run_jobs(jobs, threads, gv_worker);
 }
 
-int bo_gov_build_mt(const uint64_t *sig, uint64_t n, uint32_t sig_width, uint64_t *E, uint64_t *values,
-                    uint64_t values_words, uint64_t *signatures, uint64_t sig_words, int threads, double *seconds) {
+/* The build of buckets [b_lo, b_hi) of a GOV structure over n_global keys
+ * from the n_local signatures of that range (any order), e_lo = keys in the
+ * buckets below b_lo: writes E[b_lo..b_hi) (E[m] too when b_hi == m), the
+ * range's 2-bit fields and checksum fields into FULL-size arrays the caller
+ * zeroed (fields of different ranges are disjoint bits, so the ranges' arrays
+ * add up to the whole build).  The restatement of bsdb_dev_gov_build_range. */
+int bo_gov_build_range_mt(const uint64_t *sig, uint64_t n_local, uint64_t n_global, uint64_t b_lo, uint64_t b_hi,
+                          uint64_t e_lo, uint32_t sig_width, uint64_t *E, uint64_t *values, uint64_t *signatures,
+                          int threads) {
     threads = clamp_threads(threads);
-    const double t0 = now_s();
-    const uint64_t m = bo_num_buckets(n);
+    const uint64_t m = bo_num_buckets(n_global), nb = b_hi - b_lo, n = n_local;
     gv_job jobs[256];
     uint64_t *sorted = (uint64_t *)malloc((n ? n : 1) * 16);
-    uint32_t *local = (uint32_t *)calloc((size_t)threads * m, 4);
-    uint64_t *cursor = (uint64_t *)malloc((size_t)threads * m * 8);
-    /* A6 histogram, per thread slice */
+    uint32_t *local = (uint32_t *)calloc((size_t)threads * (nb + 1), 4);
+    uint64_t *cursor = (uint64_t *)malloc((size_t)threads * (nb + 1) * 8);
+    /* A6 histogram of the range, per thread slice (bucket b at b - b_lo) */
     for (int t = 0; t < threads; t++)
         jobs[t] = (gv_job){.kind = 2, .sig = sig, .lo = n * t / threads, .hi = n * (t + 1) / threads, .m = m,
-                           .local = local + (size_t)t * m};
+                           .b0 = b_lo, .local = local + (size_t)t * (nb + 1)};
     run_jobs(jobs, threads, gv_worker);
-    memset(E, 0, (m + 1) * 8);
-    for (uint64_t b = 0; b < m; b++) {
-        uint64_t acc = E[b];
+    uint64_t acc = 0;
+    for (uint64_t i = 0; i < nb; i++) {
+        E[b_lo + i] = e_lo + acc;
         for (int t = 0; t < threads; t++) {
-            cursor[(size_t)t * m + b] = acc;
-            acc += local[(size_t)t * m + b];
+            cursor[(size_t)t * (nb + 1) + i] = acc;
+            acc += local[(size_t)t * (nb + 1) + i];
         }
-        E[b + 1] = acc;
     }
-    /* bucket order (stable per thread slice; each bucket is sorted next) */
+    E[b_hi] = e_lo + acc;  /* the next range's offset (cleared below unless b_hi == m) */
     for (int t = 0; t < threads; t++)
         jobs[t] = (gv_job){.kind = 3, .sig = sig, .lo = n * t / threads, .hi = n * (t + 1) / threads, .m = m,
-                           .cursor = cursor + (size_t)t * m, .sorted = sorted};
+                           .b0 = b_lo, .cursor = cursor + (size_t)t * (nb + 1), .sorted = sorted};
     run_jobs(jobs, threads, gv_worker);
+    uint32_t maxc = 0;
+    for (uint64_t i = 0; i < nb; i++) {
+        const uint64_t c = (E[b_lo + i + 1] & (~0ULL >> 8)) - (E[b_lo + i] & (~0ULL >> 8));
+        if (c > maxc) maxc = (uint32_t)c;
+    }
     free(local);
     free(cursor);
-    memset(values, 0, values_words * 8);
-    uint32_t maxc = 0;
-    for (uint64_t b = 0; b < m; b++) if (E[b + 1] - E[b] > maxc) maxc = (uint32_t)(E[b + 1] - E[b]);
     const uint32_t maxnv = (uint32_t)(bo_vertex_offset(maxc) + 4);
-    /* bucket ranges of ~n/threads keys each */
-    uint64_t b0 = 0;
+    uint64_t b0 = b_lo;
     for (int t = 0; t < threads; t++) {
         uint64_t b1 = b0;
-        const uint64_t target = n * (t + 1) / threads;
-        while (b1 < m && (t == threads - 1 || E[b1] < target)) b1++;
-        jobs[t] = (gv_job){.kind = 4, .lo = b0, .hi = b1, .E = E, .values = values, .sorted = sorted,
+        const uint64_t target = e_lo + n * (t + 1) / threads;
+        while (b1 < b_hi && (t == threads - 1 || E[b1] < target)) b1++;
+        jobs[t] = (gv_job){.kind = 4, .lo = b0, .hi = b1, .E = E, .values = values, .sorted = sorted, .e0 = e_lo,
                            .ws = (int32_t *)malloc(solve_ws_words(maxc + 1, maxnv + 1) * 4 + 64),
                            .vals = (uint8_t *)malloc(maxnv + 1)};
         b0 = b1;
@@ -914,14 +927,24 @@ int bo_gov_build_mt(const uint64_t *sig, uint64_t n, uint32_t sig_width, uint64_
         free(jobs[t].vals);
     }
     if (!rc && sig_width) {
-        memset(signatures, 0, sig_words * 8);
-        bo_mph mp = {n, 2 * m, 0, m, E, values, 0, NULL};
+        bo_mph mp = {n_global, 2 * m, 0, m, E, values, 0, NULL};
         for (int t = 0; t < threads; t++)
             jobs[t] = (gv_job){.kind = 5, .lo = n * t / threads, .hi = n * (t + 1) / threads, .mp = &mp,
                                .sorted = sorted, .width = sig_width, .sigs = signatures};
         run_jobs(jobs, threads, gv_worker);
     }
+    if (b_hi < m) E[b_hi] = 0;
     free(sorted);
+    return rc;
+}
+
+int bo_gov_build_mt(const uint64_t *sig, uint64_t n, uint32_t sig_width, uint64_t *E, uint64_t *values,
+                    uint64_t values_words, uint64_t *signatures, uint64_t sig_words, int threads, double *seconds) {
+    const double t0 = now_s();
+    const uint64_t m = bo_num_buckets(n);
+    memset(values, 0, values_words * 8);
+    if (sig_width) memset(signatures, 0, sig_words * 8);
+    const int rc = bo_gov_build_range_mt(sig, n, n, 0, m, 0, sig_width, E, values, signatures, threads);
     if (seconds) *seconds = now_s() - t0;
     return rc;
 }

@@ -29,6 +29,7 @@ void bo_spooky_rehash(const uint64_t sig[2], uint64_t seed, uint64_t out[4]);
 uint64_t bo_num_buckets(uint64_t n);                       /* n/1500 + 1            */
 uint32_t bo_bucket(uint64_t sig0, uint64_t num_buckets);   /* multiplyHigh(sig0>>>1, 2m) */
 uint64_t bo_vertex_offset(uint64_t edge_offset_seed);      /* ((x & 2^56-1)*281)>>8  */
+void bo_bucket_batch(const uint64_t *sig /* 2n */, uint64_t n, uint64_t num_buckets, uint32_t *out);
 void bo_signature_to_equation(const uint64_t sig[2], uint64_t seed_bits, uint32_t nv,
                               uint32_t e[3]);              /* mph.c:63-71 */
 uint64_t bo_count_nonzero_pairs(uint64_t start, uint64_t end, const uint64_t *array);
@@ -102,6 +103,11 @@ uint64_t bo_values_words(uint64_t n);    /* words of the 2-bit value array */
  * ("port") of bench.py.  Returns as bo_gov_build; *seconds = elapsed. */
 int bo_gov_build_mt(const uint64_t *sig, uint64_t n, uint32_t sig_width, uint64_t *E, uint64_t *values,
                     uint64_t values_words, uint64_t *signatures, uint64_t sig_words, int threads, double *seconds);
+/* One bucket range [b_lo, b_hi) of a build over n_global keys into zeroed
+ * full-size arrays (the multi-GPU build's per-rank step). */
+int bo_gov_build_range_mt(const uint64_t *sig, uint64_t n_local, uint64_t n_global, uint64_t b_lo, uint64_t b_hi,
+                          uint64_t e_lo, uint32_t sig_width, uint64_t *E, uint64_t *values, uint64_t *signatures,
+                          int threads);
 /* Threaded lookups (bench / large tests). */
 void bo_lookup_batch_mt(const bo_mph *m, const uint64_t *sig, uint64_t n, int check, int64_t *out, int threads);
 /* Threaded signatures of 13-byte keys (full-build baseline input). */

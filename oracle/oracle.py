@@ -69,6 +69,10 @@ def lib() -> C.CDLL:
             L.bo_gov_build.restype = C.c_int
         if hasattr(L, "bo_lookup_batch"):
             L.bo_lookup_batch.argtypes = [C.POINTER(BoMph), _u64p, C.c_uint64, C.c_int, C.POINTER(C.c_int64)]
+        L.bo_bucket_batch.argtypes = [_u64p, C.c_uint64, C.c_uint64, _u32p]
+        L.bo_gov_build_range_mt.argtypes = [_u64p, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64,
+                                            C.c_uint32, _u64p, _u64p, _u64p, C.c_int]
+        L.bo_gov_build_range_mt.restype = C.c_int
         L.bo_gov_build_mt.argtypes = [_u64p, C.c_uint64, C.c_uint32, _u64p, _u64p, C.c_uint64, _u64p, C.c_uint64,
                                       C.c_int, C.POINTER(C.c_double)]
         L.bo_gov_build_mt.restype = C.c_int
@@ -331,3 +335,20 @@ def splitmix64_np(x: np.ndarray) -> np.ndarray:
         z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
         z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
         return z ^ (z >> np.uint64(31))
+
+
+def buckets(sig: np.ndarray, m: int) -> np.ndarray:
+    sig = np.ascontiguousarray(sig, np.uint64).reshape(-1, 2)
+    out = np.zeros(max(sig.shape[0], 1), np.uint32)
+    lib().bo_bucket_batch(_p(sig, _u64p), sig.shape[0], m, _p(out, _u32p))
+    return out[: sig.shape[0]]
+
+
+def gov_build_range(sig: np.ndarray, n_global: int, b_lo: int, b_hi: int, e_lo: int, width: int,
+                    E: np.ndarray, values: np.ndarray, sigbits: np.ndarray, threads: int = 1) -> int:
+    """bo_gov_build_range_mt into caller-zeroed full-size u64 arrays (in place)."""
+    sig = np.ascontiguousarray(sig, np.uint64).reshape(-1, 2)
+    for a in (E, values, sigbits):
+        assert a.dtype == np.uint64 and a.flags.c_contiguous
+    return lib().bo_gov_build_range_mt(_p(sig, _u64p), sig.shape[0], n_global, b_lo, b_hi, e_lo, width,
+                                       _p(E, _u64p), _p(values, _u64p), _p(sigbits, _u64p), threads)

@@ -237,7 +237,10 @@ def test_range_builds_sum_to_full_build(ctx):
     sig = O.hash_fixed_mt(keys, 13, THREADS)
     rc, E, vals, sb, _ = O.gov_build_mt(sig, width, THREADS)
     m = n // 1500 + 1
-    grouped, counts = ctx.partition_owners(dev(sig.view(np.int64)), m, G)
+    grouped, addr_g, counts = ctx.partition_owners(dev(sig.view(np.int64)), m, G,
+                                                   payload=torch.arange(n, dtype=torch.int64, device="cuda"))
+    # the payload travels with its signature
+    np.testing.assert_array_equal(u64(grouped), sig[addr_g.cpu().numpy()])
     assert sum(counts) == n
     b_of = np.array([O.bucket(int(s), m) for s in sig[:, 0]], np.int64)
     own = ((b_of + 1) * G - 1) // m

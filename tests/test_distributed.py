@@ -61,3 +61,117 @@ def test_gloo_sharded_histogram(world):
     for _, c, E in res:
         np.testing.assert_array_equal(c.view(np.uint32), ref)
         np.testing.assert_array_equal(E, refE)
+
+
+# ---- E4: the multi-GPU full build (bucket-range owners, one all-to-all) ----
+class OracleBuild:
+    """CPU stand-in for bsdb_amd.distributed.DeviceBuild (test infrastructure):
+    the oracle's range build, lookups and the index scatter on host tensors."""
+
+    def __init__(self, O):
+        self.O = O
+
+    def zeros(self, count):
+        return torch.zeros(count, dtype=torch.int64)
+
+    def partition(self, sig, addr, m, world):
+        s = sig.numpy().view(np.uint64).reshape(-1, 2)
+        b = self.O.buckets(s, m).astype(np.int64)
+        own = ((b + 1) * world - 1) // m
+        order = np.argsort(own, kind="stable")
+        counts = [int((own == g).sum()) for g in range(world)]
+        return sig[torch.from_numpy(order)], addr[torch.from_numpy(order)], counts
+
+    def build_range(self, sig, n_global, b_lo, b_hi, e_lo, width, E, values, sigbits):
+        sb = sigbits if sigbits is not None else torch.zeros(1, dtype=torch.int64)
+        rc = self.O.gov_build_range(sig.numpy().view(np.uint64), n_global, b_lo, b_hi, e_lo, width,
+                                    E.numpy().view(np.uint64), values.numpy().view(np.uint64),
+                                    sb.numpy().view(np.uint64), 2)
+        assert rc == 0
+
+    def index_slice(self, sig, addr, n_global, E, values, width, sigbits, e_lo, n_local):
+        sb = sigbits.numpy().view(np.uint64) if sigbits is not None else None
+        r = self.O.lookup_batch(sig.numpy().view(np.uint64), n_global, E.numpy().view(np.uint64),
+                                values.numpy().view(np.uint64), width, sb, True)
+        assert r.min() >= e_lo and r.max() < e_lo + n_local
+        idx = np.zeros(n_local, ">u8")
+        idx[r - e_lo] = addr.numpy().view(np.uint64)
+        return torch.from_numpy(idx.view(np.int64).copy())
+
+
+def _e4_worker(rank, world, port, n, width, path, q, use_gpu):
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle"))
+    import oracle as O
+    from bsdb_amd.distributed import DeviceBuild, sharded_full_build, write_index_slice
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    lo, hi = shard(n, rank, world)
+    keys = O.gen_keys13(lo, hi - lo)
+    addr = torch.arange(lo, hi, dtype=torch.int64) * 48 + 4096
+    if use_gpu:
+        from bsdb_amd import Context
+        ctx = Context(0)
+        backend = DeviceBuild(ctx)
+        sig = ctx.hash_fixed(torch.from_numpy(keys).cuda(), 13)
+        addr = addr.cuda()
+    else:
+        backend = OracleBuild(O)
+        sig = torch.from_numpy(O.hash_fixed(keys, 13).view(np.int64).copy())
+    res = sharded_full_build(backend, sig, addr, n, width)
+    if rank == 0:
+        write_index_slice(path, 0, None, n, create=True)
+    dist.barrier()
+    write_index_slice(path, res["e_lo"], res["index"], n, create=False)
+    dist.barrier()
+    out = {k: (v.cpu().numpy().copy() if hasattr(v, "cpu") else v) for k, v in res.items() if k != "index"}
+    q.put((rank, out))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def run_e4(world, n, width, tmp_path, use_gpu):
+    path = str(tmp_path / f"index_{world}.db")
+    port = 29700 + world * 11 + os.getpid() % 400 + (50 if use_gpu else 0)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_e4_worker, args=(r, world, port, n, width, path, q, use_gpu)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in ps)
+    for p in ps:
+        p.join(120)
+        assert p.exitcode == 0
+    import oracle as O
+    sig = O.hash_fixed(O.gen_keys13(0, n), 13)
+    rc, E, vals, sb, _ = O.gov_build_mt(sig, width, 4)
+    assert rc == 0
+    r0 = res[0]
+    np.testing.assert_array_equal(r0["E"].view(np.uint64), E)
+    np.testing.assert_array_equal(r0["values"].view(np.uint64), vals)
+    if width:
+        np.testing.assert_array_equal(r0["sigbits"].view(np.uint64)[: sb.size], sb)
+    # ranks' slices tile [0, n) in rank order; index.db == the whole-build restatement
+    assert sum(res[g]["n_local"] for g in range(world)) == n
+    assert [res[g]["e_lo"] for g in range(world)] == list(np.cumsum([0] + [res[g]["n_local"] for g in range(world)])[:-1])
+    ranks = O.lookup_batch(sig, n, E, vals, width, sb if width else None, True)
+    exp = np.zeros(n, ">u8")
+    exp[ranks] = np.arange(n, dtype=np.uint64) * 48 + 4096
+    assert open(path, "rb").read() == exp.tobytes()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_multi_gpu_full_build_oracle_standins(world, tmp_path):
+    """E4 on CPU: ranks exchange (sig0, sig1, addr) by bucket-range owner with
+    one all-to-all, build their ranges, sum-reduce the structure and write
+    their index.db slices; equal to the single-process build."""
+    run_e4(world, 240_007, 4, tmp_path, use_gpu=False)
+
+
+@pytest.mark.gpu
+def test_gloo_multi_gpu_full_build_hip_ranks(tmp_path):
+    """The same with the HIP kernels per rank (two ranks on this one GPU,
+    gloo for the collectives): the rehearsal of the 8-GPU RCCL run."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    run_e4(2, 600_001, 4, tmp_path, use_gpu=True)
