@@ -766,7 +766,7 @@ static int gov_build_impl(bsdb_ctx *c, const uint64_t *d_sig, uint64_t n_local, 
     if ((rc = grow(&c->g_status, &c->g_status_bytes, 16))) return rc;
     const uint32_t big_cap = (uint32_t)(n_local / (GS_CMAX + 1) + 1);
     if ((rc = grow(&c->g_big, &c->g_big_bytes, (size_t)big_cap * 4))) return rc;
-    const uint32_t solve_grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(nb, (uint64_t)c->num_cus));
+    const uint32_t solve_grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(nb, (uint64_t)c->num_cus * GS_PER_CU));
     if ((rc = grow(&c->g_scratch, &c->g_scratch_bytes, (size_t)solve_grid * solve_scratch_words<SolveLds>() * 8)))
         return rc;
     uint32_t *counts = (uint32_t *)c->g_counts, *status = (uint32_t *)c->g_status;
@@ -825,6 +825,9 @@ static int gov_build_impl(bsdb_ctx *c, const uint64_t *d_sig, uint64_t n_local, 
         std::vector<uint64_t> h((size_t)solve_grid * GP_N);
         HIP_OK(hipMemcpyAsync(h.data(), d_prof, h.size() * 8, hipMemcpyDeviceToHost, s));
         HIP_OK(hipStreamSynchronize(s));
+        int per_cu = 0;
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_gov_solve, GS_THREADS, 0);
+        fprintf(stderr, "[gov-profile] solver workgroups per CU: %d (LDS %zu B each)\n", per_cu, sizeof(SolveLds));
         print_gov_profile(h, solve_grid, m);
     }
     const MphView v{d_E, d_values, nullptr, n_global, mult, width};

@@ -27,9 +27,16 @@
 
 namespace bsdb {
 
-constexpr int GS_THREADS = 1024;
-constexpr int GS_CMAX = 2048;    // keys per bucket solved in LDS (expected ~1500, sigma ~39)
-constexpr int GS_NVMAX = 2304;   // > vertex_offset span of GS_CMAX keys
+#ifndef GOV_THREADS
+#define GOV_THREADS 512  // workgroup size of the solver
+#endif
+constexpr int GS_THREADS = GOV_THREADS;
+// Two solver workgroups per CU (LDS <= 80 KiB each): one's single-wave
+// phases (greedy, BFS, FVS selection) overlap the other's.  4.2 sigma above
+// the mean bucket; larger buckets (~1e-5 of them) take the global-slab path.
+constexpr int GS_PER_CU = 2;
+constexpr int GS_CMAX = 1664;    // keys per bucket solved in LDS (expected ~1500, sigma ~39)
+constexpr int GS_NVMAX = 1872;   // > vertex_offset span of GS_CMAX keys
 constexpr int GS_TINY = 12;      // brute-force buckets (only in sets of < ~1500 keys)
 #ifndef GOV_PICK_REPS
 #define GOV_PICK_REPS 8  // FVS: pairs of heavy hinges taken per stuck cascade
@@ -38,7 +45,7 @@ constexpr int GS_WMAX = (GS_CMAX + 1 + 63) / 64;  // words per bit-sliced row
 // Oversized buckets (adversarial or skewed key sets: > GS_CMAX keys, 14 sigma
 // above the mean for random keys) are solved by the same code with its state
 // in a per-workgroup slab of global memory, up to GB_CMAX keys.
-constexpr int GB_CMAX = 16384;
+constexpr int GB_CMAX = 16384;  // a power of two (the bitonic sort's padding)
 constexpr int GB_THREADS = 256;  // sort of an oversized bucket
 // FVS: most heavy hinges of a block (a larger set falls back to Gauss-Jordan
 // over the whole block).  SolveArgs::fvs_max may lower it (tests force the
@@ -86,7 +93,8 @@ __device__ __forceinline__ bool sig_less(ulonglong2 a, ulonglong2 b) { return a.
 // duplicate check on neighbours (CBHS:969-972).
 __global__ __launch_bounds__(256) void k_bucket_sort(uint64_t *sig, const uint64_t *Eb, uint64_t nb, uint64_t e0,
                                                      uint32_t *status) {
-    __shared__ ulonglong2 s[GS_CMAX];
+    constexpr int P2MAX = 1 << (32 - __builtin_clz(GS_CMAX - 1));  // the bitonic sort pads to a power of 2
+    __shared__ ulonglong2 s[P2MAX];
     for (uint64_t b = blockIdx.x; b < nb; b += gridDim.x) {
         const uint64_t lo = (Eb[b] & OFFSET_MASK) - e0, hi = (Eb[b + 1] & OFFSET_MASK) - e0;
         const uint32_t cnt = (uint32_t)(hi - lo);
@@ -205,8 +213,6 @@ struct SolveLdsT {
     static constexpr int CMAX = CMAX_;
     static constexpr int NVMAX = CMAX_ + CMAX_ / 8;  // > vertex_offset span of CMAX keys (281/256)
     static constexpr int WMAX = (CMAX_ + 1 + 63) / 64;
-    // hsys doubles as the FVS selection's reverse CSR (3*CMAX int16 + CMAX u32)
-    static constexpr int HSYS_WORDS = 2 * 6 * 256 > (10 * CMAX_ + 7) / 8 ? 2 * 6 * 256 : (10 * CMAX_ + 7) / 8;
     static_assert(CMAX_ < 32767, "int16 edge indices");
     uint16_t e[3 * CMAX];
     uint32_t deg[NVMAX];
@@ -217,19 +223,25 @@ struct SolveLdsT {
     int16_t vowner[NVMAX];
     uint8_t xval[NVMAX];
     // orientation BFS / Tarjan (not live together)
-    int16_t a0[CMAX], a1[CMAX], a2[CMAX], a3[CMAX];
+    int16_t a1[CMAX], a2[CMAX], a3[CMAX];
+    // one region: the pivot row (Gauss-Jordan), a0, b0 and b1 -- and, during
+    // the FVS selection (none of those live), the u32 pending counts (pend())
+    uint64_t prow[2 * WMAX];
+    int16_t a0[CMAX];
     uint8_t b0[NVMAX], b1[CMAX];
     int16_t dep[3 * CMAX];   // Tarjan: owner of edge k's i-th non-hinge vertex, or -1
     int16_t members[CMAX];   // components, in emission order
     int16_t comp_end[CMAX];  // end (exclusive) of component c in members
     int16_t col_of[CMAX];
-    uint64_t prow[2 * WMAX]; // pivot row
-    uint64_t hsys[HSYS_WORDS]; // a heavy-hinge system of <= 255 unknowns, word-major (stride 256)
     uint32_t ncomp, flag, pivot, rounds, chg, nleft, nscc, qtail;
+    __device__ uint32_t *pend() { return reinterpret_cast<uint32_t *>(prow); }
+    static constexpr size_t PEND_ROOM = sizeof(uint64_t) * 2 * WMAX + 2 * CMAX + NVMAX + CMAX;
+    static_assert(PEND_ROOM >= 4 * (size_t)CMAX, "pending counts fit the pivot-row region");
 };
 using SolveLds = SolveLdsT<GS_CMAX>;
 using SolveBig = SolveLdsT<GB_CMAX>;
 static_assert(SolveLds::NVMAX == GS_NVMAX && SolveLds::WMAX == GS_WMAX, "LDS layout");
+static_assert(sizeof(SolveLds) + 64 <= 160 * 1024 / GS_PER_CU, "GS_PER_CU solver workgroups per CU");
 // per-workgroup global scratch of the dense phase (bit-sliced rows, forms)
 template <class Lds>
 constexpr size_t solve_scratch_words() { return (size_t)2 * Lds::CMAX * Lds::WMAX; }
@@ -746,7 +758,7 @@ __device__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t cnt, uint32_t n
         // rows 2W words apart cost a 64-byte sector per lane).
         auto X = [&](uint32_t rr, uint32_t w, uint32_t q) -> uint64_t & { return scr[(size_t)(2 * w + q) * Lds::CMAX + rr]; };
         uint8_t *colval = L.b0;  // (Tarjan's arrays are dead here)
-        auto HS = [&](uint32_t rr, uint32_t w, uint32_t q) -> uint64_t & { return L.hsys[(2 * w + q) * 256 + rr]; };
+
         // Gauss-Jordan on rows 0..n-1 of X (n equations, n unknowns, the
         // right-hand side in column n), without row swaps: column cc's pivot
         // is the first unused row with a nonzero there (found while column
@@ -872,8 +884,10 @@ __device__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t cnt, uint32_t n
             // member's level is 1 + its dependencies' highest (heavy: 0):
             // the forms are evaluated level by level.
             uint32_t *roff = L.deg;                                        // reverse CSR offsets
-            int16_t *rev = reinterpret_cast<int16_t *>(L.hsys);            // 3 * Lds::CMAX dependents
-            uint32_t *pend = reinterpret_cast<uint32_t *>(L.hsys) + 3 * Lds::CMAX / 2;  // unplaced deps
+            // dependents (3 * CMAX int16) in the workgroup's scratch past the
+            // forms (words [28 CMAX, 29.5 CMAX)); pending counts in LDS
+            int16_t *rev = reinterpret_cast<int16_t *>(scr + (size_t)28 * Lds::CMAX);
+            uint32_t *pend = L.pend();
             int16_t *queue = L.a3;
             for (uint32_t i = tid; i <= sz; i += GS_THREADS) roff[i] = 0;
             if (tid == 0) L.qtail = 0;
@@ -1138,17 +1152,12 @@ __device__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t cnt, uint32_t n
 #pragma unroll
                     for (uint32_t w = 0; w < FW; ++w)
                         if (w < HW) {
-                            if (nH < 256) {
-                                HS(j, w, 0) = a1[w];
-                                HS(j, w, 1) = a2[w];
-                            } else {
-                                X(j, w, 0) = a1[w];
-                                X(j, w, 1) = a2[w];
-                            }
+                            X(j, w, 0) = a1[w];
+                            X(j, w, 1) = a2[w];
                         }
                 }
                 __syncthreads();
-                const bool hok = nH < 256 ? gauss_jordan(nH, HS) : gauss_jordan(nH, X);
+                const bool hok = gauss_jordan(nH, X);  // heavy rows in X: words < 12 CMAX, below the forms
                 pc.lap(GP_FVS_GJ);
                 if (!hok) return false;
                 // evaluate: x_i = forms . (x_heavy, 1)
@@ -1280,7 +1289,7 @@ __device__ void solve_bucket(Lds &L, const SolveArgs &a, uint64_t b, uint64_t *s
     pc.lap(GP_STORE);
 }
 
-__global__ __launch_bounds__(GS_THREADS) void k_gov_solve(SolveArgs a) {
+__global__ __launch_bounds__(GS_THREADS, GS_THREADS * GS_PER_CU / 256) void k_gov_solve(SolveArgs a) {
     __shared__ SolveLds L;
     uint64_t *scr = a.scratch + (size_t)blockIdx.x * solve_scratch_words<SolveLds>();
     PhaseClock pc{a.prof ? a.prof + (size_t)blockIdx.x * GP_N : nullptr, 0};

@@ -15,7 +15,9 @@ import os
 from typing import Optional
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libbsdb_mi355x.so")
+# BSDB_LIB: an alternative in-tree build of the same library (tools/ variant
+# experiments); the default is the product build
+LIB_PATH = os.environ.get("BSDB_LIB") or os.path.join(HERE, "libbsdb_mi355x.so")
 HEADER = os.path.join(os.path.dirname(HERE), "include", "bsdb_mi355x.h")
 
 BSDB_OK = 0
