@@ -214,27 +214,31 @@ struct SolveLdsT {
     static constexpr int NVMAX = CMAX_ + CMAX_ / 8;  // > vertex_offset span of CMAX keys (281/256)
     static constexpr int WMAX = (CMAX_ + 1 + 63) / 64;
     static_assert(CMAX_ < 32767, "int16 edge indices");
-    uint16_t e[3 * CMAX];
-    uint32_t deg[NVMAX];
-    uint32_t xe[NVMAX];
-    uint32_t claim[CMAX];
-    int16_t hinge[CMAX];
-    int16_t round_of[CMAX];
-    int16_t vowner[NVMAX];
-    uint8_t xval[NVMAX];
-    // orientation BFS / Tarjan (not live together)
-    int16_t a1[CMAX], a2[CMAX], a3[CMAX];
     // one region: the pivot row (Gauss-Jordan), a0, b0 and b1 -- and, during
     // the FVS selection (none of those live), the u32 pending counts (pend())
     uint64_t prow[2 * WMAX];
     int16_t a0[CMAX];
     uint8_t b0[NVMAX], b1[CMAX];
+    // another: deg, claim, dep, a1, a3 -- dead once an FVS block's forms are
+    // built, when it holds the heavy system (hs(), word-major)
+    alignas(8) uint32_t deg[NVMAX];
+    uint32_t claim[CMAX];
     int16_t dep[3 * CMAX];   // Tarjan: owner of edge k's i-th non-hinge vertex, or -1
+    int16_t a1[CMAX], a3[CMAX];
+    uint16_t e[3 * CMAX];
+    uint32_t xe[NVMAX];
+    int16_t hinge[CMAX];
+    int16_t round_of[CMAX];
+    int16_t vowner[NVMAX];
+    uint8_t xval[NVMAX];
+    int16_t a2[CMAX];        // (orientation BFS / Tarjan arrays a0-a3 are not live together)
     int16_t members[CMAX];   // components, in emission order
     int16_t comp_end[CMAX];  // end (exclusive) of component c in members
     int16_t col_of[CMAX];
     uint32_t ncomp, flag, pivot, rounds, chg, nleft, nscc, qtail;
     __device__ uint32_t *pend() { return reinterpret_cast<uint32_t *>(prow); }
+    __device__ uint64_t *hs() { return reinterpret_cast<uint64_t *>(deg); }
+    static constexpr size_t HS_WORDS = (4 * (size_t)NVMAX + 4 * CMAX + 6 * CMAX + 2 * CMAX + 2 * CMAX) / 8;
     static constexpr size_t PEND_ROOM = sizeof(uint64_t) * 2 * WMAX + 2 * CMAX + NVMAX + CMAX;
     static_assert(PEND_ROOM >= 4 * (size_t)CMAX, "pending counts fit the pivot-row region");
 };
@@ -382,10 +386,15 @@ __device__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t cnt, uint32_t n
     for (uint32_t v = tid; v < nv; v += GS_THREADS) seen[v] = 0;
     __syncthreads();
     // Greedy: every core edge in increasing order takes its first free
-    // vertex.  Wave 0 reads 64 edges' ownership at once, then resolves them
-    // in edge order in registers: lane j's choice is broadcast and clears that
-    // vertex in the later lanes, which is the sequential outcome.
+    // vertex.  Wave 0 takes 64 edges at once: a lane none of whose vertices
+    // an earlier lane of the chunk touches ("independent") takes its first
+    // free vertex at once (nothing before it in the chunk can change that,
+    // and it touches no vertex of an earlier lane); the others resolve in
+    // edge order in registers after reloading ownership: lane j's choice is
+    // broadcast and clears that vertex in the later lanes.  Together, the
+    // sequential outcome.
     if (tid < 64) {
+        uint32_t *firstl = L.xe;  // (dead after peeling) lowest lane of the chunk touching a vertex
         for (uint32_t k0 = 0; k0 < cnt; k0 += 64) {
             const uint32_t k = k0 + tid;
             const bool act = k < cnt && L.round_of[k] < 0;
@@ -398,23 +407,49 @@ __device__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t cnt, uint32_t n
                 f0 = L.vowner[v0] < 0;
                 f1 = L.vowner[v1] < 0;
                 f2 = L.vowner[v2] < 0;
+                firstl[v0] = 64;
+                firstl[v1] = 64;
+                firstl[v2] = 64;
             }
+            __builtin_amdgcn_wave_barrier();
+            if (act) {
+                atomicMin(&firstl[v0], tid);
+                atomicMin(&firstl[v1], tid);
+                atomicMin(&firstl[v2], tid);
+            }
+            __builtin_amdgcn_wave_barrier();
+            const bool ovl = act && (firstl[v0] < (uint32_t)tid || firstl[v1] < (uint32_t)tid || firstl[v2] < (uint32_t)tid);
             int chosen = -1;
-            uint64_t todo = __builtin_amdgcn_ballot_w64(act);
-            while (todo) {
-                const uint32_t j = (uint32_t)__builtin_ctzll(todo);
-                todo &= todo - 1;
-                if (tid == j) chosen = f0 ? (int)v0 : f1 ? (int)v1 : f2 ? (int)v2 : -1;
-                const int c = __builtin_amdgcn_readlane(chosen, j);
-                if (c >= 0) {
-                    f0 = f0 && v0 != (uint32_t)c;
-                    f1 = f1 && v1 != (uint32_t)c;
-                    f2 = f2 && v2 != (uint32_t)c;
+            if (act && !ovl) {
+                chosen = f0 ? (int)v0 : f1 ? (int)v1 : f2 ? (int)v2 : -1;
+                if (chosen >= 0) {
+                    L.vowner[chosen] = (int16_t)k;
+                    L.hinge[k] = (int16_t)chosen;
                 }
             }
-            if (chosen >= 0) {
-                L.vowner[chosen] = (int16_t)k;
-                L.hinge[k] = (int16_t)chosen;
+            uint64_t todo = __builtin_amdgcn_ballot_w64(ovl);
+            if (todo) {  // (wave-uniform)
+                __builtin_amdgcn_wave_barrier();
+                if (ovl) {  // the independent lanes' choices (all earlier, see above)
+                    f0 = L.vowner[v0] < 0;
+                    f1 = L.vowner[v1] < 0;
+                    f2 = L.vowner[v2] < 0;
+                }
+                while (todo) {
+                    const uint32_t j = (uint32_t)__builtin_ctzll(todo);
+                    todo &= todo - 1;
+                    if (tid == j) chosen = f0 ? (int)v0 : f1 ? (int)v1 : f2 ? (int)v2 : -1;
+                    const int c = __builtin_amdgcn_readlane(chosen, j);
+                    if (c >= 0) {
+                        f0 = f0 && v0 != (uint32_t)c;
+                        f1 = f1 && v1 != (uint32_t)c;
+                        f2 = f2 && v2 != (uint32_t)c;
+                    }
+                }
+                if (ovl && chosen >= 0) {
+                    L.vowner[chosen] = (int16_t)k;
+                    L.hinge[k] = (int16_t)chosen;
+                }
             }
             __builtin_amdgcn_wave_barrier();
         }
@@ -434,8 +469,20 @@ __device__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t cnt, uint32_t n
         uint32_t epoch = 0, ok = 1, nbfs = 0, npops = 0, ncore = 0;
         if (pc.acc)
             for (uint32_t k = 0; k < cnt; ++k) ncore += L.round_of[k] < 0;
-        for (uint32_t k0 = 0; k0 < cnt && ok; ++k0) {
-            if (L.round_of[k0] >= 0 || L.hinge[k0] >= 0) continue;  // wave-uniform
+        // unmatched core edges, 64 at a time by ballot (a BFS only matches its
+        // own root: the path it flips runs through matched edges, so the
+        // chunk's mask stays exact while its edges are taken in order)
+        uint64_t pendm = 0;
+        uint32_t base = 0;
+        for (;;) {
+            while (!pendm && base < cnt) {
+                const uint32_t k = base + lane;
+                pendm = __builtin_amdgcn_ballot_w64(k < cnt && L.round_of[k] < 0 && L.hinge[k] < 0);
+                base += 64;
+            }
+            if (!pendm || !ok) break;
+            const uint32_t k0 = base - 64 + (uint32_t)__builtin_ctzll(pendm);
+            pendm &= pendm - 1;
             ++epoch;
             ++nbfs;
             if (lane == 0) {
@@ -1129,7 +1176,11 @@ __device__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t cnt, uint32_t n
                     __syncthreads();
                 }
                 pc.lap(GP_FVS_FORMS);
-                // the heavy members' equations: cf*x_j + forms = h
+                // the heavy members' equations: cf*x_j + forms = h, in LDS
+                // (the forms' selection arrays are dead now) when they fit
+                const bool hs_lds = (size_t)2 * HW * nH <= Lds::HS_WORDS;
+                uint64_t *const hsb = L.hs();
+                auto HSL = [&](uint32_t rr, uint32_t w, uint32_t q) -> uint64_t & { return hsb[(2 * w + q) * nH + rr]; };
                 for (uint32_t i = tid; i < sz; i += GS_THREADS) {
                     if (st[i] != 2) continue;
                     const uint32_t k = (uint32_t)L.members[beg + i], j = (uint32_t)hid[i];
@@ -1152,12 +1203,18 @@ __device__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t cnt, uint32_t n
 #pragma unroll
                     for (uint32_t w = 0; w < FW; ++w)
                         if (w < HW) {
-                            X(j, w, 0) = a1[w];
-                            X(j, w, 1) = a2[w];
+                            if (hs_lds) {
+                                HSL(j, w, 0) = a1[w];
+                                HSL(j, w, 1) = a2[w];
+                            } else {
+                                X(j, w, 0) = a1[w];
+                                X(j, w, 1) = a2[w];
+                            }
                         }
                 }
                 __syncthreads();
-                const bool hok = gauss_jordan(nH, X);  // heavy rows in X: words < 12 CMAX, below the forms
+                // (rows in X: words < 12 CMAX, below the forms)
+                const bool hok = hs_lds ? gauss_jordan(nH, HSL) : gauss_jordan(nH, X);
                 pc.lap(GP_FVS_GJ);
                 if (!hok) return false;
                 // evaluate: x_i = forms . (x_heavy, 1)
