@@ -236,6 +236,7 @@ struct SolveLdsT {
     int16_t comp_end[CMAX];  // end (exclusive) of component c in members
     int16_t col_of[CMAX];
     uint32_t ncomp, flag, pivot, rounds, chg, nleft, nscc, qtail;
+    uint32_t hbin[64];       // FVS selection: open members per in-degree
     __device__ uint32_t *pend() { return reinterpret_cast<uint32_t *>(prow); }
     __device__ uint64_t *hs() { return reinterpret_cast<uint64_t *>(deg); }
     static constexpr size_t HS_WORDS = (4 * (size_t)NVMAX + 4 * CMAX + 6 * CMAX + 2 * CMAX + 2 * CMAX) / 8;
@@ -1009,10 +1010,64 @@ __device__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t cnt, uint32_t n
                         fb = true;
                         break;
                     }
-                    // (loads issued 8 at a time before any is used).  The two
-                    // best candidates turn heavy at once: any feedback vertex
-                    // set gives the same unique solution (and is singular
-                    // exactly when the block is); half the stuck cascades.
+                    // The next heavy hinges: the `want` open members of the
+                    // largest key (in-degree, then lowest index) -- the set
+                    // GOV_PICK_REPS rounds of "the best two" (the loop
+                    // below) pick, as nothing is placed between those rounds:
+                    // any feedback vertex set gives the same unique solution
+                    // and is singular exactly when the block is.  One sweep
+                    // bins the open members by in-degree (64 bins), a second
+                    // takes every member above the threshold bin and the
+                    // lowest-index ones of that bin.
+                    const uint32_t want = 2 * min((uint32_t)GOV_PICK_REPS, (fvs_max - nh) / 2);
+                    uint32_t *hb = L.hbin;
+                    hb[lane] = 0;
+                    __builtin_amdgcn_wave_barrier();
+                    for (uint32_t i0 = 0; i0 < sz; i0 += 64) {
+                        const uint32_t i = i0 + lane;
+                        if (i < sz && st[i] == 0) atomicAdd(&hb[min(indeg[i], 63u)], 1u);
+                    }
+                    __builtin_amdgcn_wave_barrier();
+                    uint32_t suf = hb[lane];  // -> open members of in-degree >= lane
+#pragma unroll
+                    for (int d = 1; d < 64; d <<= 1) {
+                        const uint32_t y = (uint32_t)__shfl_down((int)suf, d, 64);
+                        if (lane + d < 64) suf += y;
+                    }
+                    const uint64_t okm = __builtin_amdgcn_ballot_w64(suf >= want);
+                    const uint32_t T = okm ? 63u - (uint32_t)__builtin_clzll(okm) : 0u;
+                    const uint32_t above = T < 63 ? (uint32_t)__builtin_amdgcn_readlane((int)suf, (int)T + 1) : 0u;
+                    const uint32_t in_t = (uint32_t)__builtin_amdgcn_readlane((int)suf, (int)T) - above;
+                    const uint32_t take_t = okm ? want - above : in_t;  // (fewer open members than want: all)
+                    if (T < 63) {
+                        uint32_t run = 0, got = 0;
+                        for (uint32_t i0 = 0; i0 < sz; i0 += 64) {
+                            const uint32_t i = i0 + lane;
+                            const bool open = i < sz && st[i] == 0;
+                            const uint32_t dvc = open ? min(indeg[i], 63u) : 0u;
+                            const bool eq = open && dvc == T;
+                            const uint64_t em = __builtin_amdgcn_ballot_w64(eq);
+                            const uint32_t r = run + __builtin_amdgcn_mbcnt_hi((uint32_t)(em >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)em, 0u));
+                            const bool sel = (open && dvc > T) || (eq && r < take_t);
+                            run += (uint32_t)__builtin_popcountll(em);
+                            const uint64_t sm = __builtin_amdgcn_ballot_w64(sel);
+                            if (sel) {
+                                const uint32_t pos = got + __builtin_amdgcn_mbcnt_hi((uint32_t)(sm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)sm, 0u));
+                                st[i] = 2;
+                                hid[i] = (int16_t)(nh + pos);
+                                rnd[i] = 0;
+                                queue[qt + pos] = (int16_t)i;
+                            }
+                            got += (uint32_t)__builtin_popcountll(sm);
+                        }
+                        nh += got;
+                        qt += got;
+                        if (lane == 0) L.qtail = qt;
+                        __builtin_amdgcn_wave_barrier();
+                        continue;
+                    }
+                    // (64+ open members of in-degree >= 63 reach the
+                    // threshold: the exact rounds, loads issued 8 at a time)
                     for (int rep = 0; rep < GOV_PICK_REPS && nh + 2 <= fvs_max; ++rep) {
                         uint32_t key = 0, key2 = 0;
                         for (uint32_t q0 = 0; q0 * 64 < sz; q0 += 8) {
