@@ -69,9 +69,9 @@ def cpu_baseline(m: int, target_s: float, threads: int):
 
 def full_build_gpu(ctx, n: int, width: int, reps: int):
     """Full build on the device, keys resident in HBM: hash -> GOV build
-    (bucket sort, per-bucket solve, sign with `width` checksum bits) ->
-    getLong of every key -> index scatter (W:129-145).  keys/s over the
-    median run, per-stage device time."""
+    (bucket sort, per-bucket solve that also signs with `width` checksum bits
+    and returns every key's rank, F2) -> index scatter of the record
+    addresses (W:129-145).  keys/s over the median run, per-stage device time."""
     import torch
     keys = ctx.gen_keys13(0, n)
     addr = torch.arange(n, dtype=torch.int64, device="cuda")
@@ -82,9 +82,8 @@ def full_build_gpu(ctx, n: int, width: int, reps: int):
         ev[0].record()
         sig = ctx.hash_fixed(keys, 13)
         ev[1].record()
-        E, vals, sb = ctx.gov_build(sig, width)
+        E, vals, sb, rank = ctx.gov_build_ranks(sig, width)
         ev[2].record()
-        rank = ctx.lookup(sig, n, E, vals, width, sb, check=True)
         ctx.index_scatter(rank, addr, 0, n, index)
         ev[3].record()
         torch.cuda.synchronize()
@@ -96,7 +95,7 @@ def full_build_gpu(ctx, n: int, width: int, reps: int):
     del keys, addr, index
     torch.cuda.empty_cache()
     return {"n_keys": n, "checksum_bits": width, "keys_per_s": n / (total / 1e3), "ms": total,
-            "stage_ms": {"hash": hash_ms, "gov_build_sort_solve_sign": gov_ms, "lookup_index_scatter": index_ms}}
+            "stage_ms": {"hash": hash_ms, "gov_build_sort_solve_sign_rank": gov_ms, "index_scatter": index_ms}}
 
 
 def full_build_cpu(n: int, width: int, threads: int):

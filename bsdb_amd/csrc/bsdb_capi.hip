@@ -68,6 +68,8 @@ struct bsdb_ctx {
     size_t g_sorted_bytes = 0, g_counts_bytes = 0, g_cursor_bytes = 0, g_scratch_bytes = 0, g_status_bytes = 0;
     void *g_big = nullptr, *g_slabs = nullptr;  // oversized buckets: list, sort + solver slabs
     size_t g_big_bytes = 0, g_slabs_bytes = 0;
+    void *g_pay = nullptr;  // F2: input position of each sorted signature
+    size_t g_pay_bytes = 0;
     bool verify = false;
     // ordering of workspace use across streams: the last call's
     // completion event and stream
@@ -552,6 +554,7 @@ int bsdb_close(bsdb_ctx *c) {
     (void)hipFree(c->g_scratch);
     (void)hipFree(c->g_status);
     (void)hipFree(c->g_big);
+    (void)hipFree(c->g_pay);
     (void)hipFree(c->g_slabs);
     (void)hipFree(c->pack);
     comm_destroy(c);
@@ -754,9 +757,11 @@ struct DevFree {
 // n_global keys; d_sig = the n_local signatures of that range.  full: a whole
 // build (zeroes the outputs first); otherwise the caller zeroed full-size
 // outputs and E[b_hi] is cleared again unless b_hi == m (the next range owns it).
+// d_rank (optional, F2): the rank of input signature i at d_rank[i], from the
+// solve itself (n_local < 2^32).
 static int gov_build_impl(bsdb_ctx *c, const uint64_t *d_sig, uint64_t n_local, uint64_t n_global, uint64_t b_lo,
                           uint64_t b_hi, uint64_t e_lo, uint32_t width, uint64_t *d_E, uint64_t *d_values,
-                          uint64_t *d_sigbits, hipStream_t s, bool full) {
+                          uint64_t *d_sigbits, int64_t *d_rank, hipStream_t s, bool full) {
     const uint64_t m = n_global / BUCKET_SIZE + 1, nb = b_hi - b_lo;
     const uint32_t mult = (uint32_t)(2 * m);
     int rc;
@@ -764,6 +769,12 @@ static int gov_build_impl(bsdb_ctx *c, const uint64_t *d_sig, uint64_t n_local, 
     if ((rc = grow(&c->g_counts, &c->g_counts_bytes, std::max<uint64_t>(nb, 1) * 4))) return rc;
     if ((rc = grow(&c->g_cursor, &c->g_cursor_bytes, std::max<uint64_t>(nb, 1) * 8))) return rc;
     if ((rc = grow(&c->g_status, &c->g_status_bytes, 16))) return rc;
+    if (d_rank && n_local >= (1ULL << 32)) return BSDB_EINVAL;
+    uint32_t *pay = nullptr;
+    if (d_rank) {
+        if ((rc = grow(&c->g_pay, &c->g_pay_bytes, std::max<uint64_t>(n_local, 1) * 4))) return rc;
+        pay = (uint32_t *)c->g_pay;
+    }
     const uint32_t big_cap = (uint32_t)(n_local / (GS_CMAX + 1) + 1);
     if ((rc = grow(&c->g_big, &c->g_big_bytes, (size_t)big_cap * 4))) return rc;
     const uint32_t solve_grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(nb, (uint64_t)c->num_cus * GS_PER_CU));
@@ -782,9 +793,9 @@ static int gov_build_impl(bsdb_ctx *c, const uint64_t *d_sig, uint64_t n_local, 
     k_cursor_init<<<grid_for(c, nb), 256, 0, s>>>(Eb, nb, e_lo, (uint64_t *)c->g_cursor);
     if (n_local)
         k_bucket_scatter<<<grid, 256, 0, s>>>(d_sig, n_local, mult, (uint32_t)b_lo, (unsigned long long *)c->g_cursor,
-                                              sorted);
+                                              sorted, pay);
     k_bucket_sort<<<(uint32_t)std::min<uint64_t>(nb, (uint64_t)c->num_cus * 8), 256, 0, s>>>(sorted, Eb, nb, e_lo,
-                                                                                              status);  // A5
+                                                                                              status, pay);  // A5
     k_big_list<<<grid_for(c, nb), 256, 0, s>>>(Eb, nb, status, (uint32_t *)c->g_big, big_cap);
     if ((rc = launch_status())) return rc;
     uint32_t st[4] = {0, 0, 0, 0};
@@ -796,11 +807,11 @@ static int gov_build_impl(bsdb_ctx *c, const uint64_t *d_sig, uint64_t n_local, 
     const uint32_t big_grid = std::min<uint32_t>(nbig, 8);
     if (nbig) {
         // oversized buckets: per-workgroup slabs for the sort, then the solver
-        const size_t sort_bytes = (size_t)big_grid * GB_CMAX * 16;
+        const size_t sort_bytes = (size_t)big_grid * GB_CMAX * (16 + 4);  // signatures + payloads
         if ((rc = grow(&c->g_slabs, &c->g_slabs_bytes, std::max(sort_bytes, (size_t)big_grid * big_slab_bytes()))))
             return rc;
         k_bucket_sort_big<<<big_grid, GB_THREADS, 0, s>>>(sorted, Eb, e_lo, (const uint32_t *)c->g_big, nbig,
-                                                          (ulonglong2 *)c->g_slabs, status);
+                                                          (ulonglong2 *)c->g_slabs, status, pay);
     }
     // BSDB_GOV_PROFILE=1: per-phase cycle totals of the solver printed to stderr
     const bool gprof = getenv("BSDB_GOV_PROFILE") != nullptr;
@@ -815,7 +826,10 @@ static int gov_build_impl(bsdb_ctx *c, const uint64_t *d_sig, uint64_t n_local, 
     }
     uint32_t fvs_max = FVS_NH_MAX;
     if (const char *v = getenv("BSDB_GOV_FVS_MAX")) fvs_max = (uint32_t)std::max(2, std::min(atoi(v), (int)FVS_NH_MAX));
-    SolveArgs sa{sorted, b_hi, d_E, d_values, (uint64_t *)c->g_scratch, status, d_prof, fvs_max, b_lo, e_lo};
+    if (width && full) HIP_OK(hipMemsetAsync(d_sigbits, 0, ((n_global * width + 63) / 64 + 1) * 8, s));
+    // A8, with A11 (checksum bits at each rank) and F2 (ranks) in the solve
+    SolveArgs sa{sorted, b_hi, d_E, d_values, (uint64_t *)c->g_scratch, status, d_prof, fvs_max, b_lo, e_lo,
+                 d_sigbits, width, pay, d_rank};
     // zeroing status[2] (the bucket queue) above happens before both launches
     k_gov_solve<<<solve_grid, GS_THREADS, 0, s>>>(sa);  // A8
     if (nbig)
@@ -831,10 +845,6 @@ static int gov_build_impl(bsdb_ctx *c, const uint64_t *d_sig, uint64_t n_local, 
         print_gov_profile(h, solve_grid, m);
     }
     const MphView v{d_E, d_values, nullptr, n_global, mult, width};
-    if (width) {
-        if (full) HIP_OK(hipMemsetAsync(d_sigbits, 0, ((n_global * width + 63) / 64 + 1) * 8, s));
-        if (n_local) k_sign<<<grid, 256, 0, s>>>(v, sorted, n_local, d_sigbits);  // A11
-    }
     if (c->verify && n_local) {
         void *p = nullptr;
         HIP_OK(hipMalloc(&p, ((n_local + 63) / 64) * 8));
@@ -864,12 +874,25 @@ int bsdb_dev_gov_build(bsdb_ctx *c, const uint64_t *d_sig, uint64_t n, uint32_t 
     HIP_OK(hipSetDevice(c->device));
     hipStream_t s = pick(c, stream);
     Ordered ord(c, s);
-    return gov_build_impl(c, d_sig, n, n, 0, m, 0, width, d_E, d_values, d_sigbits, s, true);
+    return gov_build_impl(c, d_sig, n, n, 0, m, 0, width, d_E, d_values, d_sigbits, nullptr, s, true);
+}
+
+int bsdb_dev_gov_build_ranks(bsdb_ctx *c, const uint64_t *d_sig, uint64_t n, uint32_t width, uint64_t *d_E,
+                             uint64_t *d_values, uint64_t *d_sigbits, int64_t *d_rank, void *stream) {
+    const uint64_t m = n / BUCKET_SIZE + 1;
+    if (!c || width > 64 || !d_E || !d_values || (n && (!d_sig || !d_rank)) || (width && !d_sigbits) ||
+        !aligned16(d_sig) || m > 0x7FFFFFFFULL || n >= (1ULL << 32))
+        return BSDB_EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    HIP_OK(hipSetDevice(c->device));
+    hipStream_t s = pick(c, stream);
+    Ordered ord(c, s);
+    return gov_build_impl(c, d_sig, n, n, 0, m, 0, width, d_E, d_values, d_sigbits, d_rank, s, true);
 }
 
 int bsdb_dev_gov_build_range(bsdb_ctx *c, const uint64_t *d_sig, uint64_t n_local, uint64_t n_global, uint64_t b_lo,
                              uint64_t b_hi, uint64_t e_lo, uint32_t width, uint64_t *d_E, uint64_t *d_values,
-                             uint64_t *d_sigbits, void *stream) {
+                             uint64_t *d_sigbits, int64_t *d_rank, void *stream) {
     const uint64_t m = n_global / BUCKET_SIZE + 1;
     if (!c || width > 64 || !d_E || !d_values || (n_local && !d_sig) || (width && !d_sigbits) || !aligned16(d_sig) ||
         m > 0x7FFFFFFFULL || b_lo >= b_hi || b_hi > m || n_local > n_global || e_lo + n_local > n_global)
@@ -878,7 +901,9 @@ int bsdb_dev_gov_build_range(bsdb_ctx *c, const uint64_t *d_sig, uint64_t n_loca
     HIP_OK(hipSetDevice(c->device));
     hipStream_t s = pick(c, stream);
     Ordered ord(c, s);
-    return gov_build_impl(c, d_sig, n_local, n_global, b_lo, b_hi, e_lo, width, d_E, d_values, d_sigbits, s, false);
+    if (d_rank && n_local >= (1ULL << 32)) return BSDB_EINVAL;
+    return gov_build_impl(c, d_sig, n_local, n_global, b_lo, b_hi, e_lo, width, d_E, d_values, d_sigbits, d_rank, s,
+                          false);
 }
 
 int bsdb_dev_partition_owners(bsdb_ctx *c, const uint64_t *d_sig, const uint64_t *d_payload, uint64_t n, uint64_t m,

@@ -70,8 +70,8 @@ int mph_build(bsdb_ctx *c, uint64_t n, uint32_t width, bsdb_mph **out, HashDev &
     }
     std::unique_ptr<void, DevFree> sig_guard(sig);
     if ((rc = hash_dev((uint64_t *)sig)) ||
-        (rc = gov_build_impl(c, (const uint64_t *)sig, n, n, 0, p->m, 0, width, p->E, p->values, p->sigbits, c->stream,
-                             true))) {
+        (rc = gov_build_impl(c, (const uint64_t *)sig, n, n, 0, p->m, 0, width, p->E, p->values, p->sigbits, nullptr,
+                             c->stream, true))) {
         (void)hipStreamSynchronize(c->stream);
         mph_release(p);
         return rc;

@@ -77,13 +77,16 @@ __global__ __launch_bounds__(256) void k_cursor_init(const uint64_t *Eb, uint64_
     for (uint64_t b = (uint64_t)blockIdx.x * 256 + threadIdx.x; b < nb; b += stride) cursor[b] = (Eb[b] & OFFSET_MASK) - e0;
 }
 
+// pay_out (optional): the input position of each sorted signature (F2: the
+// solver then writes each input's rank without a lookup pass)
 __global__ __launch_bounds__(256) void k_bucket_scatter(const uint64_t *sig, uint64_t n, uint32_t mult, uint32_t b0,
-                                                        unsigned long long *cursor, uint64_t *out) {
+                                                        unsigned long long *cursor, uint64_t *out, uint32_t *pay_out) {
     const uint64_t stride = (uint64_t)gridDim.x * 256;
     for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
         const ulonglong2 s = reinterpret_cast<const ulonglong2 *>(sig)[i];
         const uint64_t pos = atomicAdd(cursor + (bucket_of_w(w64(s.x), mult) - b0), 1ULL);
         reinterpret_cast<ulonglong2 *>(out)[pos] = s;
+        if (pay_out) pay_out[pos] = (uint32_t)i;
     }
 }
 
@@ -92,9 +95,10 @@ __device__ __forceinline__ bool sig_less(ulonglong2 a, ulonglong2 b) { return a.
 // Bitonic sort of one bucket in LDS (padded with all-ones sentinels) +
 // duplicate check on neighbours (CBHS:969-972).
 __global__ __launch_bounds__(256) void k_bucket_sort(uint64_t *sig, const uint64_t *Eb, uint64_t nb, uint64_t e0,
-                                                     uint32_t *status) {
+                                                     uint32_t *status, uint32_t *pay) {
     constexpr int P2MAX = 1 << (32 - __builtin_clz(GS_CMAX - 1));  // the bitonic sort pads to a power of 2
     __shared__ ulonglong2 s[P2MAX];
+    __shared__ uint32_t sp[P2MAX];  // payloads (pay != nullptr), moved with their signatures
     for (uint64_t b = blockIdx.x; b < nb; b += gridDim.x) {
         const uint64_t lo = (Eb[b] & OFFSET_MASK) - e0, hi = (Eb[b + 1] & OFFSET_MASK) - e0;
         const uint32_t cnt = (uint32_t)(hi - lo);
@@ -103,7 +107,10 @@ __global__ __launch_bounds__(256) void k_bucket_sort(uint64_t *sig, const uint64
         while (p2 < cnt) p2 <<= 1;
         ulonglong2 *g = reinterpret_cast<ulonglong2 *>(sig) + lo;
         __syncthreads();
-        for (uint32_t i = threadIdx.x; i < p2; i += 256) s[i] = i < cnt ? g[i] : make_ulonglong2(~0ULL, ~0ULL);
+        for (uint32_t i = threadIdx.x; i < p2; i += 256) {
+            s[i] = i < cnt ? g[i] : make_ulonglong2(~0ULL, ~0ULL);
+            if (pay) sp[i] = i < cnt ? pay[lo + i] : 0u;
+        }
         __syncthreads();
         for (uint32_t k = 2; k <= p2; k <<= 1) {
             for (uint32_t j = k >> 1; j > 0; j >>= 1) {
@@ -115,6 +122,11 @@ __global__ __launch_bounds__(256) void k_bucket_sort(uint64_t *sig, const uint64
                         if (up ? sig_less(c, a) : sig_less(a, c)) {
                             s[i] = c;
                             s[l] = a;
+                            if (pay) {
+                                const uint32_t t = sp[i];
+                                sp[i] = sp[l];
+                                sp[l] = t;
+                            }
                         }
                     }
                 }
@@ -124,6 +136,7 @@ __global__ __launch_bounds__(256) void k_bucket_sort(uint64_t *sig, const uint64
         bool dup = false;
         for (uint32_t i = threadIdx.x; i < cnt; i += 256) {
             g[i] = s[i];
+            if (pay) pay[lo + i] = sp[i];
             if (i && s[i].x == s[i - 1].x && s[i].y == s[i - 1].y) dup = true;
         }
         if (dup) atomicOr(status, (uint32_t)GOV_DUP);
@@ -151,8 +164,9 @@ __global__ __launch_bounds__(256) void k_big_list(const uint64_t *Eb, uint64_t n
 // a per-workgroup global slab of GB_CMAX entries (padded with sentinels).
 __global__ __launch_bounds__(GB_THREADS) void k_bucket_sort_big(uint64_t *sig, const uint64_t *Eb, uint64_t e0,
                                                                 const uint32_t *list, uint32_t nbig, ulonglong2 *slab,
-                                                                uint32_t *status) {
+                                                                uint32_t *status, uint32_t *pay) {
     ulonglong2 *s = slab + (size_t)blockIdx.x * GB_CMAX;
+    uint32_t *sp = reinterpret_cast<uint32_t *>(slab + (size_t)gridDim.x * GB_CMAX) + (size_t)blockIdx.x * GB_CMAX;
     for (uint32_t li = blockIdx.x; li < nbig; li += gridDim.x) {
         const uint32_t b = list[li];
         const uint64_t lo = (Eb[b] & OFFSET_MASK) - e0, hi = (Eb[b + 1] & OFFSET_MASK) - e0;
@@ -161,7 +175,10 @@ __global__ __launch_bounds__(GB_THREADS) void k_bucket_sort_big(uint64_t *sig, c
         while (p2 < cnt) p2 <<= 1;
         ulonglong2 *g = reinterpret_cast<ulonglong2 *>(sig) + lo;
         __syncthreads();
-        for (uint32_t i = threadIdx.x; i < p2; i += GB_THREADS) s[i] = i < cnt ? g[i] : make_ulonglong2(~0ULL, ~0ULL);
+        for (uint32_t i = threadIdx.x; i < p2; i += GB_THREADS) {
+            s[i] = i < cnt ? g[i] : make_ulonglong2(~0ULL, ~0ULL);
+            if (pay) sp[i] = i < cnt ? pay[lo + i] : 0u;
+        }
         __syncthreads();
         for (uint32_t k = 2; k <= p2; k <<= 1) {
             for (uint32_t j = k >> 1; j > 0; j >>= 1) {
@@ -173,6 +190,11 @@ __global__ __launch_bounds__(GB_THREADS) void k_bucket_sort_big(uint64_t *sig, c
                         if (up ? sig_less(c, a) : sig_less(a, c)) {
                             s[i] = c;
                             s[l] = a;
+                            if (pay) {
+                                const uint32_t t = sp[i];
+                                sp[i] = sp[l];
+                                sp[l] = t;
+                            }
                         }
                     }
                 }
@@ -182,6 +204,7 @@ __global__ __launch_bounds__(GB_THREADS) void k_bucket_sort_big(uint64_t *sig, c
         bool dup = false;
         for (uint32_t i = threadIdx.x; i < cnt; i += GB_THREADS) {
             g[i] = s[i];
+            if (pay) pay[lo + i] = sp[i];
             if (i && s[i].x == s[i - 1].x && s[i].y == s[i - 1].y) dup = true;
         }
         if (dup) atomicOr(status, (uint32_t)GOV_DUP);
@@ -199,6 +222,13 @@ struct SolveArgs {
     uint64_t *prof;       // optional per-workgroup phase cycle counters [grid][GP_N] (BSDB_GOV_PROFILE)
     uint32_t fvs_max;     // heavy-set limit, <= FVS_NH_MAX
     uint64_t b0, e0;      // first bucket of the range, keys before it
+    // A11 + F2, fused into the solve: each key's rank is E[b] + the hinge
+    // vertices before its hinge (exactly the lookup's count of nonzero
+    // 2-bit values, GOV:557-580, as those sit at the hinges)
+    uint64_t *sigbits;    // checksum bit list (width > 0): sig0 & mask at each rank (GOV:492-508)
+    uint32_t width;
+    const uint32_t *pay;  // input position of each sorted signature (rank_out only)
+    int64_t *rank_out;    // optional: rank of input signature i at [i]
 };
 
 // phase counters (cycles, or counts for the GP_N_* slots)
@@ -1397,6 +1427,26 @@ __device__ void solve_bucket(Lds &L, const SolveArgs &a, uint64_t b, uint64_t *s
         else if (word) atomicOr((unsigned long long *)(a.values + w), (unsigned long long)word);
     }
     if (threadIdx.x == 0) a.E[b] |= (uint64_t)j << 56;
+    if (a.width || a.rank_out) {
+        uint32_t *pre = L.deg;  // (dead after the solve) hinge vertices before v
+        for (uint32_t v = threadIdx.x; v < nv; v += GS_THREADS) pre[v] = L.vowner[v] >= 0 ? 1u : 0u;
+        __syncthreads();
+        wg_excl_scan3(pre, nv, L.xe + Lds::CMAX);
+        const uint64_t mask = a.width == 64 ? ~0ULL : ((1ULL << a.width) - 1);
+        for (uint32_t k = threadIdx.x; k < cnt; k += GS_THREADS) {
+            const uint64_t r = lo + pre[L.hinge[k]];
+            if (a.rank_out) a.rank_out[a.pay[lo - a.e0 + k]] = (int64_t)r;
+            if (a.width) {
+                const uint64_t val = sig[k].x & mask, bit = r * a.width, word = bit >> 6;
+                const uint32_t off = (uint32_t)(bit & 63);
+                if (val) {
+                    atomicOr((unsigned long long *)(a.sigbits + word), (unsigned long long)(val << off));
+                    if (off + a.width > 64)
+                        atomicOr((unsigned long long *)(a.sigbits + word + 1), (unsigned long long)(val >> (64 - off)));
+                }
+            }
+        }
+    }
     __syncthreads();
     pc.lap(GP_STORE);
 }

@@ -72,13 +72,15 @@ class DeviceBuild:
         return self.ctx.partition_owners(sig, m, world, payload=addr)
 
     def build_range(self, sig, n_global, b_lo, b_hi, e_lo, width, E, values, sigbits):
-        self.ctx.gov_build_range(sig, n_global, b_lo, b_hi, e_lo, width, E, values, sigbits)
+        """The range build; the solve also returns every key's rank (F2)."""
+        self._rank = self.zeros(sig.shape[0])
+        self.ctx.gov_build_range(sig, n_global, b_lo, b_hi, e_lo, width, E, values, sigbits, rank=self._rank)
 
     def index_slice(self, sig, addr, n_global, E, values, width, sigbits, e_lo, n_local):
-        """The big-endian index slots [e_lo, e_lo + n_local) of these records."""
-        rank = self.ctx.lookup(sig, n_global, E, values, width, sigbits, check=True)
+        """The big-endian index slots [e_lo, e_lo + n_local) of these records,
+        placed by the ranks the solve returned (no lookup pass)."""
         out = self.zeros(n_local)
-        self.ctx.index_scatter(rank, addr, e_lo, n_local, out)
+        self.ctx.index_scatter(self._rank, addr, e_lo, n_local, out)
         return out
 
 

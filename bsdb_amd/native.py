@@ -43,7 +43,8 @@ SIGNATURES = [
     ("bsdb_dev_index_scatter", _i, [_vp, _vp, _vp, _u64, _u64, _u64, _vp, _vp, _vp, _vp, _vp]),
     ("bsdb_values_words", _u64, [_u64]),
     ("bsdb_dev_gov_build", _i, [_vp, _vp, _u64, _u32, _vp, _vp, _vp, _vp]),
-    ("bsdb_dev_gov_build_range", _i, [_vp, _vp, _u64, _u64, _u64, _u64, _u64, _u32, _vp, _vp, _vp, _vp]),
+    ("bsdb_dev_gov_build_ranks", _i, [_vp, _vp, _u64, _u32, _vp, _vp, _vp, _vp, _vp]),
+    ("bsdb_dev_gov_build_range", _i, [_vp, _vp, _u64, _u64, _u64, _u64, _u64, _u32, _vp, _vp, _vp, _vp, _vp]),
     ("bsdb_dev_partition_owners", _i, [_vp, _vp, _vp, _u64, _u64, _i, _vp, _vp, _vp, _vp]),
     ("bsdb_set_verify", _i, [_vp, _i]),
     ("bsdb_set_histogram_mode", _i, [_vp, _i]),
@@ -252,12 +253,27 @@ class Context:
             _stream(stream)))
         return E, values, sigbits
 
+    def gov_build_ranks(self, sig, width: int, stream=None):
+        """F2: (E, values, sigbits, rank) -- rank[i] = getLong of sig[i], from the solve."""
+        import torch
+        n = sig.shape[0]
+        m = n // 1500 + 1
+        E = torch.empty(m + 1, dtype=torch.int64, device=sig.device)
+        values = torch.empty(int(lib().bsdb_values_words(n)), dtype=torch.int64, device=sig.device)
+        sigbits = torch.empty((n * width + 63) // 64 + 1, dtype=torch.int64, device=sig.device) if width else None
+        rank = torch.empty(max(n, 1), dtype=torch.int64, device=sig.device)[:n]
+        _check("bsdb_dev_gov_build_ranks", lib().bsdb_dev_gov_build_ranks(
+            self._h, _ptr(sig), n, width, _ptr(E), _ptr(values), _ptr(sigbits) if sigbits is not None else None,
+            _ptr(rank), _stream(stream)))
+        return E, values, sigbits, rank
+
     def gov_build_range(self, sig, n_global: int, b_lo: int, b_hi: int, e_lo: int, width: int, E, values, sigbits=None,
-                        stream=None):
-        """E4: one rank's bucket range [b_lo, b_hi) into FULL-size zeroed arrays."""
+                        rank=None, stream=None):
+        """E4: one rank's bucket range [b_lo, b_hi) into FULL-size zeroed arrays
+        (rank: optional, the global rank of each local signature)."""
         _check("bsdb_dev_gov_build_range", lib().bsdb_dev_gov_build_range(
             self._h, _ptr(sig), sig.shape[0], n_global, b_lo, b_hi, e_lo, width, _ptr(E), _ptr(values),
-            _ptr(sigbits) if sigbits is not None else None, _stream(stream)))
+            _ptr(sigbits) if sigbits is not None else None, _ptr(rank) if rank is not None else None, _stream(stream)))
 
     def partition_owners(self, sig, m: int, nranks: int, payload=None, stream=None):
         """Signatures (and one int64 payload per key) grouped by owning rank

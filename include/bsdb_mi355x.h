@@ -144,6 +144,13 @@ uint64_t bsdb_values_words(uint64_t n);
 int bsdb_dev_gov_build(bsdb_ctx *ctx, const uint64_t *d_sig, uint64_t n, uint32_t width, uint64_t *d_E,
                        uint64_t *d_values, uint64_t *d_sigbits, void *stream);
 
+/* F2: the same build, also returning d_rank[i] = the rank (getLong) of d_sig[i],
+ * computed inside the solve (E[b] + the hinge vertices before the key's hinge:
+ * the lookup's nonzero-pair count, GOV:557-580) -- no lookup pass over the
+ * keys is needed to place records in index.db (W:129-145).  n < 2^32.  The
+ * checksum bits are always signed this way (A11 fused into the solve). */
+int bsdb_dev_gov_build_ranks(bsdb_ctx *ctx, const uint64_t *d_sig, uint64_t n, uint32_t width, uint64_t *d_E,
+                             uint64_t *d_values, uint64_t *d_sigbits, int64_t *d_rank, void *stream);
 /* E4: the same build restricted to the buckets [b_lo, b_hi) of a GOV structure
  * over n_global keys (one rank of the multi-GPU build).  d_sig
  * holds exactly the n_local signatures whose bucket lies in the range (any
@@ -153,10 +160,11 @@ int bsdb_dev_gov_build(bsdb_ctx *ctx, const uint64_t *d_sig, uint64_t n, uint32_
  * (plus E[m] on the last range), the 2-bit fields of the range's vertices and
  * the checksum fields of its ranks, and nothing else.  Fields of different
  * ranges are disjoint bits, so summing the ranks' arrays (one RCCL all-reduce
- * or reduce, ncclSum) assembles the global structure. */
+ * or reduce, ncclSum) assembles the global structure.  d_rank (optional):
+ * the global rank of each of the n_local signatures, as bsdb_dev_gov_build_ranks. */
 int bsdb_dev_gov_build_range(bsdb_ctx *ctx, const uint64_t *d_sig, uint64_t n_local, uint64_t n_global,
                              uint64_t b_lo, uint64_t b_hi, uint64_t e_lo, uint32_t width, uint64_t *d_E,
-                             uint64_t *d_values, uint64_t *d_sigbits, void *stream);
+                             uint64_t *d_values, uint64_t *d_sigbits, int64_t *d_rank, void *stream);
 /* E4 ownership: rank g of `nranks` owns buckets [g*m/nranks, (g+1)*m/nranks)
  * (m = num_buckets; the bucket is monotone in sig0, CBHS:129-138).  Groups the n
  * signatures of d_sig by owning rank into d_out (rank 0's first; order within a

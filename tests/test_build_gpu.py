@@ -219,6 +219,32 @@ def test_fvs_limit_fallback_is_identical(ctx, monkeypatch):
         np.testing.assert_array_equal(u64(v_d), vals)
 
 
+@pytest.mark.parametrize("n,width", [(1, 4), (3001, 0), (777_777, 4), (400_000, 64)])
+def test_ranks_from_the_solve(ctx, n, width):
+    """F2: the solve's ranks equal getLong of every key (oracle lookups), and
+    the checksum bits it signs equal the oracle's (sign-by-lookup)."""
+    keys = O.gen_keys13(31, n)
+    sig = O.hash_fixed_mt(keys, 13, THREADS)
+    rc, E, vals, sb, _ = O.gov_build_mt(sig, width, THREADS)
+    assert rc == 0
+    dE, dv, ds, rank = ctx.gov_build_ranks(dev(sig.view(np.int64)), width)
+    np.testing.assert_array_equal(u64(dE), E)
+    np.testing.assert_array_equal(u64(dv), vals)
+    if width:
+        np.testing.assert_array_equal(u64(ds)[: sb.size], sb)
+    np.testing.assert_array_equal(rank.cpu().numpy(), O.lookup_batch_mt(sig, n, E, vals, width, sb if width else None,
+                                                                         False, THREADS))
+
+
+def test_ranks_of_an_oversized_bucket(ctx):
+    keys = skewed_keys(4500, 4000)
+    sig = O.hash_fixed(keys, 13)
+    rc, E, vals, sb = O.gov_build(sig, 8)
+    dE, dv, ds, rank = ctx.gov_build_ranks(dev(sig.view(np.int64)), 8)
+    np.testing.assert_array_equal(u64(ds)[: sb.size], sb)
+    np.testing.assert_array_equal(rank.cpu().numpy(), O.lookup_batch(sig, 4500, E, vals, 8, sb, False))
+
+
 def test_verify_option(ctx):
     keys = O.gen_keys13(12, 200_000)
     sig = dev(O.hash_fixed(keys, 13).view(np.int64))
@@ -255,7 +281,9 @@ def test_range_builds_sum_to_full_build(ctx):
         got = u64(part)
         assert np.all((own[np.isin(sig[:, 0], got[:, 0])] == g))
         Er = torch.zeros_like(Es); Vr = torch.zeros_like(Vs); Sr = torch.zeros_like(Ss)
-        ctx.gov_build_range(part, n, b_lo, b_hi, e_lo, width, Er, Vr, Sr)
+        rk = torch.zeros(counts[g], dtype=torch.int64, device="cuda")
+        ctx.gov_build_range(part, n, b_lo, b_hi, e_lo, width, Er, Vr, Sr, rank=rk)
+        np.testing.assert_array_equal(rk.cpu().numpy(), O.lookup_batch(got, n, E, vals, width, sb, False))
         Es += Er; Vs += Vr; Ss += Sr
         e_lo += counts[g]
     np.testing.assert_array_equal(u64(Es), E)
