@@ -332,12 +332,22 @@ int bsdb_mph_free(bsdb_mph *p) {
 // ---- A13: the index writer ---------------------------------------------------
 int bsdb_index_open(bsdb_mph *p, int approximate, uint64_t pass_cache_bytes, const char *index_path,
                     const char *index_a_path, bsdb_index **out, uint64_t *passes) {
-    if (!p || !index_path || !out || (approximate && !index_a_path) || (p->n && pass_cache_bytes < 8)) return BSDB_EINVAL;
+    if (!p || !index_path || !out || (approximate && !index_a_path) || (p->n && pass_cache_bytes && pass_cache_bytes < 8))
+        return BSDB_EINVAL;
     *out = nullptr;
     bsdb_index *ix = new (std::nothrow) bsdb_index();
     if (!ix) return BSDB_ENOMEM;
     ix->mph = p;
     ix->approx = approximate != 0;
+    if (!pass_cache_bytes) {  // device-sized pass cache: a quarter of free HBM
+        size_t free_b = 0, total_b = 0;
+        std::lock_guard<std::mutex> g(p->c->mu);
+        if (hipSetDevice(p->c->device) != hipSuccess || hipMemGetInfo(&free_b, &total_b) != hipSuccess) {
+            delete ix;
+            return BSDB_EIO;
+        }
+        pass_cache_bytes = std::max<uint64_t>(8, free_b / 4 / (ix->approx ? 2 : 1));
+    }
     // W:112-118: passSize = min(n, passCacheSize / SLOT_SIZE), passes = ceil(n / passSize)
     ix->pass_size = std::min(p->n, pass_cache_bytes / 8);
     ix->passes = ix->pass_size ? (p->n + ix->pass_size - 1) / ix->pass_size : 0;

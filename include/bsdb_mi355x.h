@@ -310,7 +310,10 @@ int bsdb_mph_free(bsdb_mph *mph);
 /* ---------------------------------------------------------------------------
  * A13 + F2/F3: BSDBWriter.buildIndex (W:107-155, writeLBuffer W:166-179).
  * open: passSize = min(n, pass_cache_bytes / 8) slots, passes = ceil(n /
- *   passSize) (W:112-118); creates/truncates index_path and index_a_path
+ *   passSize) (W:112-118); pass_cache_bytes == 0 sizes the pass cache by the
+ *   device instead (a quarter of free HBM: one pass up to ~4 G records on an
+ *   MI355X; the files are the same, only the number of kv.db scans changes).
+ *   Creates/truncates index_path and index_a_path
  *   (the reference creates index_a.db even in exact mode, W:126; with
  *   index_a_path NULL it is not touched).  For each pass the caller feeds
  *   every record of the kv.db scan (KVWriter.forEach, W:134) with

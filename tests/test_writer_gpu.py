@@ -21,7 +21,7 @@ def read_record(base, addr):
         return f.read(kl), f.read(vl)
 
 
-@pytest.mark.parametrize("approx,partitions,pass_cache", [(False, 3, 8 * 40_000), (True, 1, 1 << 30)])
+@pytest.mark.parametrize("approx,partitions,pass_cache", [(False, 3, 8 * 40_000), (True, 1, 1 << 30), (True, 2, 0)])
 def test_build_and_read_back(tmp_path, approx, partitions, pass_cache):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
