@@ -53,13 +53,11 @@ int mph_alloc(bsdb_ctx *c, uint64_t n, uint32_t width, bsdb_mph **out) {
     return BSDB_OK;
 }
 
-// hash (host keys -> device signatures) + GOV build into a new mph
+// hash (host keys -> device signatures) + GOV build into a new mph; with
+// d_rank the solve also stores every key's rank by input position (F2).
+// The caller holds c->mu and has set the device.
 template <class HashDev>
-int mph_build(bsdb_ctx *c, uint64_t n, uint32_t width, bsdb_mph **out, HashDev &&hash_dev) {
-    if (n / BUCKET_SIZE + 1 > 0x7FFFFFFFULL) return BSDB_EINVAL;
-    std::lock_guard<std::mutex> g(c->mu);
-    HIP_OK(hipSetDevice(c->device));
-    Ordered ord(c, c->stream);
+int mph_build_locked(bsdb_ctx *c, uint64_t n, uint32_t width, bsdb_mph **out, int64_t *d_rank, HashDev &&hash_dev) {
     bsdb_mph *p = nullptr;
     int rc = mph_alloc(c, n, width, &p);
     if (rc) return rc;
@@ -70,9 +68,84 @@ int mph_build(bsdb_ctx *c, uint64_t n, uint32_t width, bsdb_mph **out, HashDev &
     }
     std::unique_ptr<void, DevFree> sig_guard(sig);
     if ((rc = hash_dev((uint64_t *)sig)) ||
-        (rc = gov_build_impl(c, (const uint64_t *)sig, n, n, 0, p->m, 0, width, p->E, p->values, p->sigbits, nullptr,
+        (rc = gov_build_impl(c, (const uint64_t *)sig, n, n, 0, p->m, 0, width, p->E, p->values, p->sigbits, d_rank,
                              c->stream, true))) {
         (void)hipStreamSynchronize(c->stream);
+        mph_release(p);
+        return rc;
+    }
+    *out = p;
+    return BSDB_OK;
+}
+
+template <class HashDev>
+int mph_build(bsdb_ctx *c, uint64_t n, uint32_t width, bsdb_mph **out, HashDev &&hash_dev) {
+    if (n / BUCKET_SIZE + 1 > 0x7FFFFFFFULL) return BSDB_EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    HIP_OK(hipSetDevice(c->device));
+    Ordered ord(c, c->stream);
+    return mph_build_locked(c, n, width, out, nullptr, hash_dev);
+}
+
+int write_chunks(FILE *f, const void *d_src, uint64_t bytes, hipStream_t s);
+
+// F2: build + index.db / index_a.db from the solve's ranks, no rescan.  The
+// slots are the same as bsdb_index_* passes over the same records give.
+template <class HashDev>
+int mph_build_index(bsdb_ctx *c, uint64_t n, uint32_t width, const uint64_t *h_addr, const uint64_t *h_value8,
+                    const uint8_t *h_vlen, bool approx, const char *index_path, const char *index_a_path,
+                    bsdb_mph **out, HashDev &&hash_dev) {
+    if (n / BUCKET_SIZE + 1 > 0x7FFFFFFFULL) return BSDB_EINVAL;
+    // W:124-127: both files created first (index_a.db empty in exact mode)
+    FILE *f = fopen(index_path, "wb");
+    FILE *fa = index_a_path ? fopen(index_a_path, "wb") : nullptr;
+    auto close_all = [&](int rc) {
+        bool ok = true;
+        if (f) ok = fclose(f) == 0 && ok;
+        if (fa) ok = fclose(fa) == 0 && ok;
+        return rc ? rc : (ok ? BSDB_OK : BSDB_EFILE);
+    };
+    if (!f || (index_a_path && !fa)) return close_all(BSDB_EFILE);
+    std::lock_guard<std::mutex> g(c->mu);
+    if (hipSetDevice(c->device) != hipSuccess) return close_all(BSDB_EIO);
+    Ordered ord(c, c->stream);
+    const uint64_t nn = std::max<uint64_t>(n, 1);
+    void *rank = nullptr, *addr = nullptr, *index = nullptr, *v8 = nullptr, *vl = nullptr, *index_a = nullptr;
+    auto free_all = [&](int rc) {
+        (void)hipStreamSynchronize(c->stream);
+        for (void *q : {rank, addr, index, v8, vl, index_a}) (void)hipFree(q);
+        return close_all(rc);
+    };
+    if (hipMalloc(&rank, nn * 8) != hipSuccess) return free_all(BSDB_ENOMEM);
+    bsdb_mph *p = nullptr;
+    int rc = mph_build_locked(c, n, width, &p, (int64_t *)rank, hash_dev);
+    if (rc) return free_all(rc);
+    if (hipMalloc(&addr, nn * 8) != hipSuccess || hipMalloc(&index, nn * 8) != hipSuccess ||
+        (approx && (hipMalloc(&v8, nn * 8) != hipSuccess || hipMalloc(&vl, nn) != hipSuccess ||
+                    hipMalloc(&index_a, nn * 8) != hipSuccess))) {
+        mph_release(p);
+        return free_all(BSDB_ENOMEM);
+    }
+    bool ok = hipMemcpyAsync(addr, h_addr, n * 8, hipMemcpyHostToDevice, c->stream) == hipSuccess &&
+              hipMemsetAsync(index, 0, nn * 8, c->stream) == hipSuccess;
+    if (ok && approx)
+        ok = hipMemcpyAsync(v8, h_value8, n * 8, hipMemcpyHostToDevice, c->stream) == hipSuccess &&
+             hipMemcpyAsync(vl, h_vlen, n, hipMemcpyHostToDevice, c->stream) == hipSuccess &&
+             hipMemsetAsync(index_a, 0, nn * 8, c->stream) == hipSuccess;
+    if (ok && n) {
+        k_index_scatter<<<grid_for(c, n), 256, 0, c->stream>>>((const int64_t *)rank, (const uint64_t *)addr, n, 0, n,
+                                                                (uint64_t *)index, (const uint64_t *)v8,
+                                                                (const uint8_t *)vl, (uint8_t *)index_a);
+        ok = hipGetLastError() == hipSuccess;
+    }
+    rc = ok ? write_chunks(f, index, n * 8, c->stream) : BSDB_EIO;
+    if (!rc && approx) rc = write_chunks(fa, index_a, n * 8, c->stream);
+    if (rc) {
+        mph_release(p);
+        return free_all(rc);
+    }
+    rc = free_all(BSDB_OK);
+    if (rc) {
         mph_release(p);
         return rc;
     }
@@ -202,6 +275,28 @@ int bsdb_mph_build_var(bsdb_ctx *c, const uint8_t *h_blob, const uint64_t *h_off
     if (!c || !out || width > 64 || (n && (!h_blob || !h_off))) return BSDB_EINVAL;
     *out = nullptr;
     return mph_build(c, n, width, out, [&](uint64_t *d_sig) { return host_hash_var_dev(c, h_blob, h_off, n, 0, d_sig); });
+}
+
+int bsdb_mph_build_index_fixed(bsdb_ctx *c, const uint8_t *h_keys, uint32_t key_len, uint64_t n, uint32_t width,
+                               const uint64_t *h_addr, const uint64_t *h_value8, const uint8_t *h_vlen,
+                               int approximate, const char *index_path, const char *index_a_path, bsdb_mph **out) {
+    if (!c || !out || !index_path || bad_key_len(key_len) || width > 64 || (approximate && !index_a_path) ||
+        (n && (!h_keys || !h_addr || (approximate && (!h_value8 || !h_vlen)))))
+        return BSDB_EINVAL;
+    *out = nullptr;
+    return mph_build_index(c, n, width, h_addr, h_value8, h_vlen, approximate != 0, index_path, index_a_path, out,
+                           [&](uint64_t *d_sig) { return host_hash_fixed_dev(c, h_keys, key_len, n, 0, d_sig); });
+}
+
+int bsdb_mph_build_index_var(bsdb_ctx *c, const uint8_t *h_blob, const uint64_t *h_off, uint64_t n, uint32_t width,
+                             const uint64_t *h_addr, const uint64_t *h_value8, const uint8_t *h_vlen, int approximate,
+                             const char *index_path, const char *index_a_path, bsdb_mph **out) {
+    if (!c || !out || !index_path || width > 64 || (approximate && !index_a_path) ||
+        (n && (!h_blob || !h_off || !h_addr || (approximate && (!h_value8 || !h_vlen)))))
+        return BSDB_EINVAL;
+    *out = nullptr;
+    return mph_build_index(c, n, width, h_addr, h_value8, h_vlen, approximate != 0, index_path, index_a_path, out,
+                           [&](uint64_t *d_sig) { return host_hash_var_dev(c, h_blob, h_off, n, 0, d_sig); });
 }
 
 int bsdb_mph_info(const bsdb_mph *p, uint64_t *n, uint64_t *m, uint32_t *width, uint64_t *values_words,

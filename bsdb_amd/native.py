@@ -71,6 +71,10 @@ SIGNATURES = [
     ("bsdb_multi_histogram_var", _i, [_vp, _vp, _vp, _u64, _u64, _vp]),
     ("bsdb_mph_build_fixed", _i, [_vp, _vp, _u32, _u64, _u32, C.POINTER(_vp)]),
     ("bsdb_mph_build_var", _i, [_vp, _vp, _vp, _u64, _u32, C.POINTER(_vp)]),
+    ("bsdb_mph_build_index_fixed", _i, [_vp, _vp, _u32, _u64, _u32, _vp, _vp, _vp, _i, C.c_char_p, C.c_char_p,
+                                        C.POINTER(_vp)]),
+    ("bsdb_mph_build_index_var", _i, [_vp, _vp, _vp, _u64, _u32, _vp, _vp, _vp, _i, C.c_char_p, C.c_char_p,
+                                      C.POINTER(_vp)]),
     ("bsdb_mph_info", _i, [_vp, C.POINTER(_u64), C.POINTER(_u64), C.POINTER(_u32), C.POINTER(_u64), C.POINTER(_u64)]),
     ("bsdb_mph_export", _i, [_vp, _vp, _vp, _vp]),
     ("bsdb_mph_import", _i, [_vp, _u64, _u32, _vp, _vp, _vp, C.POINTER(_vp)]),
@@ -323,6 +327,52 @@ class Context:
         h = C.c_void_p()
         _check("bsdb_mph_build_fixed", lib().bsdb_mph_build_fixed(
             self._h, keys_np.ctypes.data, key_len, keys_np.size // key_len, width, C.byref(h)))
+        return Mph(h, self)
+
+    @staticmethod
+    def _records_args(n, addr_np, value8_np, vlen_np, approximate):
+        import numpy as np
+        addr_np = np.ascontiguousarray(addr_np, np.uint64)
+        if addr_np.size != n:
+            raise ValueError("one address per key")
+        v8 = vl = None
+        if approximate:
+            if value8_np is None or vlen_np is None:
+                raise ValueError("approximate mode needs value8 and vlen")
+            v8 = np.ascontiguousarray(value8_np, np.uint64)
+            vl = np.ascontiguousarray(vlen_np, np.uint8)
+            if v8.size != n or vl.size != n:
+                raise ValueError("one value8/vlen per key")
+        return addr_np, v8, vl
+
+    def mph_build_index_fixed(self, keys_np, key_len: int, width: int, addr_np, index_path: str,
+                              index_a_path: Optional[str] = None, approximate: bool = False, value8_np=None,
+                              vlen_np=None) -> "Mph":
+        """F2: MPHF + index.db (+ index_a.db) in one call from the solve's
+        ranks (bsdb_mph_build_index_fixed), no rescan of the records."""
+        import numpy as np
+        keys_np = np.ascontiguousarray(keys_np, np.uint8)
+        n = keys_np.size // key_len
+        addr_np, v8, vl = self._records_args(n, addr_np, value8_np, vlen_np, approximate)
+        h = C.c_void_p()
+        _check("bsdb_mph_build_index_fixed", lib().bsdb_mph_build_index_fixed(
+            self._h, keys_np.ctypes.data, key_len, n, width, addr_np.ctypes.data,
+            v8.ctypes.data if v8 is not None else None, vl.ctypes.data if vl is not None else None,
+            1 if approximate else 0, index_path.encode(), index_a_path.encode() if index_a_path else None,
+            C.byref(h)))
+        return Mph(h, self)
+
+    def mph_build_index_var(self, blob_np, off_np, width: int, addr_np, index_path: str,
+                            index_a_path: Optional[str] = None, approximate: bool = False, value8_np=None,
+                            vlen_np=None) -> "Mph":
+        blob_np, off_np, n = self._var_host_args(blob_np, off_np)
+        addr_np, v8, vl = self._records_args(n, addr_np, value8_np, vlen_np, approximate)
+        h = C.c_void_p()
+        _check("bsdb_mph_build_index_var", lib().bsdb_mph_build_index_var(
+            self._h, blob_np.ctypes.data, off_np.ctypes.data, n, width, addr_np.ctypes.data,
+            v8.ctypes.data if v8 is not None else None, vl.ctypes.data if vl is not None else None,
+            1 if approximate else 0, index_path.encode(), index_a_path.encode() if index_a_path else None,
+            C.byref(h)))
         return Mph(h, self)
 
     def mph_build_var(self, blob_np, off_np, width: int) -> "Mph":

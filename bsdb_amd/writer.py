@@ -19,7 +19,9 @@ file set in ``base_path`` (src/main/java/tech/bsdb/write/BSDBWriter.java, "W"):
                      created empty otherwise (W:126)
 
 Every compute step is the C ABI (bsdb_mph_build_var, bsdb_index_*): no CPU
-fallback.  ``put`` is per record as in the reference; ``put_batch`` takes a
+fallback.  ``fused_index=True`` builds hash + index in one call whose solve
+returns every key's rank (bsdb_mph_build_index_var): no
+per-pass rescan, the same files.  ``put`` is per record as in the reference; ``put_batch`` takes a
 whole key blob at once.
 """
 from __future__ import annotations
@@ -40,7 +42,7 @@ class BSDBWriter:
     def __init__(self, base_path: str, tmp_dir: Optional[str] = None, checksum_bits: int = 4,
                  pass_cache_size: int = 1 << 30, compact: bool = True, compress: bool = False,
                  compress_block_size: int = 8192, shared_dict_size: int = 0, approximate_mode: bool = False,
-                 partitions: int = 1, device: int = 0):
+                 partitions: int = 1, device: int = 0, fused_index: bool = False):
         if compress or not compact:
             raise NotImplementedError("only the compact kv.db layout is mirrored (kv.db formats are out of scope)")
         self.base = base_path
@@ -50,6 +52,7 @@ class BSDBWriter:
         self.approximate = approximate_mode
         self.partitions = partitions
         self.compress_block_size = compress_block_size
+        self.fused_index = fused_index
         self._keys: list = []
         self._values: list = []
         self._batches: list = []  # (blob, offsets, value8, vlen, value bytes total)
@@ -131,6 +134,13 @@ class BSDBWriter:
         self._addr = self._write_kv(blob, off, vals)
         self._write_config(off, vals)
         self._blob, self._off, self._vals = blob, off, vals
+        if self.fused_index:
+            value8, vlen = self._value_heads()
+            mph = self.ctx.mph_build_index_var(blob, off, self.checksum_bits, self._addr,
+                                               os.path.join(self.base, "index.db"),
+                                               os.path.join(self.base, "index_a.db"), self.approximate, value8, vlen)
+            mph.dump(os.path.join(self.base, "hash.dump"))
+            return mph
         mph = self.build_hash()
         self.build_index(mph)
         return mph
@@ -144,13 +154,7 @@ class BSDBWriter:
     # W:107-155
     def build_index(self, mph: Mph, batch: int = 1 << 22):
         n = self._off.size - 1
-        value8 = np.zeros(n, np.uint64)
-        vlen = np.zeros(n, np.uint8)
-        if self.approximate:
-            for i, v in enumerate(self._vals):
-                head = v[:8]
-                value8[i] = int.from_bytes(head, "little")
-                vlen[i] = len(head)
+        value8, vlen = self._value_heads()
         off = self._off
 
         def feed(w):  # one kv.db scan per pass (W:134)
@@ -160,6 +164,18 @@ class BSDBWriter:
                           vlen[lo:hi] if self.approximate else None)
         return mph.write_index(os.path.join(self.base, "index.db"), os.path.join(self.base, "index_a.db"),
                                self.approximate, self.pass_cache_size, feed)
+
+    def _value_heads(self):
+        """index_a.db payload: the first <= 8 value bytes per record (W:140-142)."""
+        n = self._off.size - 1
+        value8 = np.zeros(n, np.uint64)
+        vlen = np.zeros(n, np.uint8)
+        if self.approximate:
+            for i, v in enumerate(self._vals):
+                head = v[:8]
+                value8[i] = int.from_bytes(head, "little")
+                vlen[i] = len(head)
+        return value8, vlen
 
     def close(self):
         self.ctx.close()

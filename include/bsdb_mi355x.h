@@ -328,6 +328,22 @@ int bsdb_mph_free(bsdb_mph *mph);
  *   (min(value length, 8)).  Uploads are double-buffered on two streams.
  * ------------------------------------------------------------------------- */
 typedef struct bsdb_index bsdb_index;
+
+/* F2: the MPHF and index.db (+ index_a.db) in ONE call from
+ * records in host memory -- hash -> GOV build whose solve also returns every
+ * key's rank (the input position is carried through the bucket sort as the
+ * store's payload, CBHS:386-388) -> addr[i] scattered big-endian at slot
+ * rank[i] -> files in writes of <= 128 MiB.  No kv.db rescan and no lookup
+ * pass: the files are identical to bsdb_index_* passes over the same
+ * records (W:107-155).  The whole index lives on the device (8n B, 17n B more
+ * in approximate mode); keys, addr[n], value8[n], vlen[n] as for put_*.
+ * index_a_path may be NULL in exact mode (otherwise created empty, W:126). */
+int bsdb_mph_build_index_fixed(bsdb_ctx *ctx, const uint8_t *h_keys, uint32_t key_len, uint64_t n, uint32_t width,
+                               const uint64_t *h_addr, const uint64_t *h_value8, const uint8_t *h_vlen,
+                               int approximate, const char *index_path, const char *index_a_path, bsdb_mph **out);
+int bsdb_mph_build_index_var(bsdb_ctx *ctx, const uint8_t *h_blob, const uint64_t *h_off, uint64_t n, uint32_t width,
+                             const uint64_t *h_addr, const uint64_t *h_value8, const uint8_t *h_vlen, int approximate,
+                             const char *index_path, const char *index_a_path, bsdb_mph **out);
 int bsdb_index_open(bsdb_mph *mph, int approximate, uint64_t pass_cache_bytes, const char *index_path,
                     const char *index_a_path, bsdb_index **out, uint64_t *passes);
 int bsdb_index_begin_pass(bsdb_index *ix, uint64_t pass);

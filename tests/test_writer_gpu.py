@@ -21,8 +21,10 @@ def read_record(base, addr):
         return f.read(kl), f.read(vl)
 
 
-@pytest.mark.parametrize("approx,partitions,pass_cache", [(False, 3, 8 * 40_000), (True, 1, 1 << 30), (True, 2, 0)])
-def test_build_and_read_back(tmp_path, approx, partitions, pass_cache):
+@pytest.mark.parametrize("approx,partitions,pass_cache,fused", [(False, 3, 8 * 40_000, False), (True, 1, 1 << 30, False),
+                                                                (True, 2, 0, False), (True, 2, 0, True),
+                                                                (False, 1, 0, True)])
+def test_build_and_read_back(tmp_path, approx, partitions, pass_cache, fused):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     from bsdb_amd.writer import BSDBWriter
@@ -32,7 +34,7 @@ def test_build_and_read_back(tmp_path, approx, partitions, pass_cache):
     vals = [rng.integers(0, 256, int(rng.integers(1, 60)), dtype=np.uint8).tobytes() for _ in range(n)]
     base = str(tmp_path / "db")
     w = BSDBWriter(base, checksum_bits=4, pass_cache_size=pass_cache, approximate_mode=approx,
-                   partitions=partitions)
+                   partitions=partitions, fused_index=fused)
     for k, v in zip(keys[: n // 2], vals[: n // 2]):
         w.put(k, v)
     rest = keys[n // 2:]
@@ -74,3 +76,51 @@ def test_build_and_read_back(tmp_path, approx, partitions, pass_cache):
     assert (ra >= 0).mean() < 0.1  # ~1/16 false positives at 4 checksum bits
     mph.close()
     w.close()
+
+
+@pytest.mark.parametrize("var,approx,n", [(False, False, 200_000), (True, True, 150_000), (False, True, 1)])
+def test_build_index_in_one_call_equals_the_pass_loop(tmp_path, var, approx, n):
+    """F2 (bsdb_mph_build_index_*): the index files from the solve's ranks are
+    byte-identical to the reference's pass loop (lookup per record, W:129-145)
+    over the same records, and the MPHF is the same."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import oracle as O
+    from bsdb_amd import Context
+    ctx = Context(0)
+    rng = np.random.default_rng(5)
+    if var:
+        blob, off = O.gen_keys_var(0, n)
+    else:
+        keys = O.gen_keys13(77, n)
+    addr = rng.integers(0, 1 << 62, n, dtype=np.uint64)
+    value8 = rng.integers(0, 1 << 63, n, dtype=np.uint64) if approx else None
+    vlen = rng.integers(0, 9, n).astype(np.uint8) if approx else None
+    d1, d2 = tmp_path / "fused", tmp_path / "loop"
+    d1.mkdir(); d2.mkdir()
+    ip1, ap1, ip2, ap2 = (str(d / f) for d in (d1, d2) for f in ("index.db", "index_a.db"))
+    if var:
+        m1 = ctx.mph_build_index_var(blob, off, 4, addr, ip1, ap1, approx, value8, vlen)
+        m2 = ctx.mph_build_var(blob, off, 4)
+    else:
+        m1 = ctx.mph_build_index_fixed(keys, 13, 4, addr, ip1, ap1, approx, value8, vlen)
+        m2 = ctx.mph_build_fixed(keys, 13, 4)
+    for a, b in zip(m1.export(), m2.export()):
+        np.testing.assert_array_equal(a, b)
+    B = 64_000
+
+    def feed(w):
+        for lo in range(0, n, B):
+            hi = min(n, lo + B)
+            v8 = value8[lo:hi] if approx else None
+            vl = vlen[lo:hi] if approx else None
+            if var:
+                w.put_var(blob, off[lo: hi + 1], addr[lo:hi], v8, vl)
+            else:
+                w.put_fixed(keys[13 * lo: 13 * hi], 13, addr[lo:hi], v8, vl)
+    passes = m2.write_index(ip2, ap2, approx, 8 * 70_000, feed)
+    assert passes == -(-n // min(n, 70_000))
+    for a, b in ((ip1, ip2), (ap1, ap2)):
+        assert open(a, "rb").read() == open(b, "rb").read()
+    assert os.path.getsize(ip1) == 8 * n and os.path.getsize(ap1) == (8 * n if approx else 0)
+    m1.close(); m2.close(); ctx.close()

@@ -2,7 +2,7 @@
 start in host memory, counts / signatures end in host memory.
 
     python tools/e2e_host.py [--n KEYS]
-    python tools/e2e_host.py --full KEYS [--approx] [--dir D]
+    python tools/e2e_host.py --full KEYS [--approx] [--dir D] [--ps BYTES | --fused]
 Keys are generated on the device (D2 recipe) and copied to a host buffer
 before timing; both a pageable and a pinned host buffer are timed.
 
@@ -23,7 +23,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from bsdb_amd import Context  # noqa: E402
 
 
-def full(ctx, n, approx, d, ps):
+def full(ctx, n, approx, d, ps, fused=False):
     keys = np.empty(13 * n, np.uint8)
     step = 500_000_000
     for k0 in range(0, n, step):
@@ -35,6 +35,20 @@ def full(ctx, n, approx, d, ps):
     vlen = np.full(n, 8, np.uint8) if approx else None
     os.makedirs(d, exist_ok=True)
     ip, ap_, hp = (os.path.join(d, f) for f in ("index.db", "index_a.db", "hash.dump"))
+    if fused:  # F2: one call, index from the solve's ranks
+        t0 = time.perf_counter()
+        mph = ctx.mph_build_index_fixed(keys, 13, 4, addr, ip, ap_, approx, value8, vlen)
+        t1 = time.perf_counter()
+        mph.dump(hp)
+        t2 = time.perf_counter()
+        res = {"n": n, "approximate": approx, "fused_index": True, "mph_build_and_index_s": t1 - t0,
+               "dump_s": t2 - t1, "total_s": t2 - t0, "keys_per_s": n / (t2 - t0),
+               "index_db_bytes": os.path.getsize(ip), "index_a_db_bytes": os.path.getsize(ap_)}
+        mph.close()
+        for f in (ip, ap_, hp):
+            os.remove(f)
+        print(json.dumps(res), flush=True)
+        return
     t0 = time.perf_counter()
     mph = ctx.mph_build_fixed(keys, 13, 4)
     t1 = time.perf_counter()
@@ -65,11 +79,12 @@ def main():
     ap.add_argument("--full", type=int, default=0)
     ap.add_argument("--approx", action="store_true")
     ap.add_argument("--dir", default="/tmp/bsdb_e2e")
+    ap.add_argument("--fused", action="store_true", help="F2: bsdb_mph_build_index_fixed")
     ap.add_argument("--ps", type=int, default=1 << 30, help="pass cache bytes (0 = device-sized)")
     args = ap.parse_args()
     if args.full:
         ctx = Context(0)
-        full(ctx, args.full, args.approx, args.dir, args.ps)
+        full(ctx, args.full, args.approx, args.dir, args.ps, args.fused)
         return
     n = args.n
     m = n // 1500 + 1
