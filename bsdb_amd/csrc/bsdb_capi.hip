@@ -234,6 +234,8 @@ D13Sel d13_select(const bsdb_ctx *c, bool var = false, uint32_t key_len = 13) {
         D13Kernel k = k_pass1_vare<0, false>;
         if (c->d13_variant == 1) k = k_pass1_vare<1, false>;
         if (c->d13_variant == 4) k = k_pass1_vare<4, false>;
+        if (c->d13_variant == 5) k = k_pass1_vare<5, false>;
+        if (c->d13_variant == 6) k = k_pass1_vare<6, false>;
         return {k, VARE_NT, VARE_TILE, VARE_MAXP, true, VARE_BIN_IDS};
     }
     switch (c->d13_variant) {

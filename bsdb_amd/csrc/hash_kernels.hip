@@ -934,18 +934,39 @@ __global__ __launch_bounds__(VARE_NT, 4) void k_pass1_vare(P1Args a, uint64_t nt
     // B); a branch runs whenever ANY lane takes it, so the caller sorts a
     // group's keys short-first: chain 0 then holds only keys < 16 B (no mix,
     // 5 dwords) unless the group has fewer than 64 of them.
+    // VARIANT 5 (profiling, results invalid): every lane reads a conflict-free
+    // address instead of its key's.  VARIANT 6: 8-byte aligned ds_read_b64
+    // reads, the odd-dword start selected in registers.
+    auto read_key = [&](uint32_t b, auto nc, uint32_t *d) __attribute__((always_inline)) {
+        constexpr int N = decltype(nc)::value;
+        if (VARIANT == 6) {
+            const uint64_t *q = reinterpret_cast<const uint64_t *>(stage) + (b >> 1);
+            const bool odd = b & 1;
+            uint32_t x[N + 1 + (N & 1)];
+#pragma unroll
+            for (int i = 0; i < (N + 2) / 2; ++i) {
+                const uint64_t v = q[i];
+                x[2 * i] = (uint32_t)v;
+                x[2 * i + 1] = (uint32_t)(v >> 32);
+            }
+#pragma unroll
+            for (int i = 0; i < N; ++i) d[i] = odd ? x[i + 1] : x[i];
+        } else {
+            const uint32_t bb = VARIANT == 5 ? (uint32_t)l * 17 : b;
+#pragma unroll
+            for (int i = 0; i < N; ++i) d[i] = stage[bb + i];
+        }
+    };
     auto sig0_staged = [&](uint32_t o, uint32_t len) __attribute__((always_inline)) {
         const uint32_t b = o >> 2, sh = (o & 3) * 8;
         uint64_t s0;
         if (__builtin_amdgcn_ballot_w64(len >= 16) == 0) {  // wave-uniform
             uint32_t d[5];
-#pragma unroll
-            for (int i = 0; i < 5; ++i) d[i] = stage[b + i];
+            read_key(b, std::integral_constant<int, 5>{}, d);
             s0 = spooky_lt16_sig0(d, sh, len, a.seed);
         } else if (len <= 64) {
             uint32_t d[17];
-#pragma unroll
-            for (int i = 0; i < 17; ++i) d[i] = stage[b + i];
+            read_key(b, std::integral_constant<int, 17>{}, d);
             s0 = spooky_le64_sig0(d, sh, len, a.seed);
         } else {
             s0 = vare_sig0_lds(stage, o, len, a.seed);
