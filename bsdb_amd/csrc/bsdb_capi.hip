@@ -738,7 +738,9 @@ static void print_gov_profile(const std::vector<uint64_t> &h, uint32_t solve_gri
     const char *names[GP_N] = {"edges", "peel", "greedy", "bfs", "tarjan", "singletons", "dense", "back",
                                "store", "n_seeds", "n_bfs", "n_bfs_pops", "n_dense_rows", "n_dense_max",
                                "n_core", "n_blocks", "n_rows_in_blocks_over_440", "n_scc_sweeps",
-                               "n_small_scc_fallbacks", "fvs_select", "fvs_forms", "fvs_gauss_jordan"};
+                               "n_small_scc_fallbacks", "fvs_select", "fvs_forms", "fvs_gauss_jordan",
+                               "n_fail_degenerate", "n_fail_orient", "n_fail_singular", "failed_attempt_cycles",
+                               "bfs_flip", "n_bfs_iters", "n_flip_steps"};
     std::vector<double> tot(GP_N, 0.0);
     for (uint32_t w = 0; w < solve_grid; ++w)
         for (int k = 0; k < GP_N; ++k) {
@@ -747,7 +749,7 @@ static void print_gov_profile(const std::vector<uint64_t> &h, uint32_t solve_gri
         }
     fprintf(stderr, "[gov-profile] m=%llu grid=%u", (unsigned long long)m, solve_grid);
     for (int k = 0; k < GP_N; ++k)
-        fprintf(stderr, " %s=%.4g", names[k], k == GP_N_DENSE_MAX ? tot[k] : tot[k] / ((k < GP_N_SEEDS || k >= GP_FVS_SEL) ? solve_grid : 1));
+        fprintf(stderr, " %s=%.4g", names[k], k == GP_N_DENSE_MAX ? tot[k] : tot[k] / ((k < GP_N_SEEDS || (k >= GP_FVS_SEL && k <= GP_FVS_GJ) || k == GP_FAILED_CYCLES || k == GP_BFS_FLIP) ? solve_grid : 1));
     fprintf(stderr, "  (cycles: mean per workgroup; counts: totals)\n");
 }
 

@@ -234,7 +234,9 @@ struct SolveArgs {
 // phase counters (cycles, or counts for the GP_N_* slots)
 enum GovProf { GP_EDGES, GP_PEEL, GP_GREEDY, GP_BFS, GP_TARJAN, GP_SINGLE, GP_DENSE, GP_BACK, GP_STORE,
                GP_N_SEEDS, GP_N_BFS, GP_N_BFS_POPS, GP_N_DENSE_ROWS, GP_N_DENSE_MAX, GP_N_CORE, GP_N_BLOCKS, GP_N_BIG_ROWS,
-               GP_N_SCC_SWEEPS, GP_N_SMALL_S, GP_FVS_SEL, GP_FVS_FORMS, GP_FVS_GJ, GP_N };
+               GP_N_SCC_SWEEPS, GP_N_SMALL_S, GP_FVS_SEL, GP_FVS_FORMS, GP_FVS_GJ,
+               GP_N_FAIL_DEGEN, GP_N_FAIL_ORIENT, GP_N_FAIL_SINGULAR, GP_FAILED_CYCLES, GP_BFS_FLIP, GP_N_BFS_ITERS,
+               GP_N_FLIP_STEPS, GP_N };
 
 // Solver state for buckets of up to CMAX_ keys: LDS for GS_CMAX, a global
 // slab per workgroup for GB_CMAX (same code; indices fit int16 either way).
@@ -338,7 +340,7 @@ __device__ void wg_excl_scan3(uint32_t *a, uint32_t n, uint32_t *wsum) {
 // Tries local seed j on bucket (sig, cnt, nv).  Returns (WG-uniform) true on
 // success with L.xval / L.vowner describing the solution.
 template <class Lds>
-__device__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t cnt, uint32_t nv, uint64_t seed_bits,
+__device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t cnt, uint32_t nv, uint64_t seed_bits,
                          uint64_t *scr, PhaseClock &pc, uint32_t fvs_max) {
     const int tid = threadIdx.x;
     pc.start();
@@ -367,7 +369,10 @@ __device__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t cnt, uint32_t n
     }
     __syncthreads();
     pc.lap(GP_EDGES);
-    if (L.flag) return false;
+    if (L.flag) {
+        pc.add(GP_N_FAIL_DEGEN, 1);
+        return false;
+    }
     if (cnt == 1 && nv == 1) {
         if (tid == 0) {
             L.vowner[0] = 0;
@@ -497,7 +502,8 @@ __device__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t cnt, uint32_t n
         int16_t *bfs_prev = L.a0, *queue = L.a1;
         uint32_t *first_lane = L.xe;  // (dead after peeling)
         const uint32_t lane = tid;
-        uint32_t epoch = 0, ok = 1, nbfs = 0, npops = 0, ncore = 0;
+        uint32_t epoch = 0, ok = 1, nbfs = 0, npops = 0, ncore = 0, niters = 0, nflip = 0;
+        uint64_t flip_cyc = 0;
         if (pc.acc)
             for (uint32_t k = 0; k < cnt; ++k) ncore += L.round_of[k] < 0;
         // unmatched core edges, 64 at a time by ballot (a BFS only matches its
@@ -555,6 +561,7 @@ __device__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t cnt, uint32_t n
                 qt += (uint32_t)__builtin_popcountll(tb);
                 qh += ch;
                 npops += ch;
+                ++niters;
                 if (fb) {
                     found_v = __builtin_amdgcn_readlane((int)v, (int)F);
                     found_e = __builtin_amdgcn_readlane(k, (int)F);
@@ -565,17 +572,20 @@ __device__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t cnt, uint32_t n
                 ok = 0;
                 break;
             }
+            const uint64_t tf = pc.acc ? clock64() : 0;
             if (lane == 0) {
                 int k = found_e, v = found_v;
                 for (;;) {
                     const int old = L.hinge[k];
                     L.hinge[k] = (int16_t)v;
                     L.vowner[v] = (int16_t)k;
+                    ++nflip;
                     if (k == (int)k0) break;
                     v = old;
                     k = bfs_prev[k];
                 }
             }
+            if (pc.acc) flip_cyc += clock64() - tf;
             __builtin_amdgcn_wave_barrier();
         }
         if (lane == 0) {
@@ -583,11 +593,17 @@ __device__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t cnt, uint32_t n
             pc.add(GP_N_BFS, nbfs);
             pc.add(GP_N_BFS_POPS, npops);
             pc.add(GP_N_CORE, ncore);
+            pc.add(GP_BFS_FLIP, flip_cyc);
+            pc.add(GP_N_BFS_ITERS, niters);
+            pc.add(GP_N_FLIP_STEPS, nflip);
         }
     }
     __syncthreads();
     pc.lap(GP_BFS);
-    if (!L.flag) return false;
+    if (!L.flag) {
+        pc.add(GP_N_FAIL_ORIENT, 1);
+        return false;
+    }
 
     // ---- tiny buckets: first satisfying assignment in base-3 order (lane 0)
     if (tiny) {
@@ -839,74 +855,69 @@ __device__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t cnt, uint32_t n
 
         // Gauss-Jordan on rows 0..n-1 of X (n equations, n unknowns, the
         // right-hand side in column n), without row swaps: column cc's pivot
-        // is the first unused row with a nonzero there (found while column
-        // cc-1 is eliminated), piv[cc] remembers it.  A nonsingular square
-        // system has ONE solution whatever the pivots, so the values equal
-        // the oracle's row-swapping elimination.  colval[cc] = x_cc.
+        // is the first unused row with a nonzero there, piv[cc] remembers it.
+        // A nonsingular square system has ONE solution whatever the pivots,
+        // so the values equal the oracle's row-swapping elimination.
+        // colval[cc] = x_cc.  ONE barrier per column: every row reads the
+        // pivot row where it lies (its owner last wrote it before the
+        // previous barrier and leaves it alone in its own column); while a
+        // row is eliminated it bids for the next column's pivot (the lowest
+        // candidate lane of each wave, one LDS atomicMin).  The bid word is
+        // triple-buffered by column (read in cc, bid into in cc, re-armed in
+        // cc + 1: each use a barrier apart).
         auto gauss_jordan = [&](uint32_t n, auto &&X) -> bool {
             const uint32_t W = (n + 1 + 63) / 64;
             int16_t *piv = L.a0;
             uint8_t *used = L.b1;
+            uint32_t *bid = L.hbin;  // bid[cc % 3]
             for (uint32_t rr = tid; rr < n; rr += GS_THREADS) used[rr] = 0;
-            if (tid == 0) {
-                L.flag = 1;
-                L.pivot = 0xFFFFFFFFu;
-            }
+            if (tid < 3) bid[tid] = 0xFFFFFFFFu;
             __threadfence_block();
             __syncthreads();
-            for (uint32_t rr = tid; rr < n; rr += GS_THREADS)
-                if ((X(rr, 0, 0) | X(rr, 0, 1)) & 1ULL) atomicMin(&L.pivot, rr);
+            for (uint32_t rr = tid; rr < n; rr += GS_THREADS) {
+                const bool cand = (X(rr, 0, 0) | X(rr, 0, 1)) & 1ULL;
+                const uint64_t bal = __builtin_amdgcn_ballot_w64(cand);
+                if (cand && (uint32_t)__builtin_ctzll(bal) == (tid & 63)) atomicMin(&bid[0], rr);
+            }
             __syncthreads();
+            bool ok = true;
             for (uint32_t cc = 0; cc < n; ++cc) {
-                const uint32_t wc = cc >> 6;
-                const uint64_t bit = 1ULL << (cc & 63);
-                const uint32_t p = L.pivot;
-                if (p == 0xFFFFFFFFu) {  // singular
-                    if (tid == 0) L.flag = 0;
-                    __syncthreads();
+                const uint32_t p = bid[cc % 3];
+                if (p == 0xFFFFFFFFu) {  // singular (uniform)
+                    ok = false;
                     break;
                 }
-                // the pivot row, normalised to coefficient 1, into LDS; it is
-                // zero in every earlier pivot column, so words below wc stay
-                // untouched
-                const bool two = (X(p, wc, 1) & bit) != 0;
-                for (uint32_t w = wc + tid; w < W; w += GS_THREADS) {
-                    const uint64_t p1 = X(p, w, 0), p2 = X(p, w, 1);
-                    L.prow[w] = two ? p2 : p1;
-                    L.prow[W + w] = two ? p1 : p2;
-                }
+                const uint32_t wc = cc >> 6;
+                const uint64_t bit = 1ULL << (cc & 63);
+                const bool two = (X(p, wc, 1) & bit) != 0;  // pivot coefficient 2: its row normalised = planes swapped
                 if (tid == 0) {
                     piv[cc] = (int16_t)p;
-                    used[p] = 1;
+                    bid[(cc + 2) % 3] = 0xFFFFFFFFu;
                 }
-                __syncthreads();
-                if (tid == 0) L.pivot = 0xFFFFFFFFu;  // read by every lane above, before the barrier
-                // eliminate column cc from every other row; meanwhile the
-                // first unused row with a nonzero in column cc+1 becomes the
-                // next pivot
-                const uint32_t wn = (cc + 1) >> 6;
-                const uint64_t nbit = 1ULL << ((cc + 1) & 63);
-                __syncthreads();
+                const uint32_t cn = cc + 1, wn = cn >> 6;
+                const uint64_t nbit = 1ULL << (cn & 63);
                 for (uint32_t rr = tid; rr < n; rr += GS_THREADS) {
                     bool cand = false;
-                    if (rr != p) {
+                    if (rr == p) {
+                        used[rr] = 1;
+                    } else {
                         const uint64_t f1 = X(rr, wc, 0) & bit, f2 = X(rr, wc, 1) & bit;
-                        if (f1 || f2)
+                        if (f1 || f2) {
+                            const bool sw = (f1 != 0) != two;  // subtract cf * (normalised pivot row)
                             for (uint32_t w = wc; w < W; ++w) {
-                                const uint64_t y1 = f1 ? L.prow[W + w] : L.prow[w];
-                                const uint64_t y2 = f1 ? L.prow[w] : L.prow[W + w];
-                                gf3_add(X(rr, w, 0), X(rr, w, 1), y1, y2);
+                                const uint64_t q1 = X(p, w, 0), q2 = X(p, w, 1);
+                                gf3_add(X(rr, w, 0), X(rr, w, 1), sw ? q2 : q1, sw ? q1 : q2);
                             }
-                        cand = cc + 1 < n && !used[rr] && ((X(rr, wn, 0) | X(rr, wn, 1)) & nbit);
+                        }
+                        cand = cn < n && !used[rr] && ((X(rr, wn, 0) | X(rr, wn, 1)) & nbit);
                     }
                     // a wave's lanes hold consecutive rows: its lowest
-                    // candidate lane alone competes (one LDS atomic per wave)
+                    // candidate lane alone bids (one LDS atomic per wave)
                     const uint64_t bal = __builtin_amdgcn_ballot_w64(cand);
-                    if (cand && (uint32_t)__builtin_ctzll(bal) == (tid & 63)) atomicMin(&L.pivot, rr);
+                    if (cand && (uint32_t)__builtin_ctzll(bal) == (tid & 63)) atomicMin(&bid[cn % 3], rr);
                 }
                 __syncthreads();
             }
-            const bool ok = L.flag != 0;
             if (ok)
                 // column cc's pivot row reads cf * x = rhs with cf in {1, 2}
                 // (every other column eliminated), so x = cf * rhs mod 3
@@ -917,6 +928,8 @@ __device__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t cnt, uint32_t n
                     const uint32_t cf = (X(pr, cc >> 6, 1) & cbit) ? 2 : 1;
                     colval[cc] = (uint8_t)(cf * rhs % 3);
                 }
+            else if (tid == 0)
+                L.flag = 0;
             __syncthreads();
             return ok;
         };
@@ -1301,7 +1314,10 @@ __device__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t cnt, uint32_t n
                 // (rows in X: words < 12 CMAX, below the forms)
                 const bool hok = hs_lds ? gauss_jordan(nH, HSL) : gauss_jordan(nH, X);
                 pc.lap(GP_FVS_GJ);
-                if (!hok) return false;
+                if (!hok) {
+                    pc.add(GP_N_FAIL_SINGULAR, 1);
+                    return false;
+                }
                 // evaluate: x_i = forms . (x_heavy, 1)
                 uint64_t *X1 = L.prow, *X2 = L.prow + 8;
                 for (uint32_t w = tid; w < 16; w += GS_THREADS) L.prow[w] = 0;
@@ -1354,7 +1370,10 @@ __device__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t cnt, uint32_t n
                 if (rhs == 1) X(rr, sz >> 6, 0) |= 1ULL << (sz & 63);
                 if (rhs == 2) X(rr, sz >> 6, 1) |= 1ULL << (sz & 63);
             }
-            if (!gauss_jordan(sz, X)) return false;
+            if (!gauss_jordan(sz, X)) {
+                pc.add(GP_N_FAIL_SINGULAR, 1);
+                return false;
+            }
             for (uint32_t cc = tid; cc < sz; cc += GS_THREADS) L.xval[L.hinge[L.members[beg + cc]]] = colval[cc];
         }
         for (uint32_t i = tid; i < sz; i += GS_THREADS) L.col_of[L.members[beg + i]] = -1;
@@ -1391,7 +1410,7 @@ __device__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t cnt, uint32_t n
 // Solves bucket b with state L (LDS or a global slab) and stores its values
 // and local seed.  Workgroup-uniform.
 template <class Lds>
-__device__ void solve_bucket(Lds &L, const SolveArgs &a, uint64_t b, uint64_t *scr, PhaseClock &pc) {
+__device__ __forceinline__ void solve_bucket(Lds &L, const SolveArgs &a, uint64_t b, uint64_t *scr, PhaseClock &pc) {
     const uint64_t lo = a.E[b] & OFFSET_MASK, hi = a.E[b + 1] & OFFSET_MASK;
     const uint32_t cnt = (uint32_t)(hi - lo);
     const uint64_t vo = vertex_offset(lo);
@@ -1403,8 +1422,11 @@ __device__ void solve_bucket(Lds &L, const SolveArgs &a, uint64_t b, uint64_t *s
     }
     const ulonglong2 *sig = reinterpret_cast<const ulonglong2 *>(a.sig) + (lo - a.e0);
     uint32_t j = 0;
-    for (; j < 256; ++j)
+    for (; j < 256; ++j) {
+        const uint64_t t_try = pc.acc ? clock64() : 0;
         if (try_seed(L, sig, cnt, nv, (uint64_t)j << 56, scr, pc, a.fvs_max)) break;
+        if (pc.acc) pc.add(GP_FAILED_CYCLES, clock64() - t_try);
+    }
     pc.start();
     if (j == 256) {
         if (threadIdx.x == 0) atomicOr(a.status, (uint32_t)GOV_SEEDS);
