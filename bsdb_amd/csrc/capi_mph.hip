@@ -87,7 +87,7 @@ int mph_build(bsdb_ctx *c, uint64_t n, uint32_t width, bsdb_mph **out, HashDev &
     return mph_build_locked(c, n, width, out, nullptr, hash_dev);
 }
 
-int write_chunks(FILE *f, const void *d_src, uint64_t bytes, hipStream_t s);
+int write_files(int device, FILE *const *files, const void *const *d_srcs, int nfiles, uint64_t bytes);
 
 // F2: build + index.db / index_a.db from the solve's ranks, no rescan.  The
 // slots are the same as bsdb_index_* passes over the same records give.
@@ -138,8 +138,14 @@ int mph_build_index(bsdb_ctx *c, uint64_t n, uint32_t width, const uint64_t *h_a
                                                                 (const uint8_t *)vl, (uint8_t *)index_a);
         ok = hipGetLastError() == hipSuccess;
     }
-    rc = ok ? write_chunks(f, index, n * 8, c->stream) : BSDB_EIO;
-    if (!rc && approx) rc = write_chunks(fa, index_a, n * 8, c->stream);
+    ok = ok && hipStreamSynchronize(c->stream) == hipSuccess;
+    if (ok) {
+        FILE *fs[2] = {f, fa};
+        const void *ds[2] = {index, index_a};
+        rc = write_files(c->device, fs, ds, approx ? 2 : 1, n * 8);
+    } else {
+        rc = BSDB_EIO;
+    }
     if (rc) {
         mph_release(p);
         return free_all(rc);
@@ -225,6 +231,65 @@ int write_chunks(FILE *f, const void *d_src, uint64_t bytes, hipStream_t s) {
         HIP_OK(hipStreamSynchronize(s));
         if (fwrite(host.data(), 1, k, f) != k) return BSDB_EFILE;
     }
+    return BSDB_OK;
+}
+
+// The same for up to two files at once (index.db and index_a.db), each on a
+// thread of its own with its own stream and two pinned 128 MiB staging
+// buffers: chunk i+1 comes over PCIe while chunk i is written.  The device
+// data must be complete (the caller has synchronised its stream).
+int write_files(int device, FILE *const *files, const void *const *d_srcs, int nfiles, uint64_t bytes) {
+    constexpr uint64_t CHUNK = 128ULL << 20;
+    if (bytes <= 2 * CHUNK) {  // small: the plain path (no pinned allocation)
+        hipStream_t s0 = nullptr;
+        for (int i = 0; i < nfiles; ++i) {
+            const int rc = write_chunks(files[i], d_srcs[i], bytes, s0);
+            if (rc) return rc;
+        }
+        return BSDB_OK;
+    }
+    std::vector<int> rcs(nfiles, BSDB_OK);
+    auto one = [&](int i) {
+        int &rc = rcs[i];
+        hipStream_t st = nullptr;
+        void *buf[2] = {nullptr, nullptr};
+        if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess ||
+            hipHostMalloc(&buf[0], CHUNK, hipHostMallocDefault) != hipSuccess ||
+            hipHostMalloc(&buf[1], CHUNK, hipHostMallocDefault) != hipSuccess) {
+            rc = BSDB_ENOMEM;
+        } else {
+            const uint8_t *src = (const uint8_t *)d_srcs[i];
+            const uint64_t nch = (bytes + CHUNK - 1) / CHUNK;
+            auto issue = [&](uint64_t c) {
+                const uint64_t o = c * CHUNK, k = std::min(CHUNK, bytes - o);
+                return hipMemcpyAsync(buf[c & 1], src + o, k, hipMemcpyDeviceToHost, st) == hipSuccess;
+            };
+            bool ok = issue(0) && hipStreamSynchronize(st) == hipSuccess;
+            for (uint64_t c = 0; ok && c < nch; ++c) {
+                if (c + 1 < nch) ok = issue(c + 1);  // overlaps the write of chunk c
+                const uint64_t k = std::min(CHUNK, bytes - c * CHUNK);
+                if (ok && fwrite(buf[c & 1], 1, k, files[i]) != k) {
+                    rc = BSDB_EFILE;
+                    ok = false;
+                }
+                if (hipStreamSynchronize(st) != hipSuccess && ok) ok = false;
+            }
+            if (!ok && rc == BSDB_OK) rc = BSDB_EIO;
+        }
+        if (st) {
+            (void)hipStreamSynchronize(st);
+            (void)hipStreamDestroy(st);
+        }
+        for (void *b : buf)
+            if (b) (void)hipHostFree(b);
+    };
+    std::vector<std::thread> th;
+    for (int i = 1; i < nfiles; ++i) th.emplace_back(one, i);
+    one(0);
+    for (auto &t : th) t.join();
+    (void)hipSetDevice(device);
+    for (int rc : rcs)
+        if (rc) return rc;
     return BSDB_OK;
 }
 
@@ -516,8 +581,10 @@ int bsdb_index_end_pass(bsdb_index *ix) {
     Ordered ord(c, c->stream);
     // W:147: the last pass writes only its lastPassSize slots
     const uint64_t start = ix->cur * ix->pass_size, len = std::min(ix->pass_size, ix->mph->n - start);
-    int rc = write_chunks(ix->f, ix->d_index, len * 8, c->stream);
-    if (!rc && ix->approx) rc = write_chunks(ix->fa, ix->d_index_a, len * 8, c->stream);
+    HIP_OK(hipStreamSynchronize(c->stream));
+    FILE *fs[2] = {ix->f, ix->fa};
+    const void *ds[2] = {ix->d_index, ix->d_index_a};
+    int rc = write_files(c->device, fs, ds, ix->approx ? 2 : 1, len * 8);
     if (rc) return rc;
     ix->cur = UINT64_MAX;
     ++ix->next_pass;
