@@ -740,7 +740,8 @@ static void print_gov_profile(const std::vector<uint64_t> &h, uint32_t solve_gri
                                "n_core", "n_blocks", "n_rows_in_blocks_over_440", "n_scc_sweeps",
                                "n_small_scc_fallbacks", "fvs_select", "fvs_forms", "fvs_gauss_jordan",
                                "n_fail_degenerate", "n_fail_orient", "n_fail_singular", "failed_attempt_cycles",
-                               "bfs_flip", "n_bfs_iters", "n_flip_steps"};
+                               "bfs_flip", "n_bfs_iters", "n_flip_steps", "n_sel_batches", "n_sel_picks",
+                               "sel_pick_cycles", "sel_prep_cycles"};
     std::vector<double> tot(GP_N, 0.0);
     for (uint32_t w = 0; w < solve_grid; ++w)
         for (int k = 0; k < GP_N; ++k) {
@@ -749,7 +750,7 @@ static void print_gov_profile(const std::vector<uint64_t> &h, uint32_t solve_gri
         }
     fprintf(stderr, "[gov-profile] m=%llu grid=%u", (unsigned long long)m, solve_grid);
     for (int k = 0; k < GP_N; ++k)
-        fprintf(stderr, " %s=%.4g", names[k], k == GP_N_DENSE_MAX ? tot[k] : tot[k] / ((k < GP_N_SEEDS || (k >= GP_FVS_SEL && k <= GP_FVS_GJ) || k == GP_FAILED_CYCLES || k == GP_BFS_FLIP) ? solve_grid : 1));
+        fprintf(stderr, " %s=%.4g", names[k], k == GP_N_DENSE_MAX ? tot[k] : tot[k] / ((k < GP_N_SEEDS || (k >= GP_FVS_SEL && k <= GP_FVS_GJ) || k == GP_FAILED_CYCLES || k == GP_BFS_FLIP || k == GP_SEL_PICK_CYCLES || k == GP_SEL_PREP_CYCLES) ? solve_grid : 1));
     fprintf(stderr, "  (cycles: mean per workgroup; counts: totals)\n");
 }
 

@@ -236,7 +236,7 @@ enum GovProf { GP_EDGES, GP_PEEL, GP_GREEDY, GP_BFS, GP_TARJAN, GP_SINGLE, GP_DE
                GP_N_SEEDS, GP_N_BFS, GP_N_BFS_POPS, GP_N_DENSE_ROWS, GP_N_DENSE_MAX, GP_N_CORE, GP_N_BLOCKS, GP_N_BIG_ROWS,
                GP_N_SCC_SWEEPS, GP_N_SMALL_S, GP_FVS_SEL, GP_FVS_FORMS, GP_FVS_GJ,
                GP_N_FAIL_DEGEN, GP_N_FAIL_ORIENT, GP_N_FAIL_SINGULAR, GP_FAILED_CYCLES, GP_BFS_FLIP, GP_N_BFS_ITERS,
-               GP_N_FLIP_STEPS, GP_N };
+               GP_N_FLIP_STEPS, GP_N_SEL_BATCHES, GP_N_SEL_PICKS, GP_SEL_PICK_CYCLES, GP_SEL_PREP_CYCLES, GP_N };
 
 // Solver state for buckets of up to CMAX_ keys: LDS for GS_CMAX, a global
 // slab per workgroup for GB_CMAX (same code; indices fit int16 either way).
@@ -1013,12 +1013,15 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
                 }
             }
             __syncthreads();
+            pc.lap(GP_SEL_PREP_CYCLES);
             if (tid < 64) {
                 const uint32_t lane = tid;
-                uint32_t qh = 0, qt = L.qtail, nh = 0, maxlev = 1;
+                uint32_t qh = 0, qt = L.qtail, nh = 0, maxlev = 1, nbatch = 0, npick = 0;
+                uint64_t pick_cyc = 0;
                 bool fb = false;
                 for (;;) {
                     while (qh < qt) {
+                        ++nbatch;
                         const uint32_t nb = min(64u, qt - qh);
                         if (lane < nb) {
                             const uint32_t p = (uint32_t)queue[qh + lane];
@@ -1062,6 +1065,8 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
                     // bins the open members by in-degree (64 bins), a second
                     // takes every member above the threshold bin and the
                     // lowest-index ones of that bin.
+                    const uint64_t tpk = pc.acc ? clock64() : 0;
+                    ++npick;
                     const uint32_t want = 2 * min((uint32_t)GOV_PICK_REPS, (fvs_max - nh) / 2);
                     uint32_t *hb = L.hbin;
                     hb[lane] = 0;
@@ -1107,6 +1112,7 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
                         qt += got;
                         if (lane == 0) L.qtail = qt;
                         __builtin_amdgcn_wave_barrier();
+                        if (pc.acc) pick_cyc += clock64() - tpk;
                         continue;
                     }
                     // (64+ open members of in-degree >= 63 reach the
@@ -1165,6 +1171,9 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
                     L.nleft = nh;
                     L.rounds = maxlev + 1;
                     L.chg = fb ? 1u : 0u;
+                    pc.add(GP_N_SEL_BATCHES, nbatch);
+                    pc.add(GP_N_SEL_PICKS, npick);
+                    pc.add(GP_SEL_PICK_CYCLES, pick_cyc);
                 }
             }
             __syncthreads();

@@ -5,6 +5,7 @@ about a minute on the box's cores, size-independent properties and samples
 where it does not.
 
   C2  1e8 x 13 B, exact index, cb = 4      full host-buffer build + index.db
+                                            (pass loop and the F2 one-call form)
   C3  1e9 x 13 B, index.approximate = true  full build + index.db/index_a.db
   C4  13 193 787 549 x 13 B (README shape)  full-size histogram == oracle
   C5  4e9 var-len 8-64 B Zipf, cb = 16      full-size histogram == oracle,
@@ -174,6 +175,13 @@ def test_c2_exact_full_build_1e8(ctx, tmp_path):
     assert np.array_equal(np.fromfile(ip, ">u8"), exp)
     assert os.path.getsize(ap) == 0
     mph.close()
+    # F2 at C2 size: one call (ranks from the solve) writes the same index.db
+    ip2 = ip + ".f2"
+    m2 = ctx.mph_build_index_fixed(keys, 13, width, addr, ip2)
+    for x, y in zip(m2.export(), (E, vals, sb)):
+        np.testing.assert_array_equal(x, y)
+    assert np.array_equal(np.fromfile(ip2, ">u8"), exp)
+    m2.close()
     shutil.rmtree(os.path.dirname(ip), ignore_errors=True)
 
 
