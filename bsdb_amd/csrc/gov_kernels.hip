@@ -1023,14 +1023,27 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
                     while (qh < qt) {
                         ++nbatch;
                         const uint32_t nb = min(64u, qt - qh);
+                        uint32_t x0 = 0, x1 = 0;
                         if (lane < nb) {
                             const uint32_t p = (uint32_t)queue[qh + lane];
                             for (int t = 0; t < 3; ++t) {
                                 const int d = idep[3 * p + t];
                                 if (d >= 0) atomicSub(&indeg[d], 1u);
                             }
-                            for (uint32_t x = roff[p]; x < roff[p + 1]; ++x) {
-                                const uint32_t i = (uint32_t)rev[x];
+                            x0 = roff[p];
+                            x1 = roff[p + 1];
+                        }
+                        // the batch's dependents, one per lane per step; the
+                        // members they make ready are appended in lane order
+                        // by ballot (the ready closure, the levels and so the
+                        // heavy set do not depend on the queue order)
+                        for (uint32_t x = x0;; ++x) {
+                            const bool act = x < x1;
+                            if (__builtin_amdgcn_ballot_w64(act) == 0) break;
+                            bool ready = false;
+                            uint32_t i = 0;
+                            if (act) {
+                                i = (uint32_t)rev[x];
                                 if (atomicSub(&pend[i], 1u) == 1u && st[i] == 0) {  // last dependency placed (not heavy)
                                     int lev = 0;
                                     for (int t = 0; t < 3; ++t) {
@@ -1040,14 +1053,19 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
                                     rnd[i] = (int16_t)(lev + 1);
                                     st[i] = 1;
                                     maxlev = max(maxlev, (uint32_t)lev + 1);
-                                    queue[atomicAdd(&L.qtail, 1u)] = (int16_t)i;
+                                    ready = true;
                                 }
                             }
+                            const uint64_t rm = __builtin_amdgcn_ballot_w64(ready);
+                            if (ready)
+                                queue[qt + __builtin_amdgcn_mbcnt_hi((uint32_t)(rm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)rm, 0u))] = (int16_t)i;
+                            qt += (uint32_t)__builtin_popcountll(rm);
                         }
                         qh += nb;
                         __builtin_amdgcn_wave_barrier();
-                        qt = L.qtail;
                     }
+                    if (lane == 0) L.qtail = qt;
+                    __builtin_amdgcn_wave_barrier();
                     if (qt >= sz) break;  // every member placed (each enters the queue once)
                     // a pick adds up to 2 heavy hinges: the heavy set stays
                     // <= fvs_max, so forms and heavy rows (constant column
