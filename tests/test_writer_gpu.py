@@ -124,3 +124,27 @@ def test_build_index_in_one_call_equals_the_pass_loop(tmp_path, var, approx, n):
         assert open(a, "rb").read() == open(b, "rb").read()
     assert os.path.getsize(ip1) == 8 * n and os.path.getsize(ap1) == (8 * n if approx else 0)
     m1.close(); m2.close(); ctx.close()
+
+
+def test_empty_key_set(tmp_path):
+    """n = 0 (a writer with no records): m = 1, E = [0, 0], empty index files,
+    through both the pass loop and the one-call form."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from bsdb_amd import Context
+    ctx = Context(0)
+    keys = np.zeros(0, np.uint8)
+    addr = np.zeros(0, np.uint64)
+    m1 = ctx.mph_build_index_fixed(keys, 13, 4, addr, str(tmp_path / "a.db"), str(tmp_path / "aa.db"))
+    E, vals, sb = m1.export()
+    assert list(E) == [0, 0]
+    assert os.path.getsize(tmp_path / "a.db") == 0 and os.path.getsize(tmp_path / "aa.db") == 0
+    m2 = ctx.mph_build_fixed(keys, 13, 4)
+    passes = m2.write_index(str(tmp_path / "b.db"), str(tmp_path / "ba.db"), False, 1 << 30, lambda w: None)
+    assert passes == 0 and os.path.getsize(tmp_path / "b.db") == 0
+    m2.dump(str(tmp_path / "h.dump"))
+    m3 = ctx.mph_load(str(tmp_path / "h.dump"))
+    assert list(m3.export()[0]) == [0, 0]
+    for m in (m1, m2, m3):
+        m.close()
+    ctx.close()
