@@ -99,13 +99,16 @@ class OracleBuild:
         return torch.from_numpy(idx.view(np.int64).copy())
 
 
-def _e4_worker(rank, world, port, n, width, path, q, use_gpu):
+def _e4_worker(rank, world, port, n, width, path, q, use_gpu, pg="gloo"):
     import sys
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle"))
     import oracle as O
     from bsdb_amd.distributed import DeviceBuild, sharded_full_build, write_index_slice
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    if pg == "nccl":
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", 0))
+    else:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
     lo, hi = shard(n, rank, world)
     keys = O.gen_keys13(lo, hi - lo)
     addr = torch.arange(lo, hi, dtype=torch.int64) * 48 + 4096
@@ -130,12 +133,12 @@ def _e4_worker(rank, world, port, n, width, path, q, use_gpu):
     dist.destroy_process_group()
 
 
-def run_e4(world, n, width, tmp_path, use_gpu):
+def run_e4(world, n, width, tmp_path, use_gpu, pg="gloo"):
     path = str(tmp_path / f"index_{world}.db")
-    port = 29700 + world * 11 + os.getpid() % 400 + (50 if use_gpu else 0)
+    port = 29700 + world * 11 + os.getpid() % 400 + (50 if use_gpu else 0) + (25 if pg == "nccl" else 0)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    ps = [ctx.Process(target=_e4_worker, args=(r, world, port, n, width, path, q, use_gpu)) for r in range(world)]
+    ps = [ctx.Process(target=_e4_worker, args=(r, world, port, n, width, path, q, use_gpu, pg)) for r in range(world)]
     for p in ps:
         p.start()
     res = dict(q.get(timeout=300) for _ in ps)
@@ -175,3 +178,13 @@ def test_gloo_multi_gpu_full_build_hip_ranks(tmp_path):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     run_e4(2, 600_001, 4, tmp_path, use_gpu=True)
+
+
+@pytest.mark.gpu
+def test_nccl_full_build_device_tensors(tmp_path):
+    """E4's RCCL code path (device tensors straight into all_to_all_single,
+    all_gather and the int64 sum-reduce) on a one-rank NCCL group: RCCL
+    refuses two ranks on one GPU, so this is as far as a one-GPU box goes."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    run_e4(1, 400_003, 4, tmp_path, use_gpu=True, pg="nccl")
