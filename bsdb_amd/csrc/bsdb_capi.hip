@@ -227,11 +227,12 @@ struct D13Sel {
     bool binned;        // runs padded to 8 ids, region copies = d13_copies
     uint32_t bin_ids;   // binned: ids per LDS bin buffer
 };
-D13Sel d13_select(const bsdb_ctx *c, bool var = false, uint32_t key_len = 13) {
+D13Sel d13_select(const bsdb_ctx *c, bool var = false, uint32_t key_len = 13, bool seed0 = false) {
     if (!var && key_len != 13)  // every other fixed length: the var-len kernel on k * L offsets
-        return {k_pass1_vare<0, true>, VARE_NT, VARE_TILE, VARE_MAXP, true, VARE_BIN_IDS};
+        return {seed0 ? k_pass1_vare<0, true, true> : k_pass1_vare<0, true>, VARE_NT, VARE_TILE, VARE_MAXP, true,
+                VARE_BIN_IDS};
     if (var) {
-        D13Kernel k = k_pass1_vare<0, false>;
+        D13Kernel k = seed0 ? k_pass1_vare<0, false, true> : k_pass1_vare<0, false>;
         if (c->d13_variant == 1) k = k_pass1_vare<1, false>;
         if (c->d13_variant == 4) k = k_pass1_vare<4, false>;
         if (c->d13_variant == 5) k = k_pass1_vare<5, false>;
@@ -244,7 +245,8 @@ D13Sel d13_select(const bsdb_ctx *c, bool var = false, uint32_t key_len = 13) {
         case 2:
             if (c->d13_threads == 256) return {k_pass1_d13<256>, 256, 256 * P1_KEYS_PER_THREAD, 512, false, 0};
             return {k_pass1_d13<512>, 512, 512 * P1_KEYS_PER_THREAD, 1024, false, 0};
-        default: return {k_pass1_d13e<0>, D13E_NT, D13E_TILE, D13E_MAXP, true, D13E_BIN_IDS};
+        default:
+            return {seed0 ? k_pass1_d13e<0, true> : k_pass1_d13e<0>, D13E_NT, D13E_TILE, D13E_MAXP, true, D13E_BIN_IDS};
     }
 }
 
@@ -320,7 +322,7 @@ int histogram_impl(bsdb_ctx *c, const uint8_t *keys, const uint64_t *offsets, ui
     chunk = std::max<uint64_t>(P1_TILE, chunk / P1_TILE * P1_TILE);
     chunk = std::min<uint64_t>(chunk, (n + P1_TILE - 1) / P1_TILE * P1_TILE);
     // the persistent kernels: 13-byte keys and variable-length keys
-    D13Sel sel = d13_select(c, var, key_len);
+    D13Sel sel = d13_select(c, var, key_len, seed == 0 && !getenv("BSDB_NO_SEED0"));  // (A/B switch for measurements)
     uint32_t bsh = 0, nb = 0, cb = 0;
     const bool fixed_other = !var && key_len != 13;
     // (fixed keys over 32 B: a 128-key group would overflow the var-len

@@ -591,8 +591,11 @@ constexpr uint16_t ID_PAD = 0xFFFF;                       // not a local id (ids
 // VARIANT 0 is production.  Profiling only (results invalid): 1 = hash and
 // bins, no cursor atomics and no write-out; 4 = per-wave phase cycles
 // (s_memtime) written over counts[8*wave ..] (tools/stamp_probe_e.py).
-template <int VARIANT>
+template <int VARIANT, bool SEED0 = false>
 __global__ __launch_bounds__(D13E_NT, 1) void k_pass1_d13e(P1Args a, uint64_t ntiles) {
+    // SEED0: the seed is 0 (every BSDBWriter build, CBHS:209): the hash's
+    // seed terms fold at compile time
+    const uint64_t seed = SEED0 ? 0ull : a.seed;
     constexpr int NT = D13E_NT, NW = D13E_NW, TILE = D13E_TILE;
     __shared__ __align__(16) uint16_t bins[2][D13E_BIN_IDS];
     __shared__ uint32_t cnt[2][D13E_MAXP];
@@ -630,7 +633,7 @@ __global__ __launch_bounds__(D13E_NT, 1) void k_pass1_d13e(P1Args a, uint64_t nt
             const uint32_t kt = tid + (q * D13_Q + j) * NT;
             const uint32_t sh = ((kt * 13u) & 3u) * 8u;  // tile0*13 is a multiple of 4
             W64 s0, s1;
-            spooky13_u(S[q][j].x, S[q][j].y, S[q][j].z, S[q][j].w, sh, a.seed, s0, s1);
+            spooky13_u(S[q][j].x, S[q][j].y, S[q][j].z, S[q][j].w, sh, seed, s0, s1);
             const uint32_t b = bucket_of_w(s0, mult);
             const uint32_t p = b >> bsh;
             const uint32_t r = atomicAdd(&cnt[cur][p], 1u);
@@ -812,8 +815,9 @@ __device__ __forceinline__ uint64_t vare_sig0_global(const uint32_t *src, uint64
 
 // FIXED: keys of a.key_len bytes each, no offsets array (key k at k * L):
 // the same kernel serves every fixed length but 13 (k_pass1_d13e).
-template <int VARIANT, bool FIXED>
+template <int VARIANT, bool FIXED, bool SEED0 = false>
 __global__ __launch_bounds__(VARE_NT, 4) void k_pass1_vare(P1Args a, uint64_t ntiles) {
+    const uint64_t seed = SEED0 ? 0ull : a.seed;  // (as k_pass1_d13e)
     constexpr int NT = VARE_NT, NW = VARE_NW, TILE = VARE_TILE, NG = VARE_NG;
     __shared__ __align__(16) uint16_t bins[VARE_BIN_IDS];
     __shared__ uint32_t cnt[2][VARE_MAXP];  // rank counters, by tile parity
@@ -905,8 +909,8 @@ __global__ __launch_bounds__(VARE_NT, 4) void k_pass1_vare(P1Args a, uint64_t nt
     // signature word 0 of the key at blob offset pos (the general path)
     auto sig0_of = [&](uint64_t pos, uint32_t len, uintptr_t lo, uint32_t nvec, bool staged) __attribute__((always_inline)) {
         const uint64_t o = blob + pos - lo;
-        if (staged) return vare_sig0_lds(stage, (uint32_t)o, len, a.seed);
-        return vare_sig0_global(reinterpret_cast<const uint32_t *>(a.keys + (lo - blob)), 4 * (uint64_t)nvec, o, len, a.seed);
+        if (staged) return vare_sig0_lds(stage, (uint32_t)o, len, seed);
+        return vare_sig0_global(reinterpret_cast<const uint32_t *>(a.keys + (lo - blob)), 4 * (uint64_t)nvec, o, len, seed);
     };
     // bin inserts, software-pipelined: the rank atomics of a group are issued
     // after its hash and the ids stored during the next group (after its key
@@ -963,13 +967,13 @@ __global__ __launch_bounds__(VARE_NT, 4) void k_pass1_vare(P1Args a, uint64_t nt
         if (__builtin_amdgcn_ballot_w64(len >= 16) == 0) {  // wave-uniform
             uint32_t d[5];
             read_key(b, std::integral_constant<int, 5>{}, d);
-            s0 = spooky_lt16_sig0(d, sh, len, a.seed);
+            s0 = spooky_lt16_sig0(d, sh, len, seed);
         } else if (len <= 64) {
             uint32_t d[17];
             read_key(b, std::integral_constant<int, 17>{}, d);
-            s0 = spooky_le64_sig0(d, sh, len, a.seed);
+            s0 = spooky_le64_sig0(d, sh, len, seed);
         } else {
-            s0 = vare_sig0_lds(stage, o, len, a.seed);
+            s0 = vare_sig0_lds(stage, o, len, seed);
         }
         return s0;
     };
