@@ -616,29 +616,49 @@ __global__ __launch_bounds__(D13E_NT, 1) void k_pass1_d13e(P1Args a, uint64_t nt
     const uint32_t my_p = owner ? (uint32_t)w * PPW + l : P;  // P = none
 
     u32x4a S[4][D13_Q];
+    // Key kt of a tile starts at byte 13 * kt of it; tile, quarter and key
+    // slot offsets (multiples of 13 * NT = 13312) are multiples of 4, so a
+    // lane's 4-byte-aligned window offset and its byte shift are the same
+    // for every key it loads: the address is a uniform base (scalar
+    // arithmetic) + one 32-bit lane offset, no per-key VALU.
+    const uint32_t lane_off = ((uint32_t)tid * 13u) & ~3u;
+    const uint32_t sh = (((uint32_t)tid * 13u) & 3u) * 8u;
+    static_assert((NT * 13) % 4 == 0 && ((uint64_t)TILE * 13) % 4 == 0, "window alignment per lane");
     // unconditional loads (past the last tile they re-read tile t0): keeps
     // the compiler's waitcnt bookkeeping free of merged paths
+    // Buffer loads through a per-tile descriptor (built by scalar code): the
+    // lane offset is the voffset, the key slot's offset the soffset, so a
+    // load costs no VALU (the flat form spent a 64-bit add per load).
+    // aux 2 = nt (streamed once, as __builtin_nontemporal_load).
     auto load_q = [&](int q, uint64_t tt) {
         const uint64_t ts = tt < ntiles ? tt : t0;
+        const uint8_t *tb = a.keys + ts * ((uint64_t)TILE * 13);
+        const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(tb), 0, TILE * 13 + 16, 0x00020000);
 #pragma unroll
         for (int j = 0; j < D13_Q; ++j) {
-            const uint64_t byte = (ts * TILE + tid + (q * D13_Q + j) * NT) * 13;
-            S[q][j] = __builtin_nontemporal_load(reinterpret_cast<const u32x4a *>(a.keys + (byte & ~3ULL)));
+            const auto v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, lane_off, (q * D13_Q + j) * NT * 13, 2);
+            S[q][j] = u32x4a{v[0], v[1], v[2], v[3]};
         }
     };
     bool ovf = false;
+    // the quarter's D13_Q keys hashed first, then their rank atomics issued
+    // together and their ids stored: one LDS round trip per quarter
     auto hash_q = [&](int q, uint32_t cur) {
+        uint32_t b[D13_Q], r[D13_Q];
 #pragma unroll
         for (int j = 0; j < D13_Q; ++j) {
-            const uint32_t kt = tid + (q * D13_Q + j) * NT;
-            const uint32_t sh = ((kt * 13u) & 3u) * 8u;  // tile0*13 is a multiple of 4
             W64 s0, s1;
             spooky13_u(S[q][j].x, S[q][j].y, S[q][j].z, S[q][j].w, sh, seed, s0, s1);
-            const uint32_t b = bucket_of_w(s0, mult);
-            const uint32_t p = b >> bsh;
-            const uint32_t r = atomicAdd(&cnt[cur][p], 1u);
+            b[j] = bucket_of_w(s0, mult);
+        }
+#pragma unroll
+        for (int j = 0; j < D13_Q; ++j) r[j] = atomicAdd(&cnt[cur][b[j] >> bsh], 1u);
+#pragma unroll
+        for (int j = 0; j < D13_Q; ++j) {
             // branch-free: an overflowing bin (flagged below) reuses its last slot
-            bins[cur][p * CAPB + (r < CAPB ? r : CAPB - 1)] = (uint16_t)(b & (PART_BUCKETS - 1));
+            const uint32_t slot = __umul24(b[j] >> bsh, CAPB) + min(r[j], CAPB - 1u);  // (v_mad_u32_u24 + v_min)
+            __builtin_assume(slot < (uint32_t)D13E_BIN_IDS);
+            bins[cur][slot] = (uint16_t)(b[j] & (PART_BUCKETS - 1));
         }
     };
     // owner state of the previous tile: padded count and cursor base of my_p
@@ -929,7 +949,7 @@ __global__ __launch_bounds__(VARE_NT, 4) void k_pass1_vare(P1Args a, uint64_t nt
         if (pend) {
 #pragma unroll
             for (int k = 0; k < 2; ++k)
-                bins[pend_p[k] * CAPB + (pend_rk[k] < CAPB ? pend_rk[k] : CAPB - 1)] = pend_id[k];
+                bins[__umul24(pend_p[k], CAPB) + min(pend_rk[k], CAPB - 1u)] = pend_id[k];
         }
         pend = false;
     };
