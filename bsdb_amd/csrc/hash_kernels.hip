@@ -1326,6 +1326,8 @@ __global__ __launch_bounds__(P2_THREADS, 1) void k_pass2b(P2Layout L, const uint
         }
         __syncthreads();
     };
+    const uint32_t sink = PART_BUCKETS + (tid & 63);
+    static_assert(PART_BUCKETS + 64 <= 0xFFFF, "pads sort above the sinks");
     int64_t cur_p = -1;
     for (uint32_t k = k_start; k < NI; ++k) {
         const uint64_t pk = pref[k], pk1 = pref[k + 1];
@@ -1342,7 +1344,9 @@ __global__ __launch_bounds__(P2_THREADS, 1) void k_pass2b(P2Layout L, const uint
         const uint64_t a8 = min(b, (a + 7) & ~7ULL), b8 = max(a8, b & ~7ULL);
         // an id with the top bit set is a pad (ID_PAD): it goes to a per-lane
         // sink word (pads of one wave on one word would serialise)
-        auto add_id = [&](uint32_t id) { atomicAdd(&hist[id < 0x8000u ? id : PART_BUCKETS + (tid & 63)], 1u); };
+        // (pads are 0xFFFF > every sink index > every id: one v_min, which the
+        // compiler folds with the 16-bit extraction into an SDWA operand)
+        auto add_id = [&](uint32_t id) { atomicAdd(&hist[min(id, sink)], 1u); };
         if (a + tid < a8) add_id(src[a + tid]);
         if (b8 + tid < b) add_id(src[b8 + tid]);
         const uint4 *v = reinterpret_cast<const uint4 *>(src);
