@@ -646,11 +646,7 @@ __global__ __launch_bounds__(D13E_NT, 1) void k_pass1_d13e(P1Args a, uint64_t nt
     auto hash_q = [&](int q, uint32_t cur) {
         uint32_t b[D13_Q], r[D13_Q];
 #pragma unroll
-        for (int j = 0; j < D13_Q; ++j) {
-            W64 s0, s1;
-            spooky13_u(S[q][j].x, S[q][j].y, S[q][j].z, S[q][j].w, sh, seed, s0, s1);
-            b[j] = bucket_of_w(s0, mult);
-        }
+        for (int j = 0; j < D13_Q; ++j) b[j] = spooky13_bucket(S[q][j].x, S[q][j].y, S[q][j].z, S[q][j].w, sh, seed, mult);
 #pragma unroll
         for (int j = 0; j < D13_Q; ++j) r[j] = atomicAdd(&cnt[cur][b[j] >> bsh], 1u);
 #pragma unroll

@@ -185,10 +185,21 @@ __device__ __forceinline__ uint64_t rotl_u(uint64_t x) {
     return ((uint64_t)r.hi << 32) | r.lo;
 }
 #define BSDB_END_STEP_U(D, C, K) D ^= C; C = rotl_u<K>(C); D = add_u(D, C);
+// D += C rotated by 32 with the halves crossed in the carry chain (2 VALU)
+// instead of swapping C into a register pair first (2 moves + the add)
+__device__ __forceinline__ uint64_t add_swapped(uint64_t d, uint64_t c) {
+    unsigned int cy;
+    const uint32_t lo = __builtin_addc((uint32_t)d, (uint32_t)(c >> 32), 0u, &cy);
+    const uint32_t hi = __builtin_addc((uint32_t)(d >> 32), (uint32_t)c, cy, &cy);
+    return ((uint64_t)hi << 32) | lo;
+}
 __device__ __forceinline__ void short_end_u(uint64_t &h0, uint64_t &h1, uint64_t &h2, uint64_t &h3) {
     BSDB_END_STEP_U(h3, h2, 15) BSDB_END_STEP_U(h0, h3, 52) BSDB_END_STEP_U(h1, h0, 26)
     BSDB_END_STEP_U(h2, h1, 51) BSDB_END_STEP_U(h3, h2, 28) BSDB_END_STEP_U(h0, h3, 9)
-    BSDB_END_STEP_U(h1, h0, 47) BSDB_END_STEP_U(h2, h1, 54) BSDB_END_STEP_U(h3, h2, 32)
+    BSDB_END_STEP_U(h1, h0, 47) BSDB_END_STEP_U(h2, h1, 54)
+    h3 ^= h2;  // step 9, K = 32
+    h3 = add_swapped(h3, h2);
+    h2 = rotl_u<32>(h2);
     BSDB_END_STEP_U(h0, h3, 25) BSDB_END_STEP_U(h1, h0, 63)
 }
 #undef BSDB_END_STEP_U
@@ -338,6 +349,30 @@ __device__ __forceinline__ uint32_t bucket_of_w(W64 sig0, uint32_t mult) {
     const uint32_t xl = __builtin_amdgcn_alignbit(sig0.hi, sig0.lo, 1);
     const uint32_t xh = sig0.hi >> 1;
     const uint64_t t = (uint64_t)xh * mult + __umulhi(xl, mult);
+    return (uint32_t)(t >> 32);
+}
+
+// The bucket of a 13-byte key straight from the hash (the histogram needs
+// nothing else): ShortEnd up to h0's last rotation, then x = sig0 >>> 1 from
+// the unrotated word h (sig0 = rotl(h, 63) = h >>> 1 | h << 63, so x =
+// h >>> 2 | (h & 1) << 62): 3 VALU instead of the rotation's 2 plus 2.
+__device__ __forceinline__ uint32_t spooky13_bucket(uint32_t d0, uint32_t d1, uint32_t d2, uint32_t d3, uint32_t sh,
+                                                    uint64_t seed, uint32_t mult) {
+    const uint64_t w0 = ((uint64_t)__builtin_amdgcn_alignbit(d2, d1, sh) << 32) | __builtin_amdgcn_alignbit(d1, d0, sh);
+    const uint64_t w1 = ((uint64_t)((d3 >> sh) & 0xFFu) << 32) | __builtin_amdgcn_alignbit(d3, d2, sh);
+    uint64_t h0 = seed + 13 * 8, h1 = seed, h2 = add_u(SC, w0), h3 = add_u(SC, w1);
+#define BSDB_END_STEP_U(D, C, K) D ^= C; C = rotl_u<K>(C); D = add_u(D, C);
+    BSDB_END_STEP_U(h3, h2, 15) BSDB_END_STEP_U(h0, h3, 52) BSDB_END_STEP_U(h1, h0, 26)
+    BSDB_END_STEP_U(h2, h1, 51) BSDB_END_STEP_U(h3, h2, 28) BSDB_END_STEP_U(h0, h3, 9)
+    BSDB_END_STEP_U(h1, h0, 47) BSDB_END_STEP_U(h2, h1, 54)
+    h3 ^= h2;
+    h3 = add_swapped(h3, h2);
+    BSDB_END_STEP_U(h0, h3, 25)
+#undef BSDB_END_STEP_U
+    const uint32_t hl = (uint32_t)h0, hh = (uint32_t)(h0 >> 32);
+    const uint32_t xl = __builtin_amdgcn_alignbit(hh, hl, 2);
+    const uint32_t xh = __builtin_amdgcn_alignbit(hl, hh, 2) & 0x7FFFFFFFu;
+    const uint64_t t = (uint64_t)xh * mult + __umulhi(xl, mult);  // GOV:559, as bucket_of_w
     return (uint32_t)(t >> 32);
 }
 
