@@ -1,0 +1,14 @@
+#!/bin/bash
+# One GPU call: the whole -m gpu suite, the bench line, the rocprofv3 kernel-trace summary.
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+OUT=gpurun_out/${TAG:-round}; mkdir -p $OUT
+timeout -k 10 500 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 || { tail -n 40 $OUT/pytest_gpu.log; exit 1; }
+tail -n 2 $OUT/pytest_gpu.log
+[ -n "$NOBENCH" ] && exit 0
+timeout -k 10 400 python -u bench.py --steps 10 --warmup 3 > $OUT/bench.json 2> $OUT/bench.err || { tail -n 20 $OUT/bench.err; exit 2; }
+tail -n 1 $OUT/bench.json | cut -c1-400
+[ -n "$NOPROF" ] && exit 0
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/prof -o bench --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu > $OUT/prof_bench.json 2> $OUT/prof_bench.err || { tail -n 20 $OUT/prof_bench.err; exit 3; }
+find $OUT/prof -name "*kernel_stats.csv" -exec cp {} $OUT/kernel_stats.csv \;
+head -n 12 $OUT/kernel_stats.csv | cut -c1-160
