@@ -1,8 +1,8 @@
-"""Per-launch HBM traffic of k_pass1_d13 from separate rocprofv3 --pmc passes.
+"""Per-launch HBM traffic of the pass-1 kernel (k_pass1_d13e) from separate rocprofv3 --pmc passes.
 
 gfx950 corrections (MI355X_MICROARCH.md §HBM): FETCH_SIZE reports half the
 bytes of a wide coalesced streaming read -> x2; WRITE_SIZE is exact for
-16-B/lane streams (our 2-byte id stores: taken as reported).  Units KiB.
+16-B/lane streams (the 16-B id-run stores).  Units KiB.
 usage: python tools/pmc_traffic.py FETCH_CSV WRITE_CSV OUT_JSON"""
 import csv, json, sys
 
@@ -18,7 +18,7 @@ write = per_dispatch(sys.argv[2], "WRITE_SIZE")
 n = 13_193_787_549
 launches = len(fetch)
 out = {
-    "kernel": "k_pass1_d13 (+ its bounds-checked tail launch reads ~0)",
+    "kernel": "k_pass1_d13e (the bench's pass-1 launches)",
     "launches_per_step": launches,
     "keys_per_launch": n / launches,
     "read_bytes_per_launch": 2 * sum(fetch) / launches,
