@@ -7,6 +7,8 @@
 #include <hip/hip_runtime.h>
 
 #include <dlfcn.h>
+#include <fcntl.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <atomic>
@@ -1202,3 +1204,4 @@ int bsdb_hash_var(bsdb_ctx *c, const uint8_t *h_blob, const uint64_t *h_off, uin
 
 #include "capi_comm.hip"
 #include "capi_mph.hip"
+#include "capi_multi.hip"

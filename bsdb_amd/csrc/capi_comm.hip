@@ -206,6 +206,14 @@ int multi_histogram(bsdb_multi *mc, uint64_t n, uint64_t *h_E, ShardFn &&shard) 
     if (m > 0x7FFFFFFFULL) return BSDB_EINVAL;
     const Rccl *r = rccl();
     if (!r) return BSDB_ECOMM;
+    if (!mc->comms[0]) {
+        std::vector<int> devs(k);
+        for (int i = 0; i < k; ++i) devs[i] = mc->ctx[i]->device;
+        if (r->comm_init_all(mc->comms.data(), k, devs.data()) != 0) {
+            mc->comms.assign(k, nullptr);
+            return BSDB_ECOMM;
+        }
+    }
     int rc = multi_grow(mc, m);
     if (rc) return rc;
     std::vector<int> rcs(k, BSDB_OK);
@@ -286,8 +294,6 @@ extern "C" {
 int bsdb_multi_open(int ndev, const int *devices, bsdb_multi **out) {
     if (!out || ndev < 1 || ndev > 64) return BSDB_EINVAL;
     *out = nullptr;
-    const Rccl *r = rccl();
-    if (!r) return BSDB_ECOMM;
     bsdb_multi *mc = new (std::nothrow) bsdb_multi();
     if (!mc) return BSDB_ENOMEM;
     std::vector<int> devs(ndev);
@@ -303,11 +309,8 @@ int bsdb_multi_open(int ndev, const int *devices, bsdb_multi **out) {
             return rc;
         }
     }
-    if (r->comm_init_all(mc->comms.data(), ndev, devs.data()) != 0) {
-        mc->comms.assign(ndev, nullptr);
-        bsdb_multi_close(mc);
-        return BSDB_ECOMM;
-    }
+    // the RCCL communicator is created by the first call that needs it (the
+    // histogram's all-reduce); the full build exchanges device to device
     for (int i = 0; i < ndev; ++i) {
         mc->ctx[i]->nranks = ndev;
         mc->ctx[i]->rank = i;

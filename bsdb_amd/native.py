@@ -69,6 +69,10 @@ SIGNATURES = [
     ("bsdb_multi_ctx", _i, [_vp, _i, C.POINTER(_vp)]),
     ("bsdb_multi_histogram_fixed", _i, [_vp, _vp, _u32, _u64, _u64, _vp]),
     ("bsdb_multi_histogram_var", _i, [_vp, _vp, _vp, _u64, _u64, _vp]),
+    ("bsdb_multi_mph_build_index_fixed", _i, [_vp, _vp, _u32, _u64, _u32, _vp, _vp, _vp, _i, C.c_char_p, C.c_char_p,
+                                              _vp, _vp, _vp]),
+    ("bsdb_multi_mph_build_index_var", _i, [_vp, _vp, _vp, _u64, _u32, _vp, _vp, _vp, _i, C.c_char_p, C.c_char_p,
+                                            _vp, _vp, _vp]),
     ("bsdb_mph_build_fixed", _i, [_vp, _vp, _u32, _u64, _u32, C.POINTER(_vp)]),
     ("bsdb_mph_build_var", _i, [_vp, _vp, _vp, _u64, _u32, C.POINTER(_vp)]),
     ("bsdb_mph_build_index_fixed", _i, [_vp, _vp, _u32, _u64, _u32, _vp, _vp, _vp, _i, C.c_char_p, C.c_char_p,
@@ -669,3 +673,46 @@ class Multi:
         _check("bsdb_multi_histogram_var", lib().bsdb_multi_histogram_var(
             self._h, blob_np.ctypes.data, off_np.ctypes.data, n, seed & (2**64 - 1), E.ctypes.data))
         return E
+
+    def _build_outputs(self, n: int, width: int):
+        import numpy as np
+        E = np.zeros(n // 1500 + 2, np.uint64)
+        vals = np.zeros(int(lib().bsdb_values_words(n)), np.uint64)
+        sb = np.zeros((n * width + 63) // 64 + 1, np.uint64) if width else None
+        return E, vals, sb
+
+    def mph_build_index_fixed(self, keys_np, key_len: int, width: int, addr_np=None, index_path: Optional[str] = None,
+                              index_a_path: Optional[str] = None, approximate: bool = False, value8_np=None,
+                              vlen_np=None):
+        """E4 over this process's devices (bsdb_multi_mph_build_index_fixed):
+        the structure's fields (E, values, sigbits) as host arrays -- the same
+        as Mph.export() of a one-device build -- and, with index_path, the
+        index files written by every device at its slice's offset."""
+        import numpy as np
+        keys_np = np.ascontiguousarray(keys_np, np.uint8)
+        n = keys_np.size // key_len
+        addr_np, v8, vl = (Context._records_args(n, addr_np, value8_np, vlen_np, approximate) if index_path
+                           else (None, None, None))
+        E, vals, sb = self._build_outputs(n, width)
+        _check("bsdb_multi_mph_build_index_fixed", lib().bsdb_multi_mph_build_index_fixed(
+            self._h, keys_np.ctypes.data, key_len, n, width, _np_ptr(addr_np), _np_ptr(v8), _np_ptr(vl),
+            1 if approximate else 0, index_path.encode() if index_path else None,
+            index_a_path.encode() if index_a_path else None, E.ctypes.data, vals.ctypes.data, _np_ptr(sb)))
+        return E, vals, sb
+
+    def mph_build_index_var(self, blob_np, off_np, width: int, addr_np=None, index_path: Optional[str] = None,
+                            index_a_path: Optional[str] = None, approximate: bool = False, value8_np=None,
+                            vlen_np=None):
+        blob_np, off_np, n = Context._var_host_args(blob_np, off_np)
+        addr_np, v8, vl = (Context._records_args(n, addr_np, value8_np, vlen_np, approximate) if index_path
+                           else (None, None, None))
+        E, vals, sb = self._build_outputs(n, width)
+        _check("bsdb_multi_mph_build_index_var", lib().bsdb_multi_mph_build_index_var(
+            self._h, blob_np.ctypes.data, off_np.ctypes.data, n, width, _np_ptr(addr_np), _np_ptr(v8), _np_ptr(vl),
+            1 if approximate else 0, index_path.encode() if index_path else None,
+            index_a_path.encode() if index_a_path else None, E.ctypes.data, vals.ctypes.data, _np_ptr(sb)))
+        return E, vals, sb
+
+
+def _np_ptr(a):
+    return a.ctypes.data if a is not None else None

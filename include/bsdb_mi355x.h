@@ -257,7 +257,8 @@ int bsdb_dev_allreduce_u64(bsdb_ctx *ctx, uint64_t *d_buf, uint64_t count, void 
 /* ---------------------------------------------------------------------------
  * B4: all the devices of one process (the reference's build runs in ONE JVM,
  * SURVEY.md §2.1), one bsdb_ctx per device and an RCCL communicator over them
- * (ncclCommInitAll).  devices == NULL means 0..ndev-1.  The host-buffer calls
+ * (ncclCommInitAll, created by the first histogram call; the full build below
+ * does not use it).  devices == NULL means 0..ndev-1.  The host-buffer calls
  * shard the keys in input order over the devices (one host thread per device,
  * each copying over its own PCIe link), histogram the shards, all-reduce the
  * counts with ONE collective and return E[0..m] (u64, offsets only) in h_E.
@@ -271,6 +272,31 @@ int bsdb_multi_histogram_fixed(bsdb_multi *mc, const uint8_t *h_keys, uint32_t k
                                uint64_t *h_E);
 int bsdb_multi_histogram_var(bsdb_multi *mc, const uint8_t *h_blob, const uint64_t *h_off, uint64_t n,
                              uint64_t seed, uint64_t *h_E);
+/* E4: the whole build over every device of the process --
+ * the single-device F2 call bsdb_mph_build_index_* with the key set sharded
+ * over the devices.  Device g owns the buckets [g*m/G, (g+1)*m/G) (a sig0
+ * range, CBHS:129-138; buckets are independent, GOV:405-448): each device
+ * hashes its input-order shard, groups the signatures (and the records' addr /
+ * value8 / vlen) by owner, ONE device-to-device exchange delivers them (xGMI
+ * peer copies), each owner solves its range (bsdb_dev_gov_build_range, the
+ * solve returning every key's rank) and writes its index slots [e_lo, e_lo +
+ * n_g) at byte 8*e_lo of index.db (and index_a.db) in writes of <= 128 MiB.
+ * Outputs the assembled structure in host arrays sized as bsdb_mph_export's:
+ * h_E[num_buckets+1], h_values[bsdb_values_words(n)], h_sigbits[(n*width+63)/64
+ * + 1] (NULL when width == 0) -- the fields of
+ * GOVMinimalPerfectHashFunctionModified (GOV:284-313); bit-identical to the
+ * one-device build, and the index files byte-identical.  index_path NULL: the
+ * MPHF only (records ignored).  A device may be listed more than once (the
+ * exchange is then a copy within it). */
+int bsdb_multi_mph_build_index_fixed(bsdb_multi *mc, const uint8_t *h_keys, uint32_t key_len, uint64_t n,
+                                     uint32_t width, const uint64_t *h_addr, const uint64_t *h_value8,
+                                     const uint8_t *h_vlen, int approximate, const char *index_path,
+                                     const char *index_a_path, uint64_t *h_E, uint64_t *h_values,
+                                     uint64_t *h_sigbits);
+int bsdb_multi_mph_build_index_var(bsdb_multi *mc, const uint8_t *h_blob, const uint64_t *h_off, uint64_t n,
+                                   uint32_t width, const uint64_t *h_addr, const uint64_t *h_value8,
+                                   const uint8_t *h_vlen, int approximate, const char *index_path,
+                                   const char *index_a_path, uint64_t *h_E, uint64_t *h_values, uint64_t *h_sigbits);
 
 /* ---------------------------------------------------------------------------
  * A14/A15 + F1/F4 from host buffers: a GOV MPHF built on and resident on one

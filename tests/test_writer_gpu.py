@@ -148,3 +148,51 @@ def test_empty_key_set(tmp_path):
     for m in (m1, m2, m3):
         m.close()
     ctx.close()
+
+
+@pytest.mark.parametrize("G,var,approx,width,n", [(2, False, False, 4, 1_000_000), (3, True, True, 4, 300_000),
+                                                  (4, False, True, 7, 50_000), (3, False, False, 4, 10),
+                                                  (2, False, False, 64, 0), (2, True, False, 0, 120_000)])
+def test_multi_device_full_build_equals_one_device(tmp_path, G, var, approx, width, n):
+    """E4 behind the C ABI (bsdb_multi_mph_build_index_*): the key set sharded
+    over G device contexts (this box's one GPU listed G times -- the exchange
+    is then a copy within it), bucket-range owners, one exchange, range
+    solves, slices written in place.  The structure and the files equal the
+    one-device F2 build byte for byte; with more devices than buckets (n = 10)
+    the empty ranges do nothing."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import oracle as O
+    from bsdb_amd import Context
+    from bsdb_amd.native import Multi
+    rng = np.random.default_rng(11)
+    if var:
+        blob, off = O.gen_keys_var(3, n)
+    else:
+        keys = O.gen_keys13(91, n)
+    addr = rng.integers(0, 1 << 62, n, dtype=np.uint64)
+    value8 = rng.integers(0, 1 << 63, n, dtype=np.uint64) if approx else None
+    vlen = rng.integers(0, 9, n).astype(np.uint8) if approx else None
+    index = width != 0
+    d1, d2 = tmp_path / "one", tmp_path / "multi"
+    d1.mkdir(); d2.mkdir()
+    ip1, ap1, ip2, ap2 = (str(d / f) for d in (d1, d2) for f in ("index.db", "index_a.db"))
+    with Context(0) as ctx:
+        if var:
+            m1 = ctx.mph_build_index_var(blob, off, width, addr, ip1, ap1, approx, value8, vlen)
+        else:
+            m1 = ctx.mph_build_index_fixed(keys, 13, width, addr, ip1, ap1, approx, value8, vlen)
+        ref = m1.export()
+        m1.close()
+    with Multi(G, [0] * G) as mc:
+        args = (addr, ip2 if index else None, ap2 if index else None, approx, value8, vlen)
+        got = mc.mph_build_index_var(blob, off, width, *args) if var else mc.mph_build_index_fixed(keys, 13, width, *args)
+    for a, b in zip(got, ref):
+        if a is None or b is None:
+            assert a is None and b is None
+        else:
+            np.testing.assert_array_equal(a, b)
+    if index:
+        for a, b in ((ip1, ip2), (ap1, ap2)):
+            assert open(a, "rb").read() == open(b, "rb").read()
+        assert os.path.getsize(ip2) == 8 * n and os.path.getsize(ap2) == (8 * n if approx else 0)
