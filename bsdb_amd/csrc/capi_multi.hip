@@ -165,6 +165,15 @@ int multi_build(bsdb_multi *mc, uint64_t n, uint32_t width, const uint64_t *h_ad
     if (m > 0x7FFFFFFFULL || G > OWN_MAXR) return BSDB_EINVAL;
     const bool index = index_path != nullptr;
     const uint64_t values_words = bsdb_values_words(n), sig_words = mph_sig_words(n, width);
+    // BSDB_MULTI_PROFILE=1: wall time of each phase to stderr
+    const bool prof = getenv("BSDB_MULTI_PROFILE") != nullptr;
+    auto t_last = std::chrono::steady_clock::now();
+    auto lap = [&](const char *what) {
+        if (!prof) return;
+        const auto now = std::chrono::steady_clock::now();
+        fprintf(stderr, "[multi-build] %s %.1f ms\n", what, std::chrono::duration<double, std::milli>(now - t_last).count());
+        t_last = now;
+    };
     std::vector<MultiDev> dv(G);
     for (int i = 0; i < G; ++i) {
         dv[i].mem.device = mc->ctx[i]->device;
@@ -200,6 +209,7 @@ int multi_build(bsdb_multi *mc, uint64_t n, uint32_t width, const uint64_t *h_ad
             }
         }
 
+    lap("files + peers");
     // ---- A: hash the shard, group by owner, gather the records' payloads
     int rc = per_device(G, [&](int i) -> int {
         bsdb_ctx *c = mc->ctx[i];
@@ -246,6 +256,7 @@ int multi_build(bsdb_multi *mc, uint64_t n, uint32_t width, const uint64_t *h_ad
         return BSDB_OK;
     });
     if (rc) return close_files(rc);
+    lap("A hash + partition + gather");
 
     // ---- B: the one exchange, every (source, owner) block device to device
     uint64_t acc = 0;
@@ -290,6 +301,7 @@ int multi_build(bsdb_multi *mc, uint64_t n, uint32_t width, const uint64_t *h_ad
         for (void *q : {(void *)dv[i].sig_g, (void *)dv[i].addr_g, (void *)dv[i].v8_g, (void *)dv[i].vl_g})
             dv[i].mem.release(q);
 
+    lap("B exchange");
     // ---- C + D: solve each range, copy its fields out, write its index slice
     rc = per_device(G, [&](int g) -> int {
         bsdb_ctx *c = mc->ctx[g];
@@ -339,6 +351,7 @@ int multi_build(bsdb_multi *mc, uint64_t n, uint32_t width, const uint64_t *h_ad
         return BSDB_OK;
     });
     if (rc) return close_files(rc);
+    lap("C+D solve + fields + index slices");
     // the boundary words: every contribution OR-ed (fields are disjoint bits)
     auto merge = [&](uint64_t *h, bool sig) {
         for (auto &d : dv)

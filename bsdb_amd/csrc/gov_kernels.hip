@@ -1573,17 +1573,46 @@ __global__ __launch_bounds__(256) void k_owner_count(const uint64_t *sig, uint64
     if (threadIdx.x < G && h[threadIdx.x]) atomicAdd(counts + threadIdx.x, (unsigned long long)h[threadIdx.x]);
 }
 
-// cursor[g] starts at rank g's offset in the output
+// cursor[g] starts at rank g's offset in the output.  A workgroup takes
+// tiles of 1024 keys: ranks within the tile per owner from an LDS histogram,
+// then ONE global atomic per owner and tile (per-key atomics on G words are
+// serialised at the memory side: ~10x slower at G = 1 or 2).
 __global__ __launch_bounds__(256) void k_owner_scatter(const uint64_t *sig, const uint64_t *payload, uint64_t n,
                                                        uint32_t mult, uint64_t m, uint32_t G,
                                                        unsigned long long *cursor, uint64_t *out,
                                                        uint64_t *payload_out) {
-    const uint64_t stride = (uint64_t)gridDim.x * 256;
-    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
-        const ulonglong2 s = reinterpret_cast<const ulonglong2 *>(sig)[i];
-        const uint64_t pos = atomicAdd(cursor + owner_of(bucket_of_w(w64(s.x), mult), m, G), 1ULL);
-        reinterpret_cast<ulonglong2 *>(out)[pos] = s;
-        if (payload) payload_out[pos] = payload[i];
+    constexpr int K = 4;
+    constexpr uint64_t TILE = 256 * K;
+    __shared__ uint32_t h[OWN_MAXR];
+    __shared__ unsigned long long base[OWN_MAXR];
+    const uint32_t tid = threadIdx.x;
+    for (uint64_t t0 = (uint64_t)blockIdx.x * TILE; t0 < n; t0 += (uint64_t)gridDim.x * TILE) {
+        if (tid < OWN_MAXR) h[tid] = 0;
+        __syncthreads();
+        ulonglong2 s[K];
+        uint32_t o[K], r[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const uint64_t i = t0 + k * 256 + tid;
+            o[k] = G;  // none
+            if (i < n) {
+                s[k] = reinterpret_cast<const ulonglong2 *>(sig)[i];
+                o[k] = owner_of(bucket_of_w(w64(s[k].x), mult), m, G);
+                r[k] = atomicAdd(&h[o[k]], 1u);
+            }
+        }
+        __syncthreads();
+        if (tid < G && h[tid]) base[tid] = atomicAdd(cursor + tid, (unsigned long long)h[tid]);
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            if (o[k] < G) {
+                const uint64_t pos = base[o[k]] + r[k];
+                reinterpret_cast<ulonglong2 *>(out)[pos] = s[k];
+                if (payload) payload_out[pos] = payload[t0 + k * 256 + tid];
+            }
+        }
+        __syncthreads();  // h and base are reused by the next tile
     }
 }
 
