@@ -230,7 +230,20 @@ struct D13Sel {
     bool binned;        // runs padded to 8 ids, region copies = d13_copies
     uint32_t bin_ids;   // binned: ids per LDS bin buffer
 };
+// Fixed key lengths the windowed kernel k_pass1_d13e serves (a key's 16-byte
+// window from its aligned start); BSDB_NO_FIXED_WINDOW=1 sends 8/12/16 to the
+// var-len kernel instead (A/B switch for measurements).
+bool windowed_len(uint32_t key_len) {
+    return key_len == 13 || ((key_len == 8 || key_len == 12 || key_len == 16) && !getenv("BSDB_NO_FIXED_WINDOW"));
+}
+
 D13Sel d13_select(const bsdb_ctx *c, bool var = false, uint32_t key_len = 13, bool seed0 = false) {
+    if (!var && key_len != 13 && windowed_len(key_len)) {
+        D13Kernel k = key_len == 8    ? (seed0 ? k_pass1_d13e<0, true, 8> : k_pass1_d13e<0, false, 8>)
+                      : key_len == 12 ? (seed0 ? k_pass1_d13e<0, true, 12> : k_pass1_d13e<0, false, 12>)
+                                      : (seed0 ? k_pass1_d13e<0, true, 16> : k_pass1_d13e<0, false, 16>);
+        return {k, D13E_NT, D13E_TILE, D13E_MAXP, true, D13E_BIN_IDS};
+    }
     if (!var && key_len != 13)  // every other fixed length: the var-len kernel on k * L offsets
         return {seed0 ? k_pass1_vare<0, true, true> : k_pass1_vare<0, true>, VARE_NT, VARE_TILE, VARE_MAXP, true,
                 VARE_BIN_IDS};
@@ -327,7 +340,8 @@ int histogram_impl(bsdb_ctx *c, const uint8_t *keys, const uint64_t *offsets, ui
     // the persistent kernels: 13-byte keys and variable-length keys
     D13Sel sel = d13_select(c, var, key_len, seed == 0 && !getenv("BSDB_NO_SEED0"));  // (A/B switch for measurements)
     uint32_t bsh = 0, nb = 0, cb = 0;
-    const bool fixed_other = !var && key_len != 13;
+    const bool windowed = !var && windowed_len(key_len);  // k_pass1_d13e (13 B, or 8 / 12 / 16 B)
+    const bool fixed_other = !var && !windowed;
     // (fixed keys over 32 B: a 128-key group would overflow the var-len
     // kernel's LDS stage, so they stay on the one-tile-per-workgroup kernels)
     bool d13 = c->frontend == 0 && !(fixed_other && (key_len == 0 || key_len > 32)) &&
@@ -422,11 +436,12 @@ int histogram_impl(bsdb_ctx *c, const uint8_t *keys, const uint64_t *offsets, ui
                 }
             } else if (d13) {
                 // full tiles whose 16-byte windows stay inside the chunk go to the
-                // persistent kernel; the rest (< 2 of its tiles) to the
-                // bounds-checked kernel, in the tail regions
-                const uint64_t dtile = sel.tile;
+                // persistent kernel (a key's window ends 16 - L bytes past it at
+                // most); the rest (< 2 of its tiles) to the bounds-checked
+                // kernel, in the tail regions
+                const uint64_t dtile = sel.tile, over = 16 - key_len;
                 uint64_t nfast = 0;
-                if (ac.blob_bytes >= 3) nfast = std::min(nk / dtile, ((ac.blob_bytes - 3) / 13) / dtile);
+                if (ac.blob_bytes >= over) nfast = std::min(nk / dtile, ((ac.blob_bytes - over) / key_len) / dtile);
                 if (nfast) {
                     const uint32_t grid = (uint32_t)std::min<uint64_t>(nfast, pp.grid_d13);
                     sel.k<<<grid, sel.nt, 0, s>>>(ac, nfast);
@@ -434,14 +449,14 @@ int histogram_impl(bsdb_ctx *c, const uint8_t *keys, const uint64_t *offsets, ui
                 const uint64_t done = nfast * dtile;
                 if (done < nk) {
                     P1Args at = ac;
-                    at.keys = ac.keys + done * 13;
+                    at.keys = ac.keys + done * key_len;
                     at.n = nk - done;
-                    at.blob_bytes = at.n * 13;
+                    at.blob_bytes = at.n * key_len;
                     at.ids = a.ids + (size_t)pp.nmain * pp.nparts * pp.cap;
                     at.cursor = a.cursor + (size_t)pp.nmain * pp.nparts;
                     at.cap = pp.cap_tail;
                     at.nregions = pp.ntail;
-                    k_pass1<SRC_DIRECT13, EPI_PARTITION, 4, 13><<<(uint32_t)((at.n + P1_TILE - 1) / P1_TILE), P1_THREADS, 0, s>>>(at);
+                    launch_pass1<EPI_PARTITION>(at, false, key_len, (at.n + P1_TILE - 1) / P1_TILE, s, 0);
                 }
             } else {
                 launch_pass1<EPI_PARTITION>(ac, var, key_len, tiles, s, c->frontend);

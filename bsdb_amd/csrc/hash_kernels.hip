@@ -591,8 +591,11 @@ constexpr uint16_t ID_PAD = 0xFFFF;                       // not a local id (ids
 // VARIANT 0 is production.  Profiling only (results invalid): 1 = hash and
 // bins, no cursor atomics and no write-out; 4 = per-wave phase cycles
 // (s_memtime) written over counts[8*wave ..] (tools/stamp_probe_e.py).
-template <int VARIANT, bool SEED0 = false>
+// L: the key length, 13 or an aligned 8 / 12 / 16 (the same design; the
+// 16-byte window of a key then starts at the key itself).
+template <int VARIANT, bool SEED0 = false, int L = 13>
 __global__ __launch_bounds__(D13E_NT, 1) void k_pass1_d13e(P1Args a, uint64_t ntiles) {
+    static_assert(L == 13 || L == 8 || L == 12 || L == 16, "key lengths of the windowed kernel");
     // SEED0: the seed is 0 (every BSDBWriter build, CBHS:209): the hash's
     // seed terms fold at compile time
     const uint64_t seed = SEED0 ? 0ull : a.seed;
@@ -616,14 +619,14 @@ __global__ __launch_bounds__(D13E_NT, 1) void k_pass1_d13e(P1Args a, uint64_t nt
     const uint32_t my_p = owner ? (uint32_t)w * PPW + l : P;  // P = none
 
     u32x4a S[4][D13_Q];
-    // Key kt of a tile starts at byte 13 * kt of it; tile, quarter and key
-    // slot offsets (multiples of 13 * NT = 13312) are multiples of 4, so a
+    // Key kt of a tile starts at byte L * kt of it; tile, quarter and key
+    // slot offsets (multiples of L * NT, e.g. 13 * 1024 = 13312) are multiples of 4, so a
     // lane's 4-byte-aligned window offset and its byte shift are the same
     // for every key it loads: the address is a uniform base (scalar
     // arithmetic) + one 32-bit lane offset, no per-key VALU.
-    const uint32_t lane_off = ((uint32_t)tid * 13u) & ~3u;
-    const uint32_t sh = (((uint32_t)tid * 13u) & 3u) * 8u;
-    static_assert((NT * 13) % 4 == 0 && ((uint64_t)TILE * 13) % 4 == 0, "window alignment per lane");
+    const uint32_t lane_off = ((uint32_t)tid * L) & ~3u;
+    const uint32_t sh = (((uint32_t)tid * L) & 3u) * 8u;  // (0 for L = 8, 12, 16)
+    static_assert((NT * L) % 4 == 0 && ((uint64_t)TILE * L) % 4 == 0, "window alignment per lane");
     // unconditional loads (past the last tile they re-read tile t0): keeps
     // the compiler's waitcnt bookkeeping free of merged paths
     // Buffer loads through a per-tile descriptor (built by scalar code): the
@@ -632,11 +635,11 @@ __global__ __launch_bounds__(D13E_NT, 1) void k_pass1_d13e(P1Args a, uint64_t nt
     // aux 2 = nt (streamed once, as __builtin_nontemporal_load).
     auto load_q = [&](int q, uint64_t tt) {
         const uint64_t ts = tt < ntiles ? tt : t0;
-        const uint8_t *tb = a.keys + ts * ((uint64_t)TILE * 13);
-        const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(tb), 0, TILE * 13 + 16, 0x00020000);
+        const uint8_t *tb = a.keys + ts * ((uint64_t)TILE * L);
+        const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(tb), 0, TILE * L + 16, 0x00020000);
 #pragma unroll
         for (int j = 0; j < D13_Q; ++j) {
-            const auto v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, lane_off, (q * D13_Q + j) * NT * 13, 2);
+            const auto v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, lane_off, (q * D13_Q + j) * NT * L, 2);
             S[q][j] = u32x4a{v[0], v[1], v[2], v[3]};
         }
     };
@@ -646,7 +649,12 @@ __global__ __launch_bounds__(D13E_NT, 1) void k_pass1_d13e(P1Args a, uint64_t nt
     auto hash_q = [&](int q, uint32_t cur) {
         uint32_t b[D13_Q], r[D13_Q];
 #pragma unroll
-        for (int j = 0; j < D13_Q; ++j) b[j] = spooky13_bucket(S[q][j].x, S[q][j].y, S[q][j].z, S[q][j].w, sh, seed, mult);
+        for (int j = 0; j < D13_Q; ++j) {
+            if constexpr (L == 13)
+                b[j] = spooky13_bucket(S[q][j].x, S[q][j].y, S[q][j].z, S[q][j].w, sh, seed, mult);
+            else
+                b[j] = spooky_fix_bucket<L>(S[q][j].x, S[q][j].y, S[q][j].z, S[q][j].w, seed, mult);
+        }
 #pragma unroll
         for (int j = 0; j < D13_Q; ++j) r[j] = atomicAdd(&cnt[cur][b[j] >> bsh], 1u);
 #pragma unroll

@@ -352,15 +352,41 @@ __device__ __forceinline__ uint32_t bucket_of_w(W64 sig0, uint32_t mult) {
     return (uint32_t)(t >> 32);
 }
 
+__device__ __forceinline__ uint32_t short_end_bucket(uint64_t h0, uint64_t h1, uint64_t h2, uint64_t h3, uint32_t mult);
+
 // The bucket of a 13-byte key straight from the hash (the histogram needs
-// nothing else): ShortEnd up to h0's last rotation, then x = sig0 >>> 1 from
-// the unrotated word h (sig0 = rotl(h, 63) = h >>> 1 | h << 63, so x =
-// h >>> 2 | (h & 1) << 62): 3 VALU instead of the rotation's 2 plus 2.
+// nothing else): spooky.c's tail case 13, then short_end_bucket.
+
 __device__ __forceinline__ uint32_t spooky13_bucket(uint32_t d0, uint32_t d1, uint32_t d2, uint32_t d3, uint32_t sh,
                                                     uint64_t seed, uint32_t mult) {
     const uint64_t w0 = ((uint64_t)__builtin_amdgcn_alignbit(d2, d1, sh) << 32) | __builtin_amdgcn_alignbit(d1, d0, sh);
     const uint64_t w1 = ((uint64_t)((d3 >> sh) & 0xFFu) << 32) | __builtin_amdgcn_alignbit(d3, d2, sh);
-    uint64_t h0 = seed + 13 * 8, h1 = seed, h2 = add_u(SC, w0), h3 = add_u(SC, w1);
+    return short_end_bucket(seed + 13 * 8, seed, add_u(SC, w0), add_u(SC, w1), mult);
+}
+
+// The bucket of a fixed-length key of L in {8, 12, 16} bytes given as the
+// 16 little-endian bytes d0..d3 from its (4-byte aligned) first byte:
+// spooky.c's tail cases 8 and 12 (h3 += the masked second word, 0 or the
+// 4 bytes 8..11) and, for 16, the one 16-byte ShortMix step with the empty
+// tail (h2, h3 += SC) -- spooky.c:97-170.
+template <int L>
+__device__ __forceinline__ uint32_t spooky_fix_bucket(uint32_t d0, uint32_t d1, uint32_t d2, uint32_t d3, uint64_t seed,
+                                                      uint32_t mult) {
+    static_assert(L == 8 || L == 12 || L == 16, "aligned fixed lengths");
+    const uint64_t w0 = ((uint64_t)d1 << 32) | d0;
+    if (L == 16) {
+        uint64_t h0 = seed, h1 = seed, h2 = add_u(SC, w0), h3 = add_u(SC, ((uint64_t)d3 << 32) | d2);
+        short_mix_u(h0, h1, h2, h3);
+        return short_end_bucket(add_u(h0, 16 * 8), h1, add_u(h2, SC), add_u(h3, SC), mult);
+    }
+    return short_end_bucket(seed + L * 8, seed, add_u(SC, w0), L == 12 ? add_u(SC, (uint64_t)d2) : SC, mult);
+}
+
+// ShortEnd (spooky.c:72-84) up to h0's last rotation, then the bucket
+// (GOV:559) from the unrotated word h (sig0 = rotl(h, 63) = h >>> 1 | h << 63,
+// so x = sig0 >>> 1 = h >>> 2 | (h & 1) << 62): 3 VALU instead of the
+// rotation's 2 plus 2.
+__device__ __forceinline__ uint32_t short_end_bucket(uint64_t h0, uint64_t h1, uint64_t h2, uint64_t h3, uint32_t mult) {
 #define BSDB_END_STEP_U(D, C, K) D ^= C; C = rotl_u<K>(C); D = add_u(D, C);
     BSDB_END_STEP_U(h3, h2, 15) BSDB_END_STEP_U(h0, h3, 52) BSDB_END_STEP_U(h1, h0, 26)
     BSDB_END_STEP_U(h2, h1, 51) BSDB_END_STEP_U(h3, h2, 28) BSDB_END_STEP_U(h0, h3, 9)

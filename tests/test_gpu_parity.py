@@ -114,7 +114,7 @@ def test_device_key_generator(ctx, golden):
     np.testing.assert_array_equal(d[: 13 * 5_000].cpu().numpy(), O.gen_keys13(123_456_789_000, 5_000))
 
 
-@pytest.mark.parametrize("L", [13, 1, 5, 8, 16, 20, 32, 33, 40, 80])
+@pytest.mark.parametrize("L", [13, 1, 5, 8, 12, 16, 20, 32, 33, 40, 80])
 @pytest.mark.parametrize("m", [1, 667, 32_768, 32_769, 8_795_859])
 def test_histogram_partitioned_many_partitions(ctx, L, m):
     # m up to the C4 bucket count: 269 partitions of 32768 buckets
@@ -122,6 +122,26 @@ def test_histogram_partitioned_many_partitions(ctx, L, m):
     keys = rand_keys(n, L, m % 97 + L)
     counts = ctx.histogram_fixed(dev(keys), L, m).cpu().numpy().view(np.uint32)
     np.testing.assert_array_equal(counts, O.histogram_fixed(keys, L, m))
+
+
+@pytest.mark.parametrize("L", [8, 12, 16])
+def test_windowed_fixed_lengths_ragged(ctx, L):
+    """8/12/16-byte keys on the windowed kernel (k_pass1_d13e<L>): the buffer
+    ends exactly at L*n bytes (the last tiles go to the bounds-checked kernel),
+    several chunks; counts == the oracle's."""
+    m = 8_795_859
+    for n in (1, 16383, 16384, 16385, 49_151, 200_003):
+        keys = rand_keys(n, L, n % 89 + L)
+        counts = ctx.histogram_fixed(dev(keys), L, m).cpu().numpy().view(np.uint32)
+        np.testing.assert_array_equal(counts, O.histogram_fixed(keys, L, m))
+    n = 300_001
+    keys = rand_keys(n, L, 7)
+    ctx.set_chunk_keys(8192 * 5)
+    try:
+        c = ctx.histogram_fixed(dev(keys), L, 66_667).cpu().numpy().view(np.uint32)
+    finally:
+        ctx.set_chunk_keys(0)
+    np.testing.assert_array_equal(c, O.histogram_fixed(keys, L, 66_667))
 
 
 def test_histogram_multi_chunk_and_accumulate(ctx):

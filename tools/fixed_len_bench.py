@@ -27,7 +27,7 @@ def timed(fn, reps):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=400_000_000)
-    ap.add_argument("--lens", type=str, default="8,16,20,32")
+    ap.add_argument("--lens", type=str, default="8,12,16,20,32")
     ap.add_argument("--reps", type=int, default=3)
     args = ap.parse_args()
     ctx = Context(0)
