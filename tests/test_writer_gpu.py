@@ -196,3 +196,23 @@ def test_multi_device_full_build_equals_one_device(tmp_path, G, var, approx, wid
         for a, b in ((ip1, ip2), (ap1, ap2)):
             assert open(a, "rb").read() == open(b, "rb").read()
         assert os.path.getsize(ip2) == 8 * n and os.path.getsize(ap2) == (8 * n if approx else 0)
+
+
+def test_multi_device_full_build_rejects_duplicates(tmp_path):
+    """A key repeated in two shards meets itself at its bucket's owner: the
+    multi-device build reports the duplicate (BSDB_EDUP, CBHS:969-972) like
+    the one-device build."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import oracle as O
+    from bsdb_amd.native import BsdbError, Multi
+    n = 200_000
+    keys = O.gen_keys13(5, n).copy()
+    keys[13 * (n - 1): 13 * n] = keys[0:13]  # the last key (shard 2) == the first (shard 1)
+    addr = np.arange(n, dtype=np.uint64)
+    with Multi(2, [0, 0]) as mc:
+        with pytest.raises(BsdbError) as e:
+            mc.mph_build_index_fixed(keys, 13, 4, addr, str(tmp_path / "i.db"))
+        assert e.value.code == -17
+        E, vals, sb = mc.mph_build_index_fixed(keys[: 13 * (n - 1)], 13, 4)  # the same contexts build after it
+    assert E[-1] == n - 1
