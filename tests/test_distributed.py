@@ -22,7 +22,7 @@ def test_shard_cover():
             assert all(lo % TILE == 0 for lo, _ in spans)
 
 
-def _worker(rank, world, port, n, m, q):
+def _worker(rank, world, port, n, m, q, use_gpu=False):
     import sys
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle"))
     import oracle as O
@@ -30,9 +30,17 @@ def _worker(rank, world, port, n, m, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     lo, hi = shard(n, rank, world)
 
-    def local(counts):
-        keys = O.gen_keys13(lo, hi - lo)
-        counts += torch.from_numpy(O.histogram_fixed(keys, 13, m).astype(np.int32))
+    if use_gpu:  # the HIP histogram of this rank's shard (every rank on cuda:0), reduced on the host
+        from bsdb_amd import Context
+        ctx = Context(0)
+
+        def local(counts):
+            keys = ctx.gen_keys13(lo, hi - lo)
+            counts += ctx.histogram_fixed(keys, 13, m, n=hi - lo).cpu()
+    else:
+        def local(counts):
+            keys = O.gen_keys13(lo, hi - lo)
+            counts += torch.from_numpy(O.histogram_fixed(keys, 13, m).astype(np.int32))
 
     c = global_histogram(local, torch.zeros(m, dtype=torch.int32))
     E = O.edge_offsets(c.numpy().view(np.uint32))
@@ -43,12 +51,25 @@ def _worker(rank, world, port, n, m, q):
 
 @pytest.mark.parametrize("world", [2, 3])
 def test_gloo_sharded_histogram(world):
-    n = 300_001
-    m = 5_000
-    port = 29500 + world * 7 + os.getpid() % 500
+    _sharded_histogram(world, 300_001, 5_000, use_gpu=False)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_sharded_histogram_hip_ranks(world):
+    """E2/E3 with the product kernels: each rank histograms its shard with
+    the HIP path (all ranks on this box's one GPU), ONE all-reduce (gloo on
+    the host here; RCCL in bench.py / the C ABI), every rank the same E."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    _sharded_histogram(world, 2_000_003, 8_795_859, use_gpu=True)
+
+
+def _sharded_histogram(world, n, m, use_gpu):
+    port = 29500 + world * 7 + os.getpid() % 500 + (60 if use_gpu else 0)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    ps = [ctx.Process(target=_worker, args=(r, world, port, n, m, q)) for r in range(world)]
+    ps = [ctx.Process(target=_worker, args=(r, world, port, n, m, q, use_gpu)) for r in range(world)]
     for p in ps:
         p.start()
     res = [q.get(timeout=120) for _ in ps]
