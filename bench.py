@@ -139,12 +139,16 @@ def e4_multi_device(ctx, n: int, width: int):
     ndev = max(1, torch.cuda.device_count())
     keys = ctx.gen_keys13(0, n)[: 13 * n].cpu().numpy()
     torch.cuda.empty_cache()
+    times = []
     with Multi(ndev) as mc:
-        t0 = _t.perf_counter()
-        E, _, _ = mc.mph_build_index_fixed(keys, 13, width)
-        dt = _t.perf_counter() - t0
-    assert int(E[-1]) & ((1 << 56) - 1) == n
+        for _ in range(2):  # best of two (the first call also grows every context's workspace)
+            t0 = _t.perf_counter()
+            E, _, _ = mc.mph_build_index_fixed(keys, 13, width)
+            times.append(_t.perf_counter() - t0)
+            assert int(E[-1]) & ((1 << 56) - 1) == n
+    dt = min(times)
     return {"n_keys": n, "checksum_bits": width, "devices": ndev, "keys_per_s": n / dt, "ms": dt * 1e3,
+            "ms_each": [t * 1e3 for t in times],
             "path": "host keys -> bsdb_multi_mph_build_index_fixed (E4, one process, every visible GPU) -> "
                     "E / values / checksum words in host memory"}
 
