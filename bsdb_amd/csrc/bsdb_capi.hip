@@ -81,6 +81,10 @@ struct bsdb_ctx {
     // RCCL rank (bsdb_comm_init) and the finalize packing buffer
     void *comm = nullptr;
     int nranks = 1, rank = 0;
+    // live MPHF objects of this context: bsdb_close releases their device
+    // arrays and detaches them, so freeing one afterwards is safe
+    std::mutex mph_mu;
+    std::vector<bsdb_mph *> mphs;
     void *pack = nullptr;
     size_t pack_bytes = 0;
     // live profiling: event pairs per launch, per kind
@@ -553,10 +557,13 @@ int bsdb_open(int device, bsdb_ctx **out) {
     return BSDB_OK;
 }
 
+static void mph_detach_all(bsdb_ctx *c);
+
 int bsdb_close(bsdb_ctx *c) {
     if (!c) return BSDB_EINVAL;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
+    mph_detach_all(c);
     (void)hipFree(c->ids);
     (void)hipFree(c->cursor);
     (void)hipFree(c->p2_pref);

@@ -5,7 +5,8 @@
 //   GOV = src/main/java/it/unimi/dsi/sux4j/mph/GOVMinimalPerfectHashFunctionModified.java
 
 struct bsdb_mph {
-    bsdb_ctx *c = nullptr;
+    bsdb_ctx *c = nullptr;  // nullptr once its context was closed (arrays released then)
+    int device = 0;
     uint64_t n = 0, m = 0;
     uint32_t width = 0;
     uint64_t values_words = 0, sig_words = 0;
@@ -25,12 +26,22 @@ namespace {
 
 uint64_t mph_sig_words(uint64_t n, uint32_t width) { return width ? (n * width + 63) / 64 + 1 : 0; }
 
-void mph_release(bsdb_mph *p) {
-    if (!p) return;
-    if (p->c) (void)hipSetDevice(p->c->device);
+void mph_free_arrays(bsdb_mph *p) {
+    (void)hipSetDevice(p->device);
     (void)hipFree(p->E);
     (void)hipFree(p->values);
     (void)hipFree(p->sigbits);
+    p->E = p->values = p->sigbits = nullptr;
+}
+
+void mph_release(bsdb_mph *p) {
+    if (!p) return;
+    if (p->c) {
+        std::lock_guard<std::mutex> g(p->c->mph_mu);
+        auto &v = p->c->mphs;
+        v.erase(std::remove(v.begin(), v.end(), p), v.end());
+    }
+    mph_free_arrays(p);
     delete p;
 }
 
@@ -39,6 +50,11 @@ int mph_alloc(bsdb_ctx *c, uint64_t n, uint32_t width, bsdb_mph **out) {
     bsdb_mph *p = new (std::nothrow) bsdb_mph();
     if (!p) return BSDB_ENOMEM;
     p->c = c;
+    p->device = c->device;
+    {
+        std::lock_guard<std::mutex> g(c->mph_mu);
+        c->mphs.push_back(p);
+    }
     p->n = n;
     p->m = n / BUCKET_SIZE + 1;
     p->width = width;
@@ -326,6 +342,16 @@ int index_put(bsdb_index *ix, const Keys &keys, uint64_t count, const uint64_t *
 
 }  // namespace
 
+// bsdb_close: every MPHF still alive loses its device arrays and its context
+static void mph_detach_all(bsdb_ctx *c) {
+    std::lock_guard<std::mutex> g(c->mph_mu);
+    for (bsdb_mph *p : c->mphs) {
+        mph_free_arrays(p);
+        p->c = nullptr;
+    }
+    c->mphs.clear();
+}
+
 extern "C" {
 
 int bsdb_mph_build_fixed(bsdb_ctx *c, const uint8_t *h_keys, uint32_t key_len, uint64_t n, uint32_t width,
@@ -376,6 +402,7 @@ int bsdb_mph_info(const bsdb_mph *p, uint64_t *n, uint64_t *m, uint32_t *width, 
 }
 
 int bsdb_mph_export(bsdb_mph *p, uint64_t *h_E, uint64_t *h_values, uint64_t *h_sigbits) {
+    if (p && !p->c) return BSDB_EINVAL;  // its context was closed
     if (!p || !h_E || !h_values || (p->width && !h_sigbits)) return BSDB_EINVAL;
     bsdb_ctx *c = p->c;
     std::lock_guard<std::mutex> g(c->mu);
@@ -412,6 +439,7 @@ int bsdb_mph_import(bsdb_ctx *c, uint64_t n, uint32_t width, const uint64_t *h_E
 
 // GOV.dump (GOV:592-619), read back by load_mph (mph.c:28-43)
 int bsdb_mph_dump(bsdb_mph *p, const char *path) {
+    if (p && !p->c) return BSDB_EINVAL;  // its context was closed
     if (!p || !path) return BSDB_EINVAL;
     std::vector<uint64_t> E(p->m + 1), vals(p->values_words);
     bsdb_ctx *c = p->c;
@@ -460,6 +488,7 @@ int bsdb_mph_load(bsdb_ctx *c, const char *path, bsdb_mph **out) {
 }
 
 int bsdb_mph_lookup_fixed(bsdb_mph *p, const uint8_t *h_keys, uint32_t key_len, uint64_t n, int check, int64_t *h_out) {
+    if (p && !p->c) return BSDB_EINVAL;  // its context was closed
     if (!p || bad_key_len(key_len) || (n && (!h_keys || !h_out))) return BSDB_EINVAL;
     bsdb_ctx *c = p->c;
     std::lock_guard<std::mutex> g(c->mu);
@@ -470,6 +499,7 @@ int bsdb_mph_lookup_fixed(bsdb_mph *p, const uint8_t *h_keys, uint32_t key_len, 
 
 int bsdb_mph_lookup_var(bsdb_mph *p, const uint8_t *h_blob, const uint64_t *h_off, uint64_t n, int check,
                         int64_t *h_out) {
+    if (p && !p->c) return BSDB_EINVAL;  // its context was closed
     if (!p || (n && (!h_blob || !h_off || !h_out))) return BSDB_EINVAL;
     bsdb_ctx *c = p->c;
     std::lock_guard<std::mutex> g(c->mu);
@@ -480,7 +510,7 @@ int bsdb_mph_lookup_var(bsdb_mph *p, const uint8_t *h_blob, const uint64_t *h_of
 
 int bsdb_mph_free(bsdb_mph *p) {
     if (!p) return BSDB_EINVAL;
-    {
+    if (p->c) {
         std::lock_guard<std::mutex> g(p->c->mu);
         (void)hipSetDevice(p->c->device);
         (void)hipStreamSynchronize(p->c->stream);
@@ -492,6 +522,7 @@ int bsdb_mph_free(bsdb_mph *p) {
 // ---- A13: the index writer ---------------------------------------------------
 int bsdb_index_open(bsdb_mph *p, int approximate, uint64_t pass_cache_bytes, const char *index_path,
                     const char *index_a_path, bsdb_index **out, uint64_t *passes) {
+    if (p && !p->c) return BSDB_EINVAL;  // its context was closed
     if (!p || !index_path || !out || (approximate && !index_a_path) || (p->n && pass_cache_bytes && pass_cache_bytes < 8))
         return BSDB_EINVAL;
     *out = nullptr;

@@ -21,8 +21,11 @@ file set in ``base_path`` (src/main/java/tech/bsdb/write/BSDBWriter.java, "W"):
 Every compute step is the C ABI (bsdb_mph_build_var, bsdb_index_*): no CPU
 fallback.  ``fused_index=True`` builds hash + index in one call whose solve
 returns every key's rank (bsdb_mph_build_index_var): no
-per-pass rescan, the same files.  ``put`` is per record as in the reference; ``put_batch`` takes a
-whole key blob at once.
+per-pass rescan, the same files.  ``devices=[...]`` makes that one call the
+multi-device build over those GPUs (bsdb_multi_mph_build_index_var, E4).
+``put`` is per record and safe to call from concurrent threads, as the
+reference's Builder does (Builder.java:144-160); ``put_batch`` takes a whole
+key blob at once.
 """
 from __future__ import annotations
 
@@ -42,7 +45,7 @@ class BSDBWriter:
     def __init__(self, base_path: str, tmp_dir: Optional[str] = None, checksum_bits: int = 4,
                  pass_cache_size: int = 1 << 30, compact: bool = True, compress: bool = False,
                  compress_block_size: int = 8192, shared_dict_size: int = 0, approximate_mode: bool = False,
-                 partitions: int = 1, device: int = 0, fused_index: bool = False):
+                 partitions: int = 1, device: int = 0, fused_index: bool = False, devices=None):
         if compress or not compact:
             raise NotImplementedError("only the compact kv.db layout is mirrored (kv.db formats are out of scope)")
         self.base = base_path
@@ -52,9 +55,9 @@ class BSDBWriter:
         self.approximate = approximate_mode
         self.partitions = partitions
         self.compress_block_size = compress_block_size
-        self.fused_index = fused_index
-        self._keys: list = []
-        self._values: list = []
+        self.fused_index = fused_index or devices is not None
+        self.devices = list(devices) if devices is not None else None
+        self._puts: list = []  # (key, value) pairs: one list.append per put, atomic across threads
         self._batches: list = []  # (blob, offsets, value8, vlen, value bytes total)
         self.ctx = Context(device)
 
@@ -64,8 +67,7 @@ class BSDBWriter:
             raise RuntimeError("currently null key/value is not support.")
         if not 0 < len(key) <= MAX_KEY_SIZE:
             raise ValueError("key length must be 1..255 bytes")
-        self._keys.append(bytes(key))
-        self._values.append(bytes(value))
+        self._puts.append((bytes(key), bytes(value)))
 
     def put_batch(self, blob: np.ndarray, offsets: np.ndarray, values: list):
         """Keys blob[offsets[i]:offsets[i+1]] with values[i] (bytes each)."""
@@ -80,11 +82,12 @@ class BSDBWriter:
     def _records(self):
         """All records as (key blob, offsets, values list)."""
         blobs, offs, vals, base = [], [np.zeros(1, np.uint64)], [], 0
-        if self._keys:
-            lens = np.fromiter((len(k) for k in self._keys), np.uint64, len(self._keys))
-            blobs.append(np.frombuffer(b"".join(self._keys), np.uint8))
+        if self._puts:
+            keys = [k for k, _ in self._puts]
+            lens = np.fromiter((len(k) for k in keys), np.uint64, len(keys))
+            blobs.append(np.frombuffer(b"".join(keys), np.uint8))
             offs.append(np.cumsum(lens, dtype=np.uint64))
-            vals += self._values
+            vals += [v for _, v in self._puts]
             base = int(offs[-1][-1])
         for blob, off, v in self._batches:
             blobs.append(blob[int(off[0]): int(off[-1])])
@@ -136,9 +139,17 @@ class BSDBWriter:
         self._blob, self._off, self._vals = blob, off, vals
         if self.fused_index:
             value8, vlen = self._value_heads()
-            mph = self.ctx.mph_build_index_var(blob, off, self.checksum_bits, self._addr,
-                                               os.path.join(self.base, "index.db"),
-                                               os.path.join(self.base, "index_a.db"), self.approximate, value8, vlen)
+            paths = (os.path.join(self.base, "index.db"), os.path.join(self.base, "index_a.db"))
+            if self.devices is not None:
+                from .native import Multi
+                with Multi(len(self.devices), self.devices) as mc:
+                    E, values, sigbits = mc.mph_build_index_var(blob, off, self.checksum_bits, self._addr, *paths,
+                                                                self.approximate, value8, vlen)
+                # the assembled fields, resident on this writer's device for dump / lookups
+                mph = self.ctx.mph_import(off.size - 1, self.checksum_bits, E, values, sigbits)
+            else:
+                mph = self.ctx.mph_build_index_var(blob, off, self.checksum_bits, self._addr, *paths,
+                                                   self.approximate, value8, vlen)
             mph.dump(os.path.join(self.base, "hash.dump"))
             return mph
         mph = self.build_hash()

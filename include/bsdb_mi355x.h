@@ -314,6 +314,11 @@ int bsdb_multi_mph_build_index_var(bsdb_multi *mc, const uint8_t *h_blob, const 
  *             no checksum bits (load gives width 0)
  *   lookup    getLong (GOV:528-532, 557-569) of host keys: rank or -1
  *             (check != 0: range and checksum test; 0: unchecked rank)
+ *   lifetime  an MPHF belongs to its context: bsdb_close releases the
+ *             device arrays of the context's live MPHFs, after which their
+ *             calls return BSDB_EINVAL and bsdb_mph_free only frees the
+ *             handle (either order of bsdb_close / bsdb_mph_free is safe);
+ *             close a bsdb_index before its MPHF
  * ------------------------------------------------------------------------- */
 typedef struct bsdb_mph bsdb_mph;
 int bsdb_mph_build_fixed(bsdb_ctx *ctx, const uint8_t *h_keys, uint32_t key_len, uint64_t n, uint32_t width,

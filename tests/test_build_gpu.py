@@ -357,3 +357,22 @@ def test_fixed_key_len_validated(ctx):
         with pytest.raises(BsdbError):
             ctx.histogram_fixed(keys, L, 10, n=1)
     assert ctx.gen_keys13(0, 1000).numel() == 13_000  # no padding key
+
+
+def test_mph_outlives_its_context():
+    """bsdb_close before bsdb_mph_free (a garbage collector's order): the
+    context releases the MPHF's device arrays and detaches it; its calls then
+    return BSDB_EINVAL and freeing it is safe."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from bsdb_amd import Context
+    from bsdb_amd.native import BsdbError
+    keys = O.gen_keys13(3, 50_000)
+    c = Context(0)
+    m = c.mph_build_fixed(keys, 13, 4)
+    assert m.info()["n"] == 50_000
+    c.close()
+    with pytest.raises(BsdbError) as e:
+        m.export()
+    assert e.value.code == -22
+    m.close()  # frees the handle only
