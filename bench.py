@@ -326,7 +326,7 @@ def main():
         log("full-build figures done")
     if rank == 0:
         cpu = None
-        if not args.no_cpu:
+        if not args.no_cpu and world == 1:  # the CPU baseline is an N = 1 figure
             cpu = cpu_baseline(m, args.cpu_seconds, args.cpu_threads)
             log("cpu baseline done")
         line = {
