@@ -209,7 +209,7 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
         else:
             dist.init_process_group("gloo")
-    if args.cpu_threads <= 0:
+    if args.cpu_threads <= 0 and world == 1 and not args.no_cpu:  # (the CPU legs only)
         args.cpu_threads = _oracle().cpu_threads()
 
     from bsdb_amd import Context
