@@ -419,8 +419,15 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
     // degrees are dead here, their words hold the stamps), so no BFS clears
     // the vertex array.
     uint32_t *seen = L.deg;
-    for (uint32_t v = tid; v < nv; v += GS_THREADS) seen[v] = 0;
+    // xe: the lowest lane of a chunk touching a vertex, as tag | lane with a
+    // tag that DEcreases every chunk, so an atomicMin needs no reset between
+    // chunks (a smaller value than every earlier chunk's)
+    for (uint32_t v = tid; v < nv; v += GS_THREADS) {
+        seen[v] = 0;
+        L.xe[v] = ~0u;
+    }
     __syncthreads();
+    uint32_t lane_tag = 0x3FFFFFFu << 6;  // (wave 0's register: 2^26 chunks per attempt)
     // Greedy: every core edge in increasing order takes its first free
     // vertex.  Wave 0 takes 64 edges at once: a lane none of whose vertices
     // an earlier lane of the chunk touches ("independent") takes its first
@@ -436,6 +443,8 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
             const bool act = k < cnt && L.round_of[k] < 0;
             uint32_t v0 = 0, v1 = 0, v2 = 0;
             bool f0 = false, f1 = false, f2 = false;
+            const uint32_t me = lane_tag | tid;
+            lane_tag -= 64;
             if (act) {
                 v0 = L.e[3 * k];
                 v1 = L.e[3 * k + 1];
@@ -443,18 +452,12 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
                 f0 = L.vowner[v0] < 0;
                 f1 = L.vowner[v1] < 0;
                 f2 = L.vowner[v2] < 0;
-                firstl[v0] = 64;
-                firstl[v1] = 64;
-                firstl[v2] = 64;
+                atomicMin(&firstl[v0], me);
+                atomicMin(&firstl[v1], me);
+                atomicMin(&firstl[v2], me);
             }
             __builtin_amdgcn_wave_barrier();
-            if (act) {
-                atomicMin(&firstl[v0], tid);
-                atomicMin(&firstl[v1], tid);
-                atomicMin(&firstl[v2], tid);
-            }
-            __builtin_amdgcn_wave_barrier();
-            const bool ovl = act && (firstl[v0] < (uint32_t)tid || firstl[v1] < (uint32_t)tid || firstl[v2] < (uint32_t)tid);
+            const bool ovl = act && (firstl[v0] < me || firstl[v1] < me || firstl[v2] < me);
             int chosen = -1;
             if (act && !ovl) {
                 chosen = f0 ? (int)v0 : f1 ? (int)v1 : f2 ? (int)v2 : -1;
@@ -535,19 +538,17 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
                 const uint32_t ei = lane / 3, vi = lane - 3 * ei;
                 int k = 0, o = -1;
                 uint32_t v = 0, sn = 0;
+                const uint32_t me = lane_tag | lane;
+                lane_tag -= 64;
                 if (act) {
                     k = queue[qh + ei];
                     v = L.e[3 * k + vi];
-                    first_lane[v] = 64;
-                }
-                __builtin_amdgcn_wave_barrier();
-                if (act) {
                     sn = seen[v];
                     o = L.vowner[v];
-                    atomicMin(&first_lane[v], lane);
+                    atomicMin(&first_lane[v], me);
                 }
                 __builtin_amdgcn_wave_barrier();
-                const bool valid = act && first_lane[v] == lane && sn != epoch;
+                const bool valid = act && first_lane[v] == me && sn != epoch;
                 const uint64_t fb = __builtin_amdgcn_ballot_w64(valid && o < 0);
                 const uint32_t F = fb ? (uint32_t)__builtin_ctzll(fb) : 64u;
                 const bool take = valid && lane < F;  // (o >= 0 below F)
