@@ -22,6 +22,23 @@ def test_shard_cover():
             assert all(lo % TILE == 0 for lo, _ in spans)
 
 
+def test_bucket_owner_ranges():
+    """E4 ownership: rank g owns [g*m/G, (g+1)*m/G) -- the ranges tile [0, m)
+    and owner_of_bucket (the kernels' ((b+1)*G-1)/m, gov_kernels.hip owner_of)
+    names the rank whose range holds b, also with more ranks than buckets."""
+    from bsdb_amd.distributed import bucket_range, owner_of_bucket
+    for m in (1, 2, 3, 7, 667, 66_667, 8_795_859):
+        for G in (1, 2, 3, 5, 8, 64):
+            ranges = [bucket_range(g, m, G) for g in range(G)]
+            assert ranges[0][0] == 0 and ranges[-1][1] == m
+            assert all(a[1] == b[0] for a, b in zip(ranges, ranges[1:]))
+            probe = sorted({0, m - 1, m // 2, m // 3, max(0, m - 2)} | {r[0] for r in ranges if r[0] < m})
+            for b in probe:
+                g = owner_of_bucket(b, m, G)
+                lo, hi = ranges[g]
+                assert lo <= b < hi, (m, G, b, g)
+
+
 def _worker(rank, world, port, n, m, q, use_gpu=False):
     import sys
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle"))
