@@ -4,9 +4,12 @@
 //   W   = src/main/java/tech/bsdb/write/BSDBWriter.java
 //   GOV = src/main/java/it/unimi/dsi/sux4j/mph/GOVMinimalPerfectHashFunctionModified.java
 
+struct bsdb_index;
+
 struct bsdb_mph {
     bsdb_ctx *c = nullptr;  // nullptr once its context was closed (arrays released then)
     int device = 0;
+    std::vector<bsdb_index *> ixs;  // its open index writers (detached when it is freed)
     uint64_t n = 0, m = 0;
     uint32_t width = 0;
     uint64_t values_words = 0, sig_words = 0;
@@ -14,13 +17,19 @@ struct bsdb_mph {
 };
 
 struct bsdb_index {
-    bsdb_mph *mph = nullptr;
+    bsdb_mph *mph = nullptr;  // nullptr once the MPHF was freed
+    int device = 0;
     bool approx = false;
     uint64_t pass_size = 0, passes = 0, next_pass = 0, cur = UINT64_MAX;
     FILE *f = nullptr, *fa = nullptr;
     uint64_t *d_index = nullptr;  // the pass's slots (big-endian addresses)
     uint8_t *d_index_a = nullptr; // approximate mode: the pass's 8-byte value slots
 };
+
+// Guards the links mph -> context, mph -> index writers and index -> mph:
+// bsdb_close / bsdb_mph_free may run (on a garbage collector's thread) before
+// the objects that point at them are freed; taken before a context's mph_mu.
+static std::mutex g_life_mu;
 
 namespace {
 
@@ -36,13 +45,25 @@ void mph_free_arrays(bsdb_mph *p) {
 
 void mph_release(bsdb_mph *p) {
     if (!p) return;
-    if (p->c) {
-        std::lock_guard<std::mutex> g(p->c->mph_mu);
-        auto &v = p->c->mphs;
-        v.erase(std::remove(v.begin(), v.end(), p), v.end());
+    {
+        std::lock_guard<std::mutex> lg(g_life_mu);
+        if (p->c) {
+            std::lock_guard<std::mutex> g(p->c->mph_mu);
+            auto &v = p->c->mphs;
+            v.erase(std::remove(v.begin(), v.end(), p), v.end());
+        }
+        for (bsdb_index *ix : p->ixs) ix->mph = nullptr;  // their later calls return EINVAL
+        p->ixs.clear();
     }
     mph_free_arrays(p);
     delete p;
+}
+
+// The context an index writer works on, or nullptr when its MPHF was freed or
+// the MPHF's context was closed.
+bsdb_ctx *index_ctx(const bsdb_index *ix) {
+    std::lock_guard<std::mutex> lg(g_life_mu);
+    return ix->mph ? ix->mph->c : nullptr;
 }
 
 // A new mph on ctx's device with its arrays allocated (not initialised).
@@ -314,8 +335,8 @@ template <class Keys>
 int index_put(bsdb_index *ix, const Keys &keys, uint64_t count, const uint64_t *h_addr, const uint64_t *h_value8,
               const uint8_t *h_vlen) {
     bsdb_mph *p = ix->mph;
-    bsdb_ctx *c = p->c;
-    if (ix->cur == UINT64_MAX) return BSDB_EINVAL;  // no pass begun
+    bsdb_ctx *c = p ? p->c : nullptr;
+    if (!c || ix->cur == UINT64_MAX) return BSDB_EINVAL;  // no pass begun / MPHF gone
     const MphView v{p->E, p->values, p->sigbits, p->n, (uint32_t)(2 * p->m), p->width};
     const uint64_t start = ix->cur * ix->pass_size;
     const uint64_t len = std::min(ix->pass_size, p->n - start);
@@ -344,6 +365,7 @@ int index_put(bsdb_index *ix, const Keys &keys, uint64_t count, const uint64_t *
 
 // bsdb_close: every MPHF still alive loses its device arrays and its context
 static void mph_detach_all(bsdb_ctx *c) {
+    std::lock_guard<std::mutex> lg(g_life_mu);
     std::lock_guard<std::mutex> g(c->mph_mu);
     for (bsdb_mph *p : c->mphs) {
         mph_free_arrays(p);
@@ -510,10 +532,15 @@ int bsdb_mph_lookup_var(bsdb_mph *p, const uint8_t *h_blob, const uint64_t *h_of
 
 int bsdb_mph_free(bsdb_mph *p) {
     if (!p) return BSDB_EINVAL;
-    if (p->c) {
-        std::lock_guard<std::mutex> g(p->c->mu);
-        (void)hipSetDevice(p->c->device);
-        (void)hipStreamSynchronize(p->c->stream);
+    bsdb_ctx *c = nullptr;
+    {
+        std::lock_guard<std::mutex> lg(g_life_mu);
+        c = p->c;
+    }
+    if (c) {
+        std::lock_guard<std::mutex> g(c->mu);
+        (void)hipSetDevice(c->device);
+        (void)hipStreamSynchronize(c->stream);
     }
     mph_release(p);
     return BSDB_OK;
@@ -529,12 +556,21 @@ int bsdb_index_open(bsdb_mph *p, int approximate, uint64_t pass_cache_bytes, con
     bsdb_index *ix = new (std::nothrow) bsdb_index();
     if (!ix) return BSDB_ENOMEM;
     ix->mph = p;
+    ix->device = p->device;
     ix->approx = approximate != 0;
+    {
+        std::lock_guard<std::mutex> lg(g_life_mu);
+        p->ixs.push_back(ix);
+    }
     if (!pass_cache_bytes) {  // device-sized pass cache: a quarter of free HBM
         size_t free_b = 0, total_b = 0;
-        std::lock_guard<std::mutex> g(p->c->mu);
-        if (hipSetDevice(p->c->device) != hipSuccess || hipMemGetInfo(&free_b, &total_b) != hipSuccess) {
-            delete ix;
+        bool got;
+        {
+            std::lock_guard<std::mutex> g(p->c->mu);
+            got = hipSetDevice(p->c->device) == hipSuccess && hipMemGetInfo(&free_b, &total_b) == hipSuccess;
+        }
+        if (!got) {
+            (void)bsdb_index_close(ix);
             return BSDB_EIO;
         }
         pass_cache_bytes = std::max<uint64_t>(8, free_b / 4 / (ix->approx ? 2 : 1));
@@ -567,7 +603,8 @@ int bsdb_index_open(bsdb_mph *p, int approximate, uint64_t pass_cache_bytes, con
 int bsdb_index_begin_pass(bsdb_index *ix, uint64_t pass) {
     // passes are written to the files in order (W:129-150)
     if (!ix || pass != ix->next_pass || pass >= ix->passes || ix->cur != UINT64_MAX) return BSDB_EINVAL;
-    bsdb_ctx *c = ix->mph->c;
+    bsdb_ctx *c = index_ctx(ix);
+    if (!c) return BSDB_EINVAL;  // its MPHF was freed or its context closed
     std::lock_guard<std::mutex> g(c->mu);
     HIP_OK(hipSetDevice(c->device));
     Ordered ord(c, c->stream);
@@ -580,7 +617,8 @@ int bsdb_index_begin_pass(bsdb_index *ix, uint64_t pass) {
 int bsdb_index_put_var(bsdb_index *ix, const uint8_t *h_blob, const uint64_t *h_off, uint64_t count,
                        const uint64_t *h_addr, const uint64_t *h_value8, const uint8_t *h_vlen) {
     if (!ix || (count && (!h_blob || !h_off || !h_addr || (ix->approx && (!h_value8 || !h_vlen))))) return BSDB_EINVAL;
-    bsdb_ctx *c = ix->mph->c;
+    bsdb_ctx *c = index_ctx(ix);
+    if (!c) return BSDB_EINVAL;
     std::lock_guard<std::mutex> g(c->mu);
     HIP_OK(hipSetDevice(c->device));
     Ordered ord(c, c->stream);
@@ -594,7 +632,8 @@ int bsdb_index_put_fixed(bsdb_index *ix, const uint8_t *h_keys, uint32_t key_len
                          const uint64_t *h_addr, const uint64_t *h_value8, const uint8_t *h_vlen) {
     if (!ix || bad_key_len(key_len) || (count && (!h_keys || !h_addr || (ix->approx && (!h_value8 || !h_vlen)))))
         return BSDB_EINVAL;
-    bsdb_ctx *c = ix->mph->c;
+    bsdb_ctx *c = index_ctx(ix);
+    if (!c) return BSDB_EINVAL;
     std::lock_guard<std::mutex> g(c->mu);
     HIP_OK(hipSetDevice(c->device));
     Ordered ord(c, c->stream);
@@ -606,7 +645,8 @@ int bsdb_index_put_fixed(bsdb_index *ix, const uint8_t *h_keys, uint32_t key_len
 
 int bsdb_index_end_pass(bsdb_index *ix) {
     if (!ix || ix->cur == UINT64_MAX) return BSDB_EINVAL;
-    bsdb_ctx *c = ix->mph->c;
+    bsdb_ctx *c = index_ctx(ix);
+    if (!c) return BSDB_EINVAL;
     std::lock_guard<std::mutex> g(c->mu);
     HIP_OK(hipSetDevice(c->device));
     Ordered ord(c, c->stream);
@@ -627,10 +667,26 @@ int bsdb_index_close(bsdb_index *ix) {
     bool ok = true;
     if (ix->f) ok = fclose(ix->f) == 0 && ok;
     if (ix->fa) ok = fclose(ix->fa) == 0 && ok;
+    // unlink from its MPHF (if that is still alive), then release the pass
+    // buffers on the writer's own device: the context may be gone already
+    bsdb_ctx *c = nullptr;
+    {
+        std::lock_guard<std::mutex> lg(g_life_mu);
+        if (ix->mph) {
+            auto &v = ix->mph->ixs;
+            v.erase(std::remove(v.begin(), v.end(), ix), v.end());
+            c = ix->mph->c;
+        }
+    }
     if (ix->d_index || ix->d_index_a) {
-        std::lock_guard<std::mutex> g(ix->mph->c->mu);
-        (void)hipSetDevice(ix->mph->c->device);
-        (void)hipStreamSynchronize(ix->mph->c->stream);
+        if (c) {
+            std::lock_guard<std::mutex> g(c->mu);
+            (void)hipSetDevice(c->device);
+            (void)hipStreamSynchronize(c->stream);
+        } else {
+            (void)hipSetDevice(ix->device);
+            (void)hipDeviceSynchronize();
+        }
         (void)hipFree(ix->d_index);
         (void)hipFree(ix->d_index_a);
     }

@@ -45,7 +45,9 @@ struct DevBufs {
     std::vector<void *> ptrs;
     template <class T>
     int alloc(T **p, uint64_t count) {
+        // a fresh host thread's current device is 0: allocate on OUR device
         void *q = nullptr;
+        if (hipSetDevice(device) != hipSuccess) return BSDB_EIO;
         if (hipMalloc(&q, std::max<uint64_t>(count, 1) * sizeof(T)) != hipSuccess) return BSDB_ENOMEM;
         ptrs.push_back(q);
         *p = (T *)q;
@@ -217,6 +219,7 @@ int multi_build(bsdb_multi *mc, uint64_t n, uint32_t width, const uint64_t *h_ad
         const uint64_t nd = d.hi - d.lo;
         uint64_t *sig = nullptr, *perm = nullptr, *perm_g = nullptr;
         int r;
+        HIP_OK(hipSetDevice(c->device));
         if ((r = d.mem.alloc(&sig, 2 * nd)) || (r = d.mem.alloc(&d.sig_g, 2 * nd))) return r;
         if (index && ((r = d.mem.alloc(&perm, nd)) || (r = d.mem.alloc(&perm_g, nd)))) return r;
         {

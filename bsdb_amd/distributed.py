@@ -121,20 +121,29 @@ def sharded_full_build(backend, sig_local, addr_local, n_global: int, width: int
     E = backend.zeros(m + 1)
     values = backend.zeros(_values_words(n_global))
     sigbits = backend.zeros((n_global * width + 63) // 64 + 1 if width else 1)
-    backend.build_range(sig_r, n_global, b_lo, b_hi, e_lo, width, E, values, sigbits if width else None)
-    # this rank's index slice; its lookups need E[b_hi]'s offset, which the
-    # next range owns (kept zero for the sum)
-    if b_hi < m:
-        E[b_hi] = e_lo + n_local
-    index = backend.index_slice(sig_r, addr_r, n_global, E, values, width, sigbits if width else None, e_lo,
-                                n_local)
-    if b_hi < m:
-        E[b_hi] = 0
-    # assemble the structure on rank 0: fields are disjoint bits, sum == or
+    if b_lo < b_hi:
+        backend.build_range(sig_r, n_global, b_lo, b_hi, e_lo, width, E, values, sigbits if width else None)
+        # this rank's index slice; its lookups need E[b_hi]'s offset, which the
+        # next range owns (kept zero for the sum)
+        if b_hi < m:
+            E[b_hi] = e_lo + n_local
+        index = backend.index_slice(sig_r, addr_r, n_global, E, values, width, sigbits if width else None, e_lo,
+                                    n_local)
+        if b_hi < m:
+            E[b_hi] = 0
+    else:
+        # more ranks than buckets: an empty range receives no keys (the owner
+        # map sends none here) but still joins the collectives below
+        if n_local:
+            raise RuntimeError(f"rank {rank} owns no buckets but received {n_local} keys")
+        index = backend.zeros(0)
+    # assemble the structure on rank 0: fields are disjoint bits, sum == or.
+    # Only rank 0's copy is defined after a reduce, so only rank 0 copies a
+    # host-side result back; every other rank keeps its own fields.
     for t in (E, values, sigbits):
         c = coll(t)
         dist.reduce(c, dst=0, op=dist.ReduceOp.SUM, group=group)
-        if c is not t:
+        if c is not t and rank == 0:
             t.copy_(c)
     return {"E": E, "values": values, "sigbits": sigbits if width else None, "index": index, "e_lo": e_lo,
             "n_local": n_local, "b_lo": b_lo, "b_hi": b_hi}

@@ -19,6 +19,12 @@ def golden():
     return dict(np.load(os.path.join(ROOT, "tests", "golden", "golden_v1.npz"), allow_pickle=False))
 
 
+@pytest.fixture(scope="session")
+def dump_golden():
+    import numpy as np
+    return dict(np.load(os.path.join(ROOT, "tests", "golden", "dump_v1.npz"), allow_pickle=False))
+
+
 def _ensure_oracle():
     import subprocess
     lib = os.path.join(ROOT, "oracle", "liboracle.so")

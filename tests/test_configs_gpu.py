@@ -122,11 +122,34 @@ def test_c5_checksum16_build_on_a_sample(ctx):
 
 
 def big_tmp(tmp_path, need_bytes):
-    """A directory with room for the index files (tmp, else /dev/shm)."""
-    for d in (str(tmp_path), "/dev/shm"):
-        if os.path.isdir(d) and shutil.disk_usage(d).free > need_bytes * 1.25:
-            return tempfile.mkdtemp(dir=d)
-    pytest.skip(f"no {need_bytes / 1e9:.0f} GB of scratch space for the index files")
+    """A directory with room for the index files: the candidate with the most
+    free space among pytest's tmp, /dev/shm, /tmp and the tree's build/.  A box
+    without room FAILS the config test (it never skips: VERDICT r2)."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    best, free = None, -1
+    for d in (str(tmp_path), "/dev/shm", "/tmp", os.path.join(root, "build")):
+        try:
+            os.makedirs(d, exist_ok=True)
+            f = shutil.disk_usage(d).free
+        except OSError:
+            continue
+        if f > free:
+            best, free = d, f
+    assert free > need_bytes * 1.1, f"no {need_bytes / 1e9:.0f} GB of scratch space for the index files (best {best}: {free / 1e9:.0f} GB)"
+    d = tempfile.mkdtemp(dir=best)
+    _SCRATCH.append(d)
+    return d
+
+
+_SCRATCH = []
+
+
+@pytest.fixture(autouse=True)
+def _remove_scratch():
+    """The multi-GB index files go away even when a test fails (/dev/shm is RAM)."""
+    yield
+    while _SCRATCH:
+        shutil.rmtree(_SCRATCH.pop(), ignore_errors=True)
 
 
 def records(first, n):

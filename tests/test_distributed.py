@@ -199,6 +199,10 @@ def run_e4(world, n, width, tmp_path, use_gpu, pg="gloo"):
     exp = np.zeros(n, ">u8")
     exp[ranks] = np.arange(n, dtype=np.uint64) * 48 + 4096
     assert open(path, "rb").read() == exp.tobytes()
+    # every other rank keeps its own fields (the reduce leaves only rank 0 defined)
+    for g in range(1, world):
+        lo, hi = res[g]["b_lo"], res[g]["b_hi"]
+        np.testing.assert_array_equal(res[g]["E"].view(np.uint64)[lo:hi], E[lo:hi])
 
 
 @pytest.mark.parametrize("world", [2, 3])
@@ -207,6 +211,12 @@ def test_gloo_multi_gpu_full_build_oracle_standins(world, tmp_path):
     one all-to-all, build their ranges, sum-reduce the structure and write
     their index.db slices; equal to the single-process build."""
     run_e4(world, 240_007, 4, tmp_path, use_gpu=False)
+
+
+def test_gloo_multi_gpu_full_build_more_ranks_than_buckets(tmp_path):
+    """world 3 over 2 000 keys (m = 2 buckets): rank 0 owns no bucket, receives
+    no keys, skips the range build and still joins every collective."""
+    run_e4(3, 2_000, 4, tmp_path, use_gpu=False)
 
 
 @pytest.mark.gpu

@@ -92,6 +92,30 @@ def test_lookup_arithmetic(golden, name):
     np.testing.assert_array_equal(got, res)
 
 
+def parse_dump(data: bytes):
+    """GOV.dump's raw layout (GOV:592-619 / mph.c:28-43): n, multiplier,
+    globalSeed, len(E), E[], len(array), array[] (native-endian u64)."""
+    w = np.frombuffer(data, "<u8")
+    n, mult, seed, ne = (int(x) for x in w[:4])
+    E = w[4: 4 + ne].copy()
+    na = int(w[4 + ne])
+    arr = w[5 + ne: 5 + ne + na].copy()
+    assert 5 + ne + na == w.size
+    return n, mult, seed, E, arr
+
+
+def test_dump_fixture_oracle_equals_reference_load_mph(dump_golden):
+    """A15: the committed GOV.dump file as the reference's load_mph +
+    mph_get_byte_array read it (tests/golden/make_golden_dump.py); the oracle's
+    reading of the same bytes gives the same ranks."""
+    n, mult, seed, E, arr = parse_dump(dump_golden["dump"].tobytes())
+    assert n == 30_000 and mult == 2 * (E.size - 1) and seed == 0 and E[-1] & ((1 << 56) - 1) == n
+    sig = O.hash_var(dump_golden["blob"], dump_golden["off"])
+    got = O.lookup_batch(sig, n, E, arr, 0, None, check=False)
+    np.testing.assert_array_equal(got, dump_golden["ref_rank"])
+    assert np.array_equal(np.sort(got), np.arange(n))
+
+
 def test_bucket_map_edges():
     m = 8_795_859
     assert O.bucket(0, m) == 0
