@@ -12,6 +12,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <functional>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -766,9 +767,9 @@ static void print_gov_profile(const std::vector<uint64_t> &h, uint32_t solve_gri
                                "store", "n_seeds", "n_bfs", "n_bfs_pops", "n_dense_rows", "n_dense_max",
                                "n_core", "n_blocks", "n_rows_in_blocks_over_440", "n_scc_sweeps",
                                "n_small_scc_fallbacks", "fvs_select", "fvs_forms", "fvs_gauss_jordan",
-                               "n_fail_degenerate", "n_fail_orient", "n_fail_singular", "failed_attempt_cycles",
+                               "n_fail_degenerate", "n_fail_orient", "n_fail_inconsistent", "failed_attempt_cycles",
                                "bfs_flip", "n_bfs_iters", "n_flip_steps", "n_sel_batches", "n_sel_picks",
-                               "sel_pick_cycles", "sel_prep_cycles"};
+                               "sel_pick_cycles", "sel_prep_cycles", "n_singular_solved", "n_null_vectors"};
     std::vector<double> tot(GP_N, 0.0);
     for (uint32_t w = 0; w < solve_grid; ++w)
         for (int k = 0; k < GP_N; ++k) {
@@ -785,47 +786,106 @@ struct DevFree {
     void operator()(void *p) const { if (p) (void)hipFree(p); }
 };
 
+// Where a GOV build takes its keys from: n_local signatures of the range
+// (sig != nullptr), or the keys themselves (fixed length or a var-len blob),
+// re-hashed and filtered to the range's buckets (the sequential range builds
+// of bsdb_dev_mph_build_index_passes: no signature array for the whole set).
+struct GovSrc {
+    const uint64_t *sig = nullptr;
+    uint64_t n = 0;  // signatures, or keys
+    const uint8_t *keys = nullptr;
+    const uint64_t *off = nullptr;
+    uint64_t blob_bytes = 0;
+    uint32_t key_len = 0;
+};
+
+// A13 fused into the solve: slot r - idx_lo of index_out gets key p's
+// byte-reversed address (addr[p] or addr_base + addr_stride * p).
+struct GovIndexOut {
+    uint64_t *index = nullptr;
+    uint64_t idx_lo = 0;
+    const uint64_t *addr = nullptr;
+    uint64_t addr_base = 0, addr_stride = 0;
+    // (optional) called once the range's key count is known, returns the
+    // slots' buffer (at least that many), nullptr when it cannot
+    std::function<uint64_t *(uint64_t n_local)> slots;
+};
+
+extern "C++" {
+template <int MODE>
+static void launch_sel(bsdb_ctx *c, const GovSrc &src, SelArgs &a, hipStream_t s) {
+    const uint32_t grid = grid_for(c, src.n);
+    if (!src.off && src.key_len == 13) k_sel<MODE, 0><<<grid, 256, 0, s>>>(a);
+    else if (!src.off) k_sel<MODE, 1><<<grid, 256, 0, s>>>(a);
+    else k_sel<MODE, 2><<<grid, 256, 0, s>>>(a);
+}
+}
+
 // A5 + A6 + A8 + A11 over the buckets [b_lo, b_hi) of a GOV structure on
 // n_global keys; d_sig = the n_local signatures of that range.  full: a whole
 // build (zeroes the outputs first); otherwise the caller zeroed full-size
 // outputs and E[b_hi] is cleared again unless b_hi == m (the next range owns it).
 // d_rank (optional, F2): the rank of input signature i at d_rank[i], from the
-// solve itself (n_local < 2^32).
-static int gov_build_impl(bsdb_ctx *c, const uint64_t *d_sig, uint64_t n_local, uint64_t n_global, uint64_t b_lo,
-                          uint64_t b_hi, uint64_t e_lo, uint32_t width, uint64_t *d_E, uint64_t *d_values,
-                          uint64_t *d_sigbits, int64_t *d_rank, hipStream_t s, bool full) {
+// solve itself.  With a key source the range's keys are found by re-hashing
+// every key, and *n_found (optional) returns how many there were.
+static int gov_build_impl(bsdb_ctx *c, const GovSrc &src, uint64_t n_global, uint64_t b_lo, uint64_t b_hi,
+                          uint64_t e_lo, uint32_t width, uint64_t *d_E, uint64_t *d_values, uint64_t *d_sigbits,
+                          int64_t *d_rank, const GovIndexOut &ixo_in, hipStream_t s, bool full, uint64_t *n_found = nullptr) {
     const uint64_t m = n_global / BUCKET_SIZE + 1, nb = b_hi - b_lo;
     const uint32_t mult = (uint32_t)(2 * m);
+    const bool from_keys = src.sig == nullptr;
     int rc;
-    if ((rc = grow(&c->g_sorted, &c->g_sorted_bytes, std::max<uint64_t>(n_local, 1) * 16))) return rc;
     if ((rc = grow(&c->g_counts, &c->g_counts_bytes, std::max<uint64_t>(nb, 1) * 4))) return rc;
     if ((rc = grow(&c->g_cursor, &c->g_cursor_bytes, std::max<uint64_t>(nb, 1) * 8))) return rc;
     if ((rc = grow(&c->g_status, &c->g_status_bytes, 16))) return rc;
-    if (d_rank && n_local >= (1ULL << 32)) return BSDB_EINVAL;
-    uint32_t *pay = nullptr;
-    if (d_rank) {
-        if ((rc = grow(&c->g_pay, &c->g_pay_bytes, std::max<uint64_t>(n_local, 1) * 4))) return rc;
-        pay = (uint32_t *)c->g_pay;
+    uint32_t *counts = (uint32_t *)c->g_counts, *status = (uint32_t *)c->g_status;
+    HIP_OK(hipMemsetAsync(counts, 0, std::max<uint64_t>(nb, 1) * 4, s));
+    HIP_OK(hipMemsetAsync(status, 0, 16, s));
+    if (full) HIP_OK(hipMemsetAsync(d_values, 0, bsdb_values_words(n_global) * 8, s));
+    uint64_t *Eb = d_E + b_lo;
+    SelArgs sel{src.keys, src.off, src.blob_bytes, src.n, src.key_len, mult, (uint32_t)b_lo, (uint32_t)nb,
+                counts, nullptr, nullptr, nullptr};
+    if (from_keys) {
+        if (src.n) launch_sel<0>(c, src, sel, s);
+    } else if (src.n) {
+        k_bucket_count<<<grid_for(c, src.n), 256, 0, s>>>(src.sig, src.n, mult, (uint32_t)b_lo, counts);
+    }
+    if ((rc = edge_offsets_impl(c, counts, nb, Eb, s))) return rc;  // A6: Eb[0..nb]
+    if (e_lo) k_add_base<<<grid_for(c, nb + 1), 256, 0, s>>>(Eb, nb + 1, e_lo);
+    uint64_t n_local = src.n;
+    if (from_keys) {  // the range's key count: its last offset
+        uint64_t eh = 0;
+        HIP_OK(hipMemcpyAsync(&eh, Eb + nb, 8, hipMemcpyDeviceToHost, s));
+        HIP_OK(hipStreamSynchronize(s));
+        n_local = (eh & OFFSET_MASK) - e_lo;
+    }
+    if (n_found) *n_found = n_local;
+    if (e_lo + n_local > n_global) return BSDB_EINVAL;
+    GovIndexOut ixo = ixo_in;
+    if (ixo.slots && !(ixo.index = ixo.slots(n_local))) return BSDB_ENOMEM;
+    if ((rc = grow(&c->g_sorted, &c->g_sorted_bytes, std::max<uint64_t>(n_local, 1) * 16))) return rc;
+    uint64_t *pay = nullptr;
+    if (d_rank || ixo.index || from_keys) {  // (a key source always records positions)
+        if ((rc = grow(&c->g_pay, &c->g_pay_bytes, std::max<uint64_t>(n_local, 1) * 8))) return rc;
+        pay = (uint64_t *)c->g_pay;
     }
     const uint32_t big_cap = (uint32_t)(n_local / (GS_CMAX + 1) + 1);
     if ((rc = grow(&c->g_big, &c->g_big_bytes, (size_t)big_cap * 4))) return rc;
     const uint32_t solve_grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(nb, (uint64_t)c->num_cus * GS_PER_CU));
     if ((rc = grow(&c->g_scratch, &c->g_scratch_bytes, (size_t)solve_grid * solve_scratch_words<SolveLds>() * 8)))
         return rc;
-    uint32_t *counts = (uint32_t *)c->g_counts, *status = (uint32_t *)c->g_status;
     uint64_t *sorted = (uint64_t *)c->g_sorted;
-    HIP_OK(hipMemsetAsync(counts, 0, std::max<uint64_t>(nb, 1) * 4, s));
-    HIP_OK(hipMemsetAsync(status, 0, 16, s));
-    if (full) HIP_OK(hipMemsetAsync(d_values, 0, bsdb_values_words(n_global) * 8, s));
-    const uint32_t grid = grid_for(c, n_local);
-    uint64_t *Eb = d_E + b_lo;
-    if (n_local) k_bucket_count<<<grid, 256, 0, s>>>(d_sig, n_local, mult, (uint32_t)b_lo, counts);
-    if ((rc = edge_offsets_impl(c, counts, nb, Eb, s))) return rc;  // A6: Eb[0..nb]
-    if (e_lo) k_add_base<<<grid_for(c, nb + 1), 256, 0, s>>>(Eb, nb + 1, e_lo);
     k_cursor_init<<<grid_for(c, nb), 256, 0, s>>>(Eb, nb, e_lo, (uint64_t *)c->g_cursor);
-    if (n_local)
-        k_bucket_scatter<<<grid, 256, 0, s>>>(d_sig, n_local, mult, (uint32_t)b_lo, (unsigned long long *)c->g_cursor,
-                                              sorted, pay);
+    if (from_keys) {
+        sel.cursor = (unsigned long long *)c->g_cursor;
+        sel.sorted = sorted;
+        sel.pay = pay;
+        if (src.n) launch_sel<1>(c, src, sel, s);
+    } else if (n_local) {
+        k_bucket_scatter<<<grid_for(c, n_local), 256, 0, s>>>(src.sig, n_local, mult, (uint32_t)b_lo,
+                                                              (unsigned long long *)c->g_cursor, sorted, pay);
+    }
+    const uint32_t grid = grid_for(c, n_local);
     k_bucket_sort<<<(uint32_t)std::min<uint64_t>(nb, (uint64_t)c->num_cus * 8), 256, 0, s>>>(sorted, Eb, nb, e_lo,
                                                                                               status, pay);  // A5
     k_big_list<<<grid_for(c, nb), 256, 0, s>>>(Eb, nb, status, (uint32_t *)c->g_big, big_cap);
@@ -839,7 +899,7 @@ static int gov_build_impl(bsdb_ctx *c, const uint64_t *d_sig, uint64_t n_local, 
     const uint32_t big_grid = std::min<uint32_t>(nbig, 8);
     if (nbig) {
         // oversized buckets: per-workgroup slabs for the sort, then the solver
-        const size_t sort_bytes = (size_t)big_grid * GB_CMAX * (16 + 4);  // signatures + payloads
+        const size_t sort_bytes = (size_t)big_grid * GB_CMAX * (16 + 8);  // signatures + payloads
         if ((rc = grow(&c->g_slabs, &c->g_slabs_bytes, std::max(sort_bytes, (size_t)big_grid * big_slab_bytes()))))
             return rc;
         k_bucket_sort_big<<<big_grid, GB_THREADS, 0, s>>>(sorted, Eb, e_lo, (const uint32_t *)c->g_big, nbig,
@@ -859,9 +919,10 @@ static int gov_build_impl(bsdb_ctx *c, const uint64_t *d_sig, uint64_t n_local, 
     uint32_t fvs_max = FVS_NH_MAX;
     if (const char *v = getenv("BSDB_GOV_FVS_MAX")) fvs_max = (uint32_t)std::max(2, std::min(atoi(v), (int)FVS_NH_MAX));
     if (width && full) HIP_OK(hipMemsetAsync(d_sigbits, 0, ((n_global * width + 63) / 64 + 1) * 8, s));
-    // A8, with A11 (checksum bits at each rank) and F2 (ranks) in the solve
+    // A8, with A11 (checksum bits at each rank), F2 (ranks) and A13 (index
+    // slots) in the solve
     SolveArgs sa{sorted, b_hi, d_E, d_values, (uint64_t *)c->g_scratch, status, d_prof, fvs_max, b_lo, e_lo,
-                 d_sigbits, width, pay, d_rank};
+                 d_sigbits, width, pay, d_rank, ixo.index, ixo.idx_lo, ixo.addr, ixo.addr_base, ixo.addr_stride};
     // zeroing status[2] (the bucket queue) above happens before both launches
     k_gov_solve<<<solve_grid, GS_THREADS, 0, s>>>(sa);  // A8
     if (nbig)
@@ -896,6 +957,17 @@ static int gov_build_impl(bsdb_ctx *c, const uint64_t *d_sig, uint64_t n_local, 
     return BSDB_OK;
 }
 
+// the signature form used by the existing entry points
+static int gov_build_impl(bsdb_ctx *c, const uint64_t *d_sig, uint64_t n_local, uint64_t n_global, uint64_t b_lo,
+                          uint64_t b_hi, uint64_t e_lo, uint32_t width, uint64_t *d_E, uint64_t *d_values,
+                          uint64_t *d_sigbits, int64_t *d_rank, hipStream_t s, bool full) {
+    GovSrc src;
+    src.sig = d_sig ? d_sig : reinterpret_cast<const uint64_t *>(16);  // (n_local == 0: never read)
+    src.n = n_local;
+    return gov_build_impl(c, src, n_global, b_lo, b_hi, e_lo, width, d_E, d_values, d_sigbits, d_rank, GovIndexOut{}, s,
+                          full);
+}
+
 int bsdb_dev_gov_build(bsdb_ctx *c, const uint64_t *d_sig, uint64_t n, uint32_t width, uint64_t *d_E,
                        uint64_t *d_values, uint64_t *d_sigbits, void *stream) {
     const uint64_t m = n / BUCKET_SIZE + 1;
@@ -913,7 +985,7 @@ int bsdb_dev_gov_build_ranks(bsdb_ctx *c, const uint64_t *d_sig, uint64_t n, uin
                              uint64_t *d_values, uint64_t *d_sigbits, int64_t *d_rank, void *stream) {
     const uint64_t m = n / BUCKET_SIZE + 1;
     if (!c || width > 64 || !d_E || !d_values || (n && (!d_sig || !d_rank)) || (width && !d_sigbits) ||
-        !aligned16(d_sig) || m > 0x7FFFFFFFULL || n >= (1ULL << 32))
+        !aligned16(d_sig) || m > 0x7FFFFFFFULL)
         return BSDB_EINVAL;
     std::lock_guard<std::mutex> g(c->mu);
     HIP_OK(hipSetDevice(c->device));
@@ -933,7 +1005,6 @@ int bsdb_dev_gov_build_range(bsdb_ctx *c, const uint64_t *d_sig, uint64_t n_loca
     HIP_OK(hipSetDevice(c->device));
     hipStream_t s = pick(c, stream);
     Ordered ord(c, s);
-    if (d_rank && n_local >= (1ULL << 32)) return BSDB_EINVAL;
     return gov_build_impl(c, d_sig, n_local, n_global, b_lo, b_hi, e_lo, width, d_E, d_values, d_sigbits, d_rank, s,
                           false);
 }
@@ -1228,3 +1299,4 @@ int bsdb_hash_var(bsdb_ctx *c, const uint8_t *h_blob, const uint64_t *h_off, uin
 #include "capi_comm.hip"
 #include "capi_mph.hip"
 #include "capi_multi.hip"
+#include "capi_passes.hip"

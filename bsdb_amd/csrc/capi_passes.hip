@@ -1,0 +1,159 @@
+// capi_passes.hip -- the full build of a key set resident in ONE device's HBM
+// (BASELINE C4: 13 193 787 549 x 13 B = 171.5 GB of keys; C5: 4e9 var-len)
+// by sequential bucket-range passes.  Included by bsdb_capi.hip.
+//   CBHS = src/main/java/it/unimi/dsi/sux4j/io/ConcurrentBucketedHashStore.java
+//   GOV  = src/main/java/it/unimi/dsi/sux4j/mph/GOVMinimalPerfectHashFunctionModified.java
+//   W    = src/main/java/tech/bsdb/write/BSDBWriter.java
+//
+// The reference builds README-size sets in bounded memory: every key's
+// signature is spilled to one of 256 segment files by its top byte
+// (CBHS:379-395, 497-508), and the segments are read back, sorted and solved
+// one at a time (CBHS:852-978 feeding GOV:385-448).  A segment is a contiguous
+// sig0 range and so a contiguous bucket range (the bucket is monotone in sig0,
+// CBHS:129-138).  Here the keys stay resident and pass p of P covers buckets
+// [p*m/P, (p+1)*m/P): every key is re-hashed and the range's keys are
+// grouped by bucket with their input position (no spill and no 16-B/key
+// signature array: 211 GB at C4), then sorted, solved and signed (A5-A11);
+// the solve writes each key's index.db slot itself (A13 with F2: no getLong
+// pass).  A pass's slots are contiguous, [E[b_lo], E[b_hi]), and are copied to
+// the caller's host array while the next pass runs.
+
+namespace {
+
+// device bytes per key of one pass: sorted signature + position payload, plus
+// the pass's index slots (twice when they go to host memory: one buffer is
+// copied out while the next pass fills the other)
+uint64_t pass_bytes_per_key(bool dev_index, bool host_index) {
+    return 16 + 8 + (dev_index ? 0 : host_index ? 16 : 0);
+}
+
+int passes_build(bsdb_ctx *c, const GovSrc &src, uint64_t n, uint32_t width, uint32_t passes, const uint64_t *d_addr,
+                 uint64_t addr_base, uint64_t addr_stride, uint64_t *d_E, uint64_t *d_values, uint64_t *d_sigbits,
+                 uint64_t *d_index, uint64_t *h_index, uint32_t *passes_used, hipStream_t s) {
+    const uint64_t m = n / BUCKET_SIZE + 1;
+    if (passes == 0) {
+        // the fewest passes whose working set fits 85 % of the free HBM (the
+        // solver scratch and the per-bucket arrays come on top: ~10 GB)
+        size_t free_b = 0, total_b = 0;
+        HIP_OK(hipMemGetInfo(&free_b, &total_b));
+        const double room = 0.85 * (double)free_b - 12e9;
+        const double need = 1.05 * (double)n * (double)pass_bytes_per_key(d_index != nullptr, h_index != nullptr);
+        passes = room <= 0 ? 64u : (uint32_t)std::min(64.0, std::max(1.0, std::ceil(need / room)));
+    }
+    passes = (uint32_t)std::min<uint64_t>(passes, m);
+    if (passes_used) *passes_used = passes;
+    HIP_OK(hipMemsetAsync(d_values, 0, bsdb_values_words(n) * 8, s));
+    if (width) HIP_OK(hipMemsetAsync(d_sigbits, 0, ((n * width + 63) / 64 + 1) * 8, s));
+    // host index: two device slice buffers; the copy of pass p's slots runs on
+    // a thread of its own (own stream) while pass p+1 solves into the other
+    void *slice[2] = {nullptr, nullptr};
+    size_t slice_bytes[2] = {0, 0};
+    std::thread copier[2];
+    int copy_rc[2] = {BSDB_OK, BSDB_OK};
+    auto join = [&](int i) {
+        if (copier[i].joinable()) copier[i].join();
+        return copy_rc[i];
+    };
+    auto finish = [&](int rc) {
+        for (int i = 0; i < 2; ++i) {
+            const int r = join(i);
+            if (!rc) rc = r;
+        }
+        (void)hipSetDevice(c->device);
+        for (void *q : slice) (void)hipFree(q);
+        return rc;
+    };
+    uint64_t e_lo = 0;
+    for (uint32_t p = 0; p < passes; ++p) {
+        const uint64_t b_lo = (uint64_t)p * m / passes, b_hi = (uint64_t)(p + 1) * m / passes;
+        if (b_lo >= b_hi) continue;
+        const int sl = (int)(p & 1);
+        GovIndexOut ixo;
+        ixo.addr = d_addr;
+        ixo.addr_base = addr_base;
+        ixo.addr_stride = addr_stride;
+        if (d_index) {
+            ixo.index = d_index;  // global slots
+        } else if (h_index) {
+            ixo.idx_lo = e_lo;
+            ixo.slots = [&](uint64_t nl) -> uint64_t * {
+                if (join(sl)) return nullptr;  // the copy out of this buffer (pass p-2) is done
+                if (grow(&slice[sl], &slice_bytes[sl], std::max<uint64_t>(nl, 1) * 8)) return nullptr;
+                return (uint64_t *)slice[sl];
+            };
+        }  // (neither: the structure only)
+        uint64_t nl = 0;
+        int rc = gov_build_impl(c, src, n, b_lo, b_hi, e_lo, width, d_E, d_values, d_sigbits, nullptr, ixo, s, false, &nl);
+        if (rc) return finish(rc);
+        if (h_index && nl) {  // gov_build_impl returned after the device finished
+            uint64_t *dst = h_index + e_lo;
+            const void *src_slots = slice[sl];
+            const int dev = c->device;
+            copy_rc[sl] = BSDB_OK;
+            copier[sl] = std::thread([&, dst, src_slots, nl, dev, sl] {
+                hipStream_t cs = nullptr;
+                int r = BSDB_OK;
+                if (hipSetDevice(dev) != hipSuccess || hipStreamCreateWithFlags(&cs, hipStreamNonBlocking) != hipSuccess ||
+                    hipMemcpyAsync(dst, src_slots, nl * 8, hipMemcpyDeviceToHost, cs) != hipSuccess ||
+                    hipStreamSynchronize(cs) != hipSuccess)
+                    r = BSDB_EIO;
+                if (cs) (void)hipStreamDestroy(cs);
+                copy_rc[sl] = r;
+            });
+        }
+        e_lo += nl;
+    }
+    const int rc = finish(BSDB_OK);
+    if (rc) return rc;
+    return e_lo == n ? BSDB_OK : BSDB_EIO;
+}
+
+int passes_entry(bsdb_ctx *c, const GovSrc &src, uint64_t n, uint32_t width, uint32_t passes, const uint64_t *d_addr,
+                 uint64_t addr_base, uint64_t addr_stride, uint64_t *d_E, uint64_t *d_values, uint64_t *d_sigbits,
+                 uint64_t *d_index, uint64_t *h_index, uint32_t *passes_used, void *stream) {
+    const uint64_t m = n / BUCKET_SIZE + 1;
+    if (!c || width > 64 || !d_E || !d_values || (width && !d_sigbits) || m > 0x7FFFFFFFULL || passes > 4096 ||
+        (d_index && h_index) || (n && !src.keys))
+        return BSDB_EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    HIP_OK(hipSetDevice(c->device));
+    hipStream_t s = pick(c, stream);
+    Ordered ord(c, s);
+    return passes_build(c, src, n, width, passes, d_addr, addr_base, addr_stride, d_E, d_values, d_sigbits, d_index,
+                        h_index, passes_used, s);
+}
+
+}  // namespace
+
+extern "C" {
+
+int bsdb_dev_mph_build_index_passes_fixed(bsdb_ctx *c, const uint8_t *d_keys, uint32_t key_len, uint64_t n,
+                                          uint32_t width, uint32_t passes, const uint64_t *d_addr, uint64_t addr_base,
+                                          uint64_t addr_stride, uint64_t *d_E, uint64_t *d_values, uint64_t *d_sigbits,
+                                          uint64_t *d_index, uint64_t *h_index, uint32_t *passes_used, void *stream) {
+    if (bad_key_len(key_len)) return BSDB_EINVAL;
+    GovSrc src;
+    src.keys = d_keys;
+    src.n = n;
+    src.key_len = key_len;
+    src.blob_bytes = n * key_len;
+    return passes_entry(c, src, n, width, passes, d_addr, addr_base, addr_stride, d_E, d_values, d_sigbits, d_index,
+                        h_index, passes_used, stream);
+}
+
+int bsdb_dev_mph_build_index_passes_var(bsdb_ctx *c, const uint8_t *d_blob, uint64_t blob_bytes, const uint64_t *d_off,
+                                        uint64_t n, uint32_t width, uint32_t passes, const uint64_t *d_addr,
+                                        uint64_t addr_base, uint64_t addr_stride, uint64_t *d_E, uint64_t *d_values,
+                                        uint64_t *d_sigbits, uint64_t *d_index, uint64_t *h_index,
+                                        uint32_t *passes_used, void *stream) {
+    if (n && !d_off) return BSDB_EINVAL;
+    GovSrc src;
+    src.keys = d_blob;
+    src.off = d_off;
+    src.n = n;
+    src.blob_bytes = blob_bytes;
+    return passes_entry(c, src, n, width, passes, d_addr, addr_base, addr_stride, d_E, d_values, d_sigbits, d_index,
+                        h_index, passes_used, stream);
+}
+
+}  // extern "C"

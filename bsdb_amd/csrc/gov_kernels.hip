@@ -51,6 +51,10 @@ constexpr int GB_THREADS = 256;  // sort of an oversized bucket
 // over the whole block).  SolveArgs::fvs_max may lower it (tests force the
 // fallback with it); the result is the block's unique solution either way.
 constexpr uint32_t FVS_NH_MAX = 380;
+// FVS blocks whose heavy system is singular but consistent: at most NB_MAX
+// null vectors are reduced in place (more fall back to Gauss-Jordan over the
+// whole block, which reaches the same solution)
+constexpr uint32_t NB_MAX = 128;
 
 enum GovStatus : uint32_t { GOV_TOO_BIG = 1u, GOV_SEEDS = 2u, GOV_DUP = 4u, GOV_VERIFY = 8u };
 
@@ -80,13 +84,13 @@ __global__ __launch_bounds__(256) void k_cursor_init(const uint64_t *Eb, uint64_
 // pay_out (optional): the input position of each sorted signature (F2: the
 // solver then writes each input's rank without a lookup pass)
 __global__ __launch_bounds__(256) void k_bucket_scatter(const uint64_t *sig, uint64_t n, uint32_t mult, uint32_t b0,
-                                                        unsigned long long *cursor, uint64_t *out, uint32_t *pay_out) {
+                                                        unsigned long long *cursor, uint64_t *out, uint64_t *pay_out) {
     const uint64_t stride = (uint64_t)gridDim.x * 256;
     for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
         const ulonglong2 s = reinterpret_cast<const ulonglong2 *>(sig)[i];
         const uint64_t pos = atomicAdd(cursor + (bucket_of_w(w64(s.x), mult) - b0), 1ULL);
         reinterpret_cast<ulonglong2 *>(out)[pos] = s;
-        if (pay_out) pay_out[pos] = (uint32_t)i;
+        if (pay_out) pay_out[pos] = i;
     }
 }
 
@@ -95,10 +99,10 @@ __device__ __forceinline__ bool sig_less(ulonglong2 a, ulonglong2 b) { return a.
 // Bitonic sort of one bucket in LDS (padded with all-ones sentinels) +
 // duplicate check on neighbours (CBHS:969-972).
 __global__ __launch_bounds__(256) void k_bucket_sort(uint64_t *sig, const uint64_t *Eb, uint64_t nb, uint64_t e0,
-                                                     uint32_t *status, uint32_t *pay) {
+                                                     uint32_t *status, uint64_t *pay) {
     constexpr int P2MAX = 1 << (32 - __builtin_clz(GS_CMAX - 1));  // the bitonic sort pads to a power of 2
     __shared__ ulonglong2 s[P2MAX];
-    __shared__ uint32_t sp[P2MAX];  // payloads (pay != nullptr), moved with their signatures
+    __shared__ uint64_t sp[P2MAX];  // payloads (pay != nullptr), moved with their signatures
     for (uint64_t b = blockIdx.x; b < nb; b += gridDim.x) {
         const uint64_t lo = (Eb[b] & OFFSET_MASK) - e0, hi = (Eb[b + 1] & OFFSET_MASK) - e0;
         const uint32_t cnt = (uint32_t)(hi - lo);
@@ -123,7 +127,7 @@ __global__ __launch_bounds__(256) void k_bucket_sort(uint64_t *sig, const uint64
                             s[i] = c;
                             s[l] = a;
                             if (pay) {
-                                const uint32_t t = sp[i];
+                                const uint64_t t = sp[i];
                                 sp[i] = sp[l];
                                 sp[l] = t;
                             }
@@ -164,9 +168,9 @@ __global__ __launch_bounds__(256) void k_big_list(const uint64_t *Eb, uint64_t n
 // a per-workgroup global slab of GB_CMAX entries (padded with sentinels).
 __global__ __launch_bounds__(GB_THREADS) void k_bucket_sort_big(uint64_t *sig, const uint64_t *Eb, uint64_t e0,
                                                                 const uint32_t *list, uint32_t nbig, ulonglong2 *slab,
-                                                                uint32_t *status, uint32_t *pay) {
+                                                                uint32_t *status, uint64_t *pay) {
     ulonglong2 *s = slab + (size_t)blockIdx.x * GB_CMAX;
-    uint32_t *sp = reinterpret_cast<uint32_t *>(slab + (size_t)gridDim.x * GB_CMAX) + (size_t)blockIdx.x * GB_CMAX;
+    uint64_t *sp = reinterpret_cast<uint64_t *>(slab + (size_t)gridDim.x * GB_CMAX) + (size_t)blockIdx.x * GB_CMAX;
     for (uint32_t li = blockIdx.x; li < nbig; li += gridDim.x) {
         const uint32_t b = list[li];
         const uint64_t lo = (Eb[b] & OFFSET_MASK) - e0, hi = (Eb[b + 1] & OFFSET_MASK) - e0;
@@ -191,7 +195,7 @@ __global__ __launch_bounds__(GB_THREADS) void k_bucket_sort_big(uint64_t *sig, c
                             s[i] = c;
                             s[l] = a;
                             if (pay) {
-                                const uint32_t t = sp[i];
+                                const uint64_t t = sp[i];
                                 sp[i] = sp[l];
                                 sp[l] = t;
                             }
@@ -227,16 +231,24 @@ struct SolveArgs {
     // 2-bit values, GOV:557-580, as those sit at the hinges)
     uint64_t *sigbits;    // checksum bit list (width > 0): sig0 & mask at each rank (GOV:492-508)
     uint32_t width;
-    const uint32_t *pay;  // input position of each sorted signature (rank_out only)
+    const uint64_t *pay;  // input position of each sorted signature (rank_out / index_out)
     int64_t *rank_out;    // optional: rank of input signature i at [i]
+    // optional, A13 fused into the solve (W:129-145): the key at input
+    // position p has index.db slot r = its rank; index_out[r - idx_lo] =
+    // byte-reversed address, addr[p] or addr_base + addr_stride * p
+    uint64_t *index_out;
+    uint64_t idx_lo;
+    const uint64_t *addr;
+    uint64_t addr_base, addr_stride;
 };
 
 // phase counters (cycles, or counts for the GP_N_* slots)
 enum GovProf { GP_EDGES, GP_PEEL, GP_GREEDY, GP_BFS, GP_TARJAN, GP_SINGLE, GP_DENSE, GP_BACK, GP_STORE,
                GP_N_SEEDS, GP_N_BFS, GP_N_BFS_POPS, GP_N_DENSE_ROWS, GP_N_DENSE_MAX, GP_N_CORE, GP_N_BLOCKS, GP_N_BIG_ROWS,
                GP_N_SCC_SWEEPS, GP_N_SMALL_S, GP_FVS_SEL, GP_FVS_FORMS, GP_FVS_GJ,
-               GP_N_FAIL_DEGEN, GP_N_FAIL_ORIENT, GP_N_FAIL_SINGULAR, GP_FAILED_CYCLES, GP_BFS_FLIP, GP_N_BFS_ITERS,
-               GP_N_FLIP_STEPS, GP_N_SEL_BATCHES, GP_N_SEL_PICKS, GP_SEL_PICK_CYCLES, GP_SEL_PREP_CYCLES, GP_N };
+               GP_N_FAIL_DEGEN, GP_N_FAIL_ORIENT, GP_N_FAIL_INCONS, GP_FAILED_CYCLES, GP_BFS_FLIP, GP_N_BFS_ITERS,
+               GP_N_FLIP_STEPS, GP_N_SEL_BATCHES, GP_N_SEL_PICKS, GP_SEL_PICK_CYCLES, GP_SEL_PREP_CYCLES,
+               GP_N_SING_SOLVED, GP_N_NULL_VECS, GP_N };
 
 // Solver state for buckets of up to CMAX_ keys: LDS for GS_CMAX, a global
 // slab per workgroup for GB_CMAX (same code; indices fit int16 either way).
@@ -268,6 +280,7 @@ struct SolveLdsT {
     int16_t comp_end[CMAX];  // end (exclusive) of component c in members
     int16_t col_of[CMAX];
     uint32_t ncomp, flag, pivot, rounds, chg, nleft, nscc, qtail;
+    uint32_t nfree, npos;    // Gauss-Jordan: free columns; null-space reduction: last nonzero + 1
     uint32_t hbin[64];       // FVS selection: open members per in-degree
     __device__ uint32_t *pend() { return reinterpret_cast<uint32_t *>(prow); }
     __device__ uint64_t *hs() { return reinterpret_cast<uint64_t *>(deg); }
@@ -282,6 +295,9 @@ static_assert(sizeof(SolveLds) + 64 <= 160 * 1024 / GS_PER_CU, "GS_PER_CU solver
 // per-workgroup global scratch of the dense phase (bit-sliced rows, forms)
 template <class Lds>
 constexpr size_t solve_scratch_words() { return (size_t)2 * Lds::CMAX * Lds::WMAX; }
+// FVS null vectors (bytes) at word 30 CMAX of the scratch, past the forms
+// (words [16, 28) CMAX) and the reverse dependency CSR ([28, 29.5) CMAX)
+static_assert(30 * 8 + NB_MAX <= 8 * 2 * GS_WMAX, "FVS null-vector basis fits the dense scratch");
 
 __device__ __forceinline__ void gf3_add(uint64_t &x1, uint64_t &x2, uint64_t y1, uint64_t y2) {
     const uint64_t a1 = x1, a2 = x2;
@@ -845,6 +861,26 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
         // dense block c
         const uint32_t beg = c ? (uint32_t)L.comp_end[c - 1] : 0;
         const uint32_t sz = (uint32_t)L.comp_end[c] - beg;
+        // the block's columns in increasing edge order (the order that
+        // defines the solution of a singular block, see gauss_jordan): S
+        // comes out of the ordered compaction sorted, Tarjan's blocks in stack
+        // order are ranked (tiny, or rare: no big S)
+        {
+            bool unsorted = false;
+            for (uint32_t i = tid; i + 1 < sz; i += GS_THREADS) unsorted |= L.members[beg + i] > L.members[beg + i + 1];
+            if (__syncthreads_or(unsorted)) {
+                int16_t *tmp = L.a3;  // (Tarjan's stack is dead; the FVS queue comes later)
+                for (uint32_t i = tid; i < sz; i += GS_THREADS) {
+                    const int16_t k = L.members[beg + i];
+                    uint32_t rk = 0;
+                    for (uint32_t j = 0; j < sz; ++j) rk += L.members[beg + j] < k;
+                    tmp[rk] = k;
+                }
+                __syncthreads();
+                for (uint32_t i = tid; i < sz; i += GS_THREADS) L.members[beg + i] = tmp[i];
+                __syncthreads();
+            }
+        }
         for (uint32_t i = tid; i < sz; i += GS_THREADS) L.col_of[L.members[beg + i]] = (int16_t)i;
         __syncthreads();
         // Rows live word-major in the workgroup's scratch: plane q (the two
@@ -856,10 +892,15 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
 
         // Gauss-Jordan on rows 0..n-1 of X (n equations, n unknowns, the
         // right-hand side in column n), without row swaps: column cc's pivot
-        // is the first unused row with a nonzero there, piv[cc] remembers it.
-        // A nonsingular square system has ONE solution whatever the pivots,
-        // so the values equal the oracle's row-swapping elimination.
-        // colval[cc] = x_cc.  ONE barrier per column: every row reads the
+        // is the first unused row with a nonzero there, piv[cc] remembers it
+        // (-1: no such row, a free column).  The result is the reduced row
+        // echelon form up to the order of its rows, whatever the pivot rows,
+        // so the pivot columns, and the solution with every free column 0,
+        // equal the oracle's row-swapping elimination.  Returns whether the
+        // system is consistent (every row left without a pivot reads 0 = 0);
+        // colval[cc] = x_cc, L.nfree = the free columns (GOV:425-432: only an
+        // inconsistent system is "unsolvable" and moves to the next seed).
+        // ONE barrier per column: every row reads the
         // pivot row where it lies (its owner last wrote it before the
         // previous barrier and leaves it alone in its own column); while a
         // row is eliminated it bids for the next column's pivot (the lowest
@@ -873,6 +914,7 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
             uint32_t *bid = L.hbin;  // bid[cc % 3]
             for (uint32_t rr = tid; rr < n; rr += GS_THREADS) used[rr] = 0;
             if (tid < 3) bid[tid] = 0xFFFFFFFFu;
+            if (tid == 0) L.nfree = 0;
             __threadfence_block();
             __syncthreads();
             for (uint32_t rr = tid; rr < n; rr += GS_THREADS) {
@@ -881,12 +923,23 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
                 if (cand && (uint32_t)__builtin_ctzll(bal) == (tid & 63)) atomicMin(&bid[0], rr);
             }
             __syncthreads();
-            bool ok = true;
             for (uint32_t cc = 0; cc < n; ++cc) {
                 const uint32_t p = bid[cc % 3];
-                if (p == 0xFFFFFFFFu) {  // singular (uniform)
-                    ok = false;
-                    break;
+                if (p == 0xFFFFFFFFu) {  // a free column (uniform): x_cc = 0
+                    const uint32_t cn = cc + 1, wn = cn >> 6;
+                    const uint64_t nbit = 1ULL << (cn & 63);
+                    if (tid == 0) {
+                        piv[cc] = -1;
+                        ++L.nfree;
+                        bid[(cc + 2) % 3] = 0xFFFFFFFFu;
+                    }
+                    for (uint32_t rr = tid; rr < n; rr += GS_THREADS) {
+                        const bool cand = cn < n && !used[rr] && ((X(rr, wn, 0) | X(rr, wn, 1)) & nbit);
+                        const uint64_t bal = __builtin_amdgcn_ballot_w64(cand);
+                        if (cand && (uint32_t)__builtin_ctzll(bal) == (tid & 63)) atomicMin(&bid[cn % 3], rr);
+                    }
+                    __syncthreads();
+                    continue;
                 }
                 const uint32_t wc = cc >> 6;
                 const uint64_t bit = 1ULL << (cc & 63);
@@ -919,18 +972,27 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
                 }
                 __syncthreads();
             }
-            if (ok)
-                // column cc's pivot row reads cf * x = rhs with cf in {1, 2}
-                // (every other column eliminated), so x = cf * rhs mod 3
-                for (uint32_t cc = tid; cc < n; cc += GS_THREADS) {
-                    const uint32_t pr = (uint32_t)piv[cc];
-                    const uint64_t rbit = 1ULL << (n & 63), cbit = 1ULL << (cc & 63);
-                    const uint32_t rhs = (X(pr, n >> 6, 0) & rbit) ? 1 : (X(pr, n >> 6, 1) & rbit) ? 2 : 0;
-                    const uint32_t cf = (X(pr, cc >> 6, 1) & cbit) ? 2 : 1;
-                    colval[cc] = (uint8_t)(cf * rhs % 3);
+            // column cc's pivot row reads cf * x + (free columns, all 0) = rhs
+            // with cf in {1, 2} (every other pivot column eliminated), so
+            // x = cf * rhs mod 3; a row without a pivot is all zero and must
+            // read rhs = 0
+            const uint64_t rbit = 1ULL << (n & 63);
+            for (uint32_t cc = tid; cc < n; cc += GS_THREADS) {
+                const int pr = piv[cc];
+                if (pr < 0) {
+                    colval[cc] = 0;
+                    continue;
                 }
-            else if (tid == 0)
-                L.flag = 0;
+                const uint64_t cbit = 1ULL << (cc & 63);
+                const uint32_t rhs = (X(pr, n >> 6, 0) & rbit) ? 1 : (X(pr, n >> 6, 1) & rbit) ? 2 : 0;
+                const uint32_t cf = (X(pr, cc >> 6, 1) & cbit) ? 2 : 1;
+                colval[cc] = (uint8_t)(cf * rhs % 3);
+            }
+            bool bad = false;
+            for (uint32_t rr = tid; rr < n; rr += GS_THREADS)
+                if (!used[rr] && ((X(rr, n >> 6, 0) | X(rr, n >> 6, 1)) & rbit)) bad = true;
+            const bool ok = !__syncthreads_or(bad);
+            if (!ok && tid == 0) L.flag = 0;
             __syncthreads();
             return ok;
         };
@@ -942,8 +1004,11 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
         // (vectors over nH heavy columns + a constant column), the heavy
         // hinges' own equations are an nH x nH system (~20 % of the block),
         // and the forms are evaluated.  Block elimination by a triangular
-        // part with unit-or-two diagonal: the same unique solution, singular
-        // exactly when the block is.
+        // part with unit-or-two diagonal: the block's solutions are exactly
+        // x = T y + t over the heavy system's solutions y (solvable exactly
+        // when the block is, with the same null space dimension); a singular
+        // one is then moved to the block's own canonical solution (free
+        // columns 0) through that null space, below.
         constexpr uint32_t FVS_MIN = 96, FW = 6;  // <= 6 words per form / heavy row
         static_assert(FVS_NH_MAX + 1 <= 64 * FW, "heavy columns + the constant column must fit FW words");
         constexpr size_t V0 = (size_t)16 * Lds::CMAX;          // affine forms, past that region
@@ -1343,9 +1408,10 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
                 const bool hok = hs_lds ? gauss_jordan(nH, HSL) : gauss_jordan(nH, X);
                 pc.lap(GP_FVS_GJ);
                 if (!hok) {
-                    pc.add(GP_N_FAIL_SINGULAR, 1);
+                    pc.add(GP_N_FAIL_INCONS, 1);
                     return false;
                 }
+                const uint32_t nfree = L.nfree;
                 // evaluate: x_i = forms . (x_heavy, 1)
                 uint64_t *X1 = L.prow, *X2 = L.prow + 8;
                 for (uint32_t w = tid; w < 16; w += GS_THREADS) L.prow[w] = 0;
@@ -1373,7 +1439,94 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
                     L.xval[L.hinge[k]] = (uint8_t)val;
                 }
                 __syncthreads();
-                solved = true;
+                if (nfree && nfree <= NB_MAX) {
+                    // x0 above solves the block; with a singular heavy system
+                    // the block's solutions are x0 + span{T z_f}, z_f the heavy
+                    // null vectors (z_f: x_f = 1 at free heavy column f, 0 at
+                    // the other free ones, -cf_c * a_cf at pivot column c).  The
+                    // canonical solution has 0 at the block's free columns =
+                    // the last nonzero positions (in member = increasing edge
+                    // order) of its null vectors: the T z_f are reduced to a
+                    // basis n_p with distinct last nonzero p, n_p[p] = 1 and 0
+                    // at the other basis positions, and x = x0 - sum x0[p] n_p.
+                    pc.add(GP_N_SING_SOLVED, 1);
+                    pc.add(GP_N_NULL_VECS, nfree);
+                    const int16_t *piv = L.a0;
+                    uint8_t *coef = L.b1;                                   // (GJ's marks are dead)
+                    int16_t *bpos = reinterpret_cast<int16_t *>(L.hbin);    // basis positions (NB_MAX)
+                    uint8_t *nbv = reinterpret_cast<uint8_t *>(scr + (size_t)30 * Lds::CMAX);  // past the reverse CSR
+                    auto NBV = [&](uint32_t l, uint32_t i) -> uint8_t & { return nbv[(size_t)l * Lds::CMAX + i]; };
+                    auto HSA = [&](uint32_t rr, uint32_t w, uint32_t q) -> uint64_t { return hs_lds ? HSL(rr, w, q) : X(rr, w, q); };
+                    uint64_t *Z1 = L.prow, *Z2 = L.prow + 8;
+                    uint32_t nb = 0;
+                    for (uint32_t f = 0; f < nH; ++f) {
+                        if (piv[f] >= 0) continue;  // (uniform)
+                        for (uint32_t w = tid; w < 16; w += GS_THREADS) L.prow[w] = 0;
+                        if (tid == 0) L.npos = 0;
+                        __syncthreads();
+                        for (uint32_t cc = tid; cc < nH; cc += GS_THREADS) {
+                            const int pr = piv[cc];
+                            uint32_t zc = 0;
+                            if (cc == f) {
+                                zc = 1;
+                            } else if (pr >= 0) {
+                                const uint64_t fbit = 1ULL << (f & 63), cbit = 1ULL << (cc & 63);
+                                const uint32_t av = (HSA(pr, f >> 6, 0) & fbit) ? 1 : (HSA(pr, f >> 6, 1) & fbit) ? 2 : 0;
+                                const uint32_t cf = (HSA(pr, cc >> 6, 1) & cbit) ? 2 : 1;
+                                zc = (3 - cf * av % 3) % 3;
+                            }
+                            if (zc) atomicOr((unsigned long long *)&(zc == 1 ? Z1 : Z2)[cc >> 6], 1ULL << (cc & 63));
+                        }
+                        __syncthreads();
+                        // u = T z: the forms without their constant column (z has
+                        // no bit there); a heavy member's form is its unit vector
+                        for (uint32_t i = tid; i < sz; i += GS_THREADS) {
+                            uint32_t sm = 0;
+                            for (uint32_t w = 0; w < HW; ++w) {
+                                const uint64_t p1 = V(i, w, 0), p2 = V(i, w, 1);
+                                sm += __builtin_popcountll(p1 & Z1[w]) + 2 * __builtin_popcountll(p1 & Z2[w]) +
+                                      2 * __builtin_popcountll(p2 & Z1[w]) + __builtin_popcountll(p2 & Z2[w]);
+                            }
+                            NBV(nb, i) = (uint8_t)(sm % 3);
+                        }
+                        __syncthreads();
+                        for (uint32_t l = tid; l < nb; l += GS_THREADS) coef[l] = NBV(nb, (uint32_t)bpos[l]);
+                        __syncthreads();
+                        for (uint32_t i = tid; i < sz; i += GS_THREADS) {
+                            uint32_t t = 0;
+                            for (uint32_t l = 0; l < nb; ++l) t += coef[l] * NBV(l, i);
+                            const uint32_t u = (NBV(nb, i) + 2 * t) % 3;  // u - t (mod 3)
+                            NBV(nb, i) = (uint8_t)u;
+                            if (u) atomicMax(&L.npos, i + 1);
+                        }
+                        __syncthreads();
+                        const uint32_t pnew = L.npos - 1;  // (T z is independent of the basis: npos > 0)
+                        const uint32_t sc = NBV(nb, pnew);  // 1 or 2 = its own inverse
+                        for (uint32_t l = tid; l < nb; l += GS_THREADS) coef[l] = NBV(l, pnew);
+                        __syncthreads();
+                        for (uint32_t i = tid; i < sz; i += GS_THREADS) {
+                            const uint32_t u = NBV(nb, i) * sc % 3;
+                            NBV(nb, i) = (uint8_t)u;
+                            for (uint32_t l = 0; l < nb; ++l) NBV(l, i) = (uint8_t)((NBV(l, i) + 2 * coef[l] * u) % 3);
+                        }
+                        if (tid == 0) bpos[nb] = (int16_t)pnew;
+                        __syncthreads();
+                        ++nb;
+                    }
+                    for (uint32_t l = tid; l < nb; l += GS_THREADS)
+                        coef[l] = L.xval[L.hinge[L.members[beg + (uint32_t)bpos[l]]]];
+                    __syncthreads();
+                    for (uint32_t i = tid; i < sz; i += GS_THREADS) {
+                        uint32_t t = 0;
+                        for (uint32_t l = 0; l < nb; ++l) t += coef[l] * NBV(l, i);
+                        uint8_t &xv = L.xval[L.hinge[L.members[beg + i]]];
+                        xv = (uint8_t)((xv + 2 * t) % 3);
+                    }
+                    __syncthreads();
+                }
+                // (more null vectors than NB_MAX, never seen: the whole-block
+                // Gauss-Jordan below)
+                solved = nfree <= NB_MAX;
             }
         }
         if (!solved) {
@@ -1399,7 +1552,7 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
                 if (rhs == 2) X(rr, sz >> 6, 1) |= 1ULL << (sz & 63);
             }
             if (!gauss_jordan(sz, X)) {
-                pc.add(GP_N_FAIL_SINGULAR, 1);
+                pc.add(GP_N_FAIL_INCONS, 1);
                 return false;
             }
             for (uint32_t cc = tid; cc < sz; cc += GS_THREADS) L.xval[L.hinge[L.members[beg + cc]]] = colval[cc];
@@ -1477,7 +1630,7 @@ __device__ __forceinline__ void solve_bucket(Lds &L, const SolveArgs &a, uint64_
         else if (word) atomicOr((unsigned long long *)(a.values + w), (unsigned long long)word);
     }
     if (threadIdx.x == 0) a.E[b] |= (uint64_t)j << 56;
-    if (a.width || a.rank_out) {
+    if (a.width || a.rank_out || a.index_out) {
         uint32_t *pre = L.deg;  // (dead after the solve) hinge vertices before v
         for (uint32_t v = threadIdx.x; v < nv; v += GS_THREADS) pre[v] = L.vowner[v] >= 0 ? 1u : 0u;
         __syncthreads();
@@ -1486,6 +1639,10 @@ __device__ __forceinline__ void solve_bucket(Lds &L, const SolveArgs &a, uint64_
         for (uint32_t k = threadIdx.x; k < cnt; k += GS_THREADS) {
             const uint64_t r = lo + pre[L.hinge[k]];
             if (a.rank_out) a.rank_out[a.pay[lo - a.e0 + k]] = (int64_t)r;
+            if (a.index_out) {
+                const uint64_t p = a.pay[lo - a.e0 + k];
+                a.index_out[r - a.idx_lo] = __builtin_bswap64(a.addr ? a.addr[p] : a.addr_base + a.addr_stride * p);
+            }
             if (a.width) {
                 const uint64_t val = sig[k].x & mask, bit = r * a.width, word = bit >> 6;
                 const uint32_t off = (uint32_t)(bit & 63);
@@ -1534,6 +1691,74 @@ __global__ __launch_bounds__(GS_THREADS) void k_gov_solve_big(SolveArgs a, const
 // bytes of one k_gov_solve_big workgroup slab (state + dense scratch)
 constexpr size_t big_slab_bytes() {
     return ((sizeof(SolveBig) + 255) & ~(size_t)255) + solve_scratch_words<SolveBig>() * 8;
+}
+
+// ---- keys straight into one bucket range (sequential range builds) ----------
+// The build of a bucket range from the keys themselves (resident in HBM): the
+// range's buckets are counted, then its keys re-hashed and scattered to their
+// bucket's cursor with their input position -- no signature array for the
+// whole key set.  KIND 0: 13-byte keys (dword-aligned 16-byte windows), 1:
+// fixed key_len, 2: variable length (offsets).
+struct SelArgs {
+    const uint8_t *keys;
+    const uint64_t *off;     // KIND 2
+    uint64_t blob_bytes, n;
+    uint32_t key_len;        // KIND 0/1
+    uint32_t mult;           // 2m
+    uint32_t b_lo, nb;       // the range [b_lo, b_lo + nb)
+    uint32_t *counts;        // MODE 0: per bucket of the range
+    unsigned long long *cursor;  // MODE 1: next slot of each bucket (range-local positions)
+    uint64_t *sorted;        // MODE 1: (sig0, sig1) pairs
+    uint64_t *pay;           // MODE 1: input positions
+};
+
+__device__ __forceinline__ uint64_t sel_gload64(const uint8_t *base, uint64_t limit, uint64_t pos) {
+    const uint64_t a = pos & ~3ULL;
+    const uint32_t sh = (uint32_t)(pos & 3) * 8;
+    auto ld = [&](uint64_t x) -> uint32_t {
+        if (x + 4 <= limit) return *reinterpret_cast<const uint32_t *>(base + x);
+        uint32_t w = 0;
+        for (int b = 0; b < 4; ++b)
+            if (x + b < limit) w |= (uint32_t)base[x + b] << (8 * b);
+        return w;
+    };
+    return funnel64(ld(a), ld(a + 4), ld(a + 8), sh);
+}
+
+template <int MODE, int KIND>
+__global__ __launch_bounds__(256) void k_sel(SelArgs a) {
+    typedef unsigned int u32x4w __attribute__((ext_vector_type(4), aligned(4)));
+    const uint64_t stride = (uint64_t)gridDim.x * 256;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < a.n; i += stride) {
+        uint64_t s0, s1;
+        if (KIND == 0) {
+            const uint64_t byte = i * 13, al = byte & ~3ULL;
+            if (al + 16 <= a.blob_bytes) {
+                const u32x4w w = __builtin_nontemporal_load(reinterpret_cast<const u32x4w *>(a.keys + al));
+                W64 x0, x1;
+                spooky13_u(w.x, w.y, w.z, w.w, (uint32_t)(byte & 3) * 8, 0, x0, x1);
+                s0 = u64(x0);
+                s1 = u64(x1);
+            } else {
+                auto rd = [&](uint32_t o) -> uint64_t { return sel_gload64(a.keys, a.blob_bytes, byte + o); };
+                spooky_short(rd, 13, 0, s0, s1);
+            }
+        } else {
+            const uint64_t pos = KIND == 2 ? a.off[i] : i * a.key_len;
+            const uint32_t len = KIND == 2 ? (uint32_t)(a.off[i + 1] - pos) : a.key_len;
+            auto rd = [&](uint32_t o) -> uint64_t { return sel_gload64(a.keys, a.blob_bytes, pos + o); };
+            spooky_short(rd, len, 0, s0, s1);
+        }
+        const uint32_t rb = bucket_of_w(w64(s0), a.mult) - a.b_lo;  // (wraps below the range)
+        if (rb >= a.nb) continue;
+        if (MODE == 0) {
+            atomicAdd(a.counts + rb, 1u);
+        } else {
+            const uint64_t p = atomicAdd(a.cursor + rb, 1ULL);
+            reinterpret_cast<ulonglong2 *>(a.sorted)[p] = make_ulonglong2(s0, s1);
+            a.pay[p] = i;
+        }
+    }
 }
 
 // ---- checks and E4 ownership -------------------------------------------------

@@ -45,6 +45,10 @@ SIGNATURES = [
     ("bsdb_dev_gov_build", _i, [_vp, _vp, _u64, _u32, _vp, _vp, _vp, _vp]),
     ("bsdb_dev_gov_build_ranks", _i, [_vp, _vp, _u64, _u32, _vp, _vp, _vp, _vp, _vp]),
     ("bsdb_dev_gov_build_range", _i, [_vp, _vp, _u64, _u64, _u64, _u64, _u64, _u32, _vp, _vp, _vp, _vp, _vp]),
+    ("bsdb_dev_mph_build_index_passes_fixed", _i, [_vp, _vp, _u32, _u64, _u32, _u32, _vp, _u64, _u64, _vp, _vp,
+                                                   _vp, _vp, _vp, C.POINTER(_u32), _vp]),
+    ("bsdb_dev_mph_build_index_passes_var", _i, [_vp, _vp, _u64, _vp, _u64, _u32, _u32, _vp, _u64, _u64, _vp, _vp,
+                                                 _vp, _vp, _vp, C.POINTER(_u32), _vp]),
     ("bsdb_dev_partition_owners", _i, [_vp, _vp, _vp, _u64, _u64, _i, _vp, _vp, _vp, _vp]),
     ("bsdb_set_verify", _i, [_vp, _i]),
     ("bsdb_set_histogram_mode", _i, [_vp, _i]),
@@ -282,6 +286,42 @@ class Context:
         _check("bsdb_dev_gov_build_range", lib().bsdb_dev_gov_build_range(
             self._h, _ptr(sig), sig.shape[0], n_global, b_lo, b_hi, e_lo, width, _ptr(E), _ptr(values),
             _ptr(sigbits) if sigbits is not None else None, _ptr(rank) if rank is not None else None, _stream(stream)))
+
+    def mph_build_index_passes(self, keys, key_len: int, n: int, width: int, passes: int = 0, offsets=None,
+                               addr=None, addr_base: int = 0, addr_stride: int = 0, index=None, stream=None):
+        """The whole build from keys resident on the device by sequential
+        bucket-range passes (fixed key_len, or a var-len blob with offsets).
+        index: None (structure only), a device int64 tensor of n slots, or a
+        host numpy uint64/int64 array of n slots (each pass's slice copied out
+        while the next solves).  addr: device int64 tensor of n addresses, else
+        addr_base + addr_stride * i.  Returns (E, values, sigbits, passes_used)."""
+        import torch
+        import numpy as np
+        dev = keys.device
+        m = n // 1500 + 1
+        E = torch.empty(m + 1, dtype=torch.int64, device=dev)
+        values = torch.empty(int(lib().bsdb_values_words(n)), dtype=torch.int64, device=dev)
+        sigbits = torch.empty((n * width + 63) // 64 + 1, dtype=torch.int64, device=dev) if width else None
+        d_index = h_index = None
+        if index is not None:
+            if isinstance(index, np.ndarray):
+                assert index.dtype.itemsize == 8 and index.size >= n and index.flags.c_contiguous
+                h_index = index.ctypes.data
+            else:
+                assert index.dtype == torch.int64 and index.numel() >= n and index.device == dev
+                d_index = _ptr(index)
+        used = C.c_uint32()
+        sb = _ptr(sigbits) if sigbits is not None else None
+        ad = _ptr(addr) if addr is not None else None
+        if offsets is None:
+            _check("bsdb_dev_mph_build_index_passes_fixed", lib().bsdb_dev_mph_build_index_passes_fixed(
+                self._h, _ptr(keys), key_len, n, width, passes, ad, addr_base, addr_stride, _ptr(E), _ptr(values), sb,
+                d_index, h_index, C.byref(used), _stream(stream)))
+        else:
+            _check("bsdb_dev_mph_build_index_passes_var", lib().bsdb_dev_mph_build_index_passes_var(
+                self._h, _ptr(keys), keys.numel(), _ptr(offsets), n, width, passes, ad, addr_base, addr_stride,
+                _ptr(E), _ptr(values), sb, d_index, h_index, C.byref(used), _stream(stream)))
+        return E, values, sigbits, used.value
 
     def partition_owners(self, sig, m: int, nranks: int, payload=None, stream=None):
         """Signatures (and one int64 payload per key) grouped by owning rank

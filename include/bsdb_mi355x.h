@@ -46,7 +46,7 @@
 extern "C" {
 #endif
 
-#define BSDB_ABI_VERSION 2
+#define BSDB_ABI_VERSION 3
 
 /* Return codes (negative errno-style). */
 #define BSDB_OK          0
@@ -147,7 +147,7 @@ int bsdb_dev_gov_build(bsdb_ctx *ctx, const uint64_t *d_sig, uint64_t n, uint32_
 /* F2: the same build, also returning d_rank[i] = the rank (getLong) of d_sig[i],
  * computed inside the solve (E[b] + the hinge vertices before the key's hinge:
  * the lookup's nonzero-pair count, GOV:557-580) -- no lookup pass over the
- * keys is needed to place records in index.db (W:129-145).  n < 2^32.  The
+ * keys is needed to place records in index.db (W:129-145).  The
  * checksum bits are always signed this way (A11 fused into the solve). */
 int bsdb_dev_gov_build_ranks(bsdb_ctx *ctx, const uint64_t *d_sig, uint64_t n, uint32_t width, uint64_t *d_E,
                              uint64_t *d_values, uint64_t *d_sigbits, int64_t *d_rank, void *stream);
@@ -165,6 +165,29 @@ int bsdb_dev_gov_build_ranks(bsdb_ctx *ctx, const uint64_t *d_sig, uint64_t n, u
 int bsdb_dev_gov_build_range(bsdb_ctx *ctx, const uint64_t *d_sig, uint64_t n_local, uint64_t n_global,
                              uint64_t b_lo, uint64_t b_hi, uint64_t e_lo, uint32_t width, uint64_t *d_E,
                              uint64_t *d_values, uint64_t *d_sigbits, int64_t *d_rank, void *stream);
+/* The whole build of a key set resident in this device's HBM (C4: 13.19e9 x
+ * 13 B; C5: 4e9 var-len) by sequential bucket-range passes: pass p of P covers
+ * buckets [p*m/P, (p+1)*m/P) (the reference's 256 spill segments are such
+ * ranges, CBHS:379-395, solved one at a time, CBHS:852-978 / GOV:385-448).
+ * Every pass re-hashes all keys and keeps its range's: no signature array for
+ * the whole set.  Writes d_E / d_values / d_sigbits (sizes as
+ * bsdb_dev_gov_build; zeroed here) and, optionally, index.db's slots
+ * (W:129-145): slot rank(key i) = byte-reversed addr(i), addr(i) = d_addr[i]
+ * when d_addr != NULL, else addr_base + addr_stride * i (fixed-size records of
+ * one data file).  The slots go to d_index[n] (device) or h_index[n] (host
+ * memory: each pass's contiguous slice is copied out while the next pass
+ * solves) or nowhere when both are NULL.  passes = 0 picks the fewest passes
+ * that fit the free HBM; *passes_used (optional) returns the count.  Results
+ * equal bsdb_dev_gov_build's on the same keys.  Synchronous. */
+int bsdb_dev_mph_build_index_passes_fixed(bsdb_ctx *ctx, const uint8_t *d_keys, uint32_t key_len, uint64_t n,
+                                          uint32_t width, uint32_t passes, const uint64_t *d_addr, uint64_t addr_base,
+                                          uint64_t addr_stride, uint64_t *d_E, uint64_t *d_values, uint64_t *d_sigbits,
+                                          uint64_t *d_index, uint64_t *h_index, uint32_t *passes_used, void *stream);
+int bsdb_dev_mph_build_index_passes_var(bsdb_ctx *ctx, const uint8_t *d_blob, uint64_t blob_bytes,
+                                        const uint64_t *d_off, uint64_t n, uint32_t width, uint32_t passes,
+                                        const uint64_t *d_addr, uint64_t addr_base, uint64_t addr_stride,
+                                        uint64_t *d_E, uint64_t *d_values, uint64_t *d_sigbits, uint64_t *d_index,
+                                        uint64_t *h_index, uint32_t *passes_used, void *stream);
 /* E4 ownership: rank g of `nranks` owns buckets [g*m/nranks, (g+1)*m/nranks)
  * (m = num_buckets; the bucket is monotone in sig0, CBHS:129-138).  Groups the n
  * signatures of d_sig by owning rank into d_out (rank 0's first; order within a

@@ -431,10 +431,35 @@ uint64_t bo_values_words(uint64_t n) { return (2 * (1 + ((n * 281) >> 8)) + 63) 
  *      vertex e0,e1,e2) plus BFS augmenting paths in edge order;           *
  *   3. the core system (unknowns = core hinges, non-hinge vertices = 0) is *
  *      solved over F3 block by block on the SCCs of its dependency graph   *
- *      (Gauss-Jordan per block; a singular block or an unorientable core   *
- *      moves to the next local seed);                                      *
+ *      (Gauss-Jordan per block, columns in increasing edge order);         *
  *   4. peeled edges are solved in reverse round order.                     *
+ *                                                                          *
+ * Seed rule (GOV:425-432): the next local seed only when the bucket's      *
+ * system has NO solution -- an unorientable core (sux4j's "unorientable",  *
+ * GOV:427) or an inconsistent block ("unsolvable", GOV:428).  A singular   *
+ * but consistent block is solved: its solution is the one whose free       *
+ * columns (the columns of its reduced row echelon form without a pivot,    *
+ * in increasing edge order) are 0.  That choice is a function of the block *
+ * alone, whatever elimination reaches it, which keeps the device's         *
+ * feedback-vertex-set solver bit-identical to this one.                    *
  * ======================================================================== */
+
+/* attempts and their outcomes (bo_solve_stats), summed over threads */
+static uint64_t g_stats[5];  /* attempts, unorientable, inconsistent, degenerate edge, singular solved */
+
+void bo_solve_stats(uint64_t out[5], int reset) {
+    for (int i = 0; i < 5; i++) {
+        out[i] = __atomic_load_n(&g_stats[i], __ATOMIC_RELAXED);
+        if (reset) __atomic_store_n(&g_stats[i], 0, __ATOMIC_RELAXED);
+    }
+}
+
+static inline void stat_add(int i) { __atomic_fetch_add(&g_stats[i], 1, __ATOMIC_RELAXED); }
+
+static int cmp_i32(const void *a, const void *b) {
+    const int32_t x = *(const int32_t *)a, y = *(const int32_t *)b;
+    return x < y ? -1 : x > y;
+}
 
 static int cmp_sig(const void *a, const void *b) {
     const uint64_t *x = (const uint64_t *)a, *y = (const uint64_t *)b;
@@ -451,11 +476,12 @@ static inline void gf3_add(uint64_t *x1, uint64_t *x2, const uint64_t y1, const 
 }
 
 /* Solves one bucket.  sig: cnt sorted signatures; writes vals[nv] (0..3).
- * Returns 0 solved, 1 unorientable/singular (try next seed). */
+ * Returns 0 solved, 1 no solution under this seed (try the next one). */
 static int solve_bucket(const uint64_t *sig, uint32_t cnt, uint32_t nv, uint64_t seed_bits, uint8_t *vals,
                         int32_t *ws) {
     memset(vals, 0, nv);
     if (cnt == 0) return 0;
+    stat_add(0);
     /* one key on one vertex: its edge is (0,0,0); h = 0 holds for any value and
      * the hinge stores 3 (GOV:126-139).  Other triple edges take the next seed. */
     if (cnt == 1 && nv == 1) { vals[0] = 3; return 0; }
@@ -479,7 +505,7 @@ static int solve_bucket(const uint64_t *sig, uint32_t cnt, uint32_t nv, uint64_t
         bo_signature_to_equation(sig + 2 * k, seed_bits, nv, ee);
         /* a repeated vertex is kept (coefficient 2); a triple one makes the
          * equation 0 = h unsatisfiable for its orientation: next seed */
-        if (ee[0] == ee[1] && ee[1] == ee[2] && !tiny) return 1;
+        if (ee[0] == ee[1] && ee[1] == ee[2] && !tiny) { stat_add(3); return 1; }
         e[3 * k] = ee[0]; e[3 * k + 1] = ee[1]; e[3 * k + 2] = ee[2];
     }
     memset(deg, 0, nv * sizeof *deg);
@@ -544,7 +570,7 @@ static int solve_bucket(const uint64_t *sig, uint32_t cnt, uint32_t nv, uint64_t
                 queue[qt++] = o;
             }
         }
-        if (found_v < 0) return 1; /* unorientable */
+        if (found_v < 0) { stat_add(1); return 1; } /* unorientable */
         /* flip along the path: found_e takes found_v, its old hinge goes to prev ... */
         int32_t k = found_e, v = found_v;
         for (;;) {
@@ -587,8 +613,8 @@ static int solve_bucket(const uint64_t *sig, uint32_t cnt, uint32_t nv, uint64_t
      * solved block by block over the strongly connected components of "edge k
      * uses the hinge of edge k'" (Tarjan, iterative, edges in increasing order;
      * components come out sinks first, so every block sees its dependencies
-     * solved).  A singular block fails the seed.  (When every block is
-     * nonsingular the core matrix is, and the solution is its unique one.) */
+     * solved).  An inconsistent block fails the seed; a consistent singular
+     * one takes its free columns = 0 (the header's seed rule). */
     if (ncore) {
         int32_t *tidx = (int32_t *)malloc(cnt * sizeof(int32_t));
         int32_t *tlow = (int32_t *)malloc(cnt * sizeof(int32_t));
@@ -598,6 +624,7 @@ static int solve_bucket(const uint64_t *sig, uint32_t cnt, uint32_t nv, uint64_t
         uint8_t *onst = (uint8_t *)calloc(cnt, 1);
         int32_t *members = (int32_t *)malloc(cnt * sizeof(int32_t));
         int32_t *col_of = (int32_t *)malloc(cnt * sizeof(int32_t));
+        int32_t *pivrow = (int32_t *)malloc(cnt * sizeof(int32_t));
         int fail = 0, counter = 0, sp = 0;
         for (uint32_t k = 0; k < cnt; k++) { tidx[k] = -1; col_of[k] = -1; }
         /* successor i (0..2) of core edge k: owner of e_k[i] when that vertex is
@@ -633,6 +660,8 @@ static int solve_bucket(const uint64_t *sig, uint32_t cnt, uint32_t nv, uint64_t
                     members[sz++] = w;
                     if (w == k) break;
                 }
+                /* columns (and rows) in increasing edge order */
+                qsort(members, sz, sizeof(int32_t), cmp_i32);
                 for (int i = 0; i < sz; i++) col_of[members[i]] = i;
                 /* dense block: rows/cols = members (col i = hinge of members[i]) */
                 const int W = (sz + 1 + 63) / 64;
@@ -656,44 +685,58 @@ static int solve_bucket(const uint64_t *sig, uint32_t cnt, uint32_t nv, uint64_t
                     if (rhs == 1) m1[(size_t)r * W + (sz >> 6)] |= 1ULL << (sz & 63);
                     if (rhs == 2) m2[(size_t)r * W + (sz >> 6)] |= 1ULL << (sz & 63);
                 }
-                for (int c = 0; c < sz && !fail; c++) {
+                /* reduced row echelon form: column c takes the first row at or
+                 * below `pr` with a nonzero there (swapped up, scaled to 1,
+                 * eliminated from every other row); a column with none is free */
+                int pr = 0;
+                for (int c = 0; c < sz; c++) {
                     const int wc = c >> 6;
                     const uint64_t bit = 1ULL << (c & 63);
-                    int p = c;
+                    int p = pr;
                     while (p < sz && !((m1[(size_t)p * W + wc] | m2[(size_t)p * W + wc]) & bit)) p++;
-                    if (p == sz) { fail = 1; break; }
-                    if (p != c)
+                    if (p == sz) { pivrow[c] = -1; continue; }
+                    if (p != pr)
                         for (int w2 = 0; w2 < W; w2++) {
-                            uint64_t t = m1[(size_t)p * W + w2]; m1[(size_t)p * W + w2] = m1[(size_t)c * W + w2]; m1[(size_t)c * W + w2] = t;
-                            t = m2[(size_t)p * W + w2]; m2[(size_t)p * W + w2] = m2[(size_t)c * W + w2]; m2[(size_t)c * W + w2] = t;
+                            uint64_t t = m1[(size_t)p * W + w2]; m1[(size_t)p * W + w2] = m1[(size_t)pr * W + w2]; m1[(size_t)pr * W + w2] = t;
+                            t = m2[(size_t)p * W + w2]; m2[(size_t)p * W + w2] = m2[(size_t)pr * W + w2]; m2[(size_t)pr * W + w2] = t;
                         }
-                    if (m2[(size_t)c * W + wc] & bit)
+                    if (m2[(size_t)pr * W + wc] & bit)
                         for (int w2 = 0; w2 < W; w2++) {
-                            const uint64_t t = m1[(size_t)c * W + w2]; m1[(size_t)c * W + w2] = m2[(size_t)c * W + w2]; m2[(size_t)c * W + w2] = t;
+                            const uint64_t t = m1[(size_t)pr * W + w2]; m1[(size_t)pr * W + w2] = m2[(size_t)pr * W + w2]; m2[(size_t)pr * W + w2] = t;
                         }
                     for (int r = 0; r < sz; r++) {
-                        if (r == c) continue;
+                        if (r == pr) continue;
                         const uint64_t f1 = m1[(size_t)r * W + wc] & bit, f2 = m2[(size_t)r * W + wc] & bit;
                         if (!f1 && !f2) continue;
                         for (int w2 = 0; w2 < W; w2++) {
-                            const uint64_t y1 = f1 ? m2[(size_t)c * W + w2] : m1[(size_t)c * W + w2];
-                            const uint64_t y2 = f1 ? m1[(size_t)c * W + w2] : m2[(size_t)c * W + w2];
+                            const uint64_t y1 = f1 ? m2[(size_t)pr * W + w2] : m1[(size_t)pr * W + w2];
+                            const uint64_t y2 = f1 ? m1[(size_t)pr * W + w2] : m2[(size_t)pr * W + w2];
                             gf3_add(&m1[(size_t)r * W + w2], &m2[(size_t)r * W + w2], y1, y2);
                         }
                     }
+                    pivrow[c] = pr++;
                 }
-                if (!fail)
-                    for (int c = 0; c < sz; c++) {
-                        const uint64_t bit = 1ULL << (sz & 63);
-                        const int wn = sz >> 6;
-                        xval[hinge[members[c]]] = (m1[(size_t)c * W + wn] & bit) ? 1 : (m2[(size_t)c * W + wn] & bit) ? 2 : 0;
-                    }
+                /* rows without a pivot are 0 = rhs: the block is solvable iff
+                 * every such rhs is 0 (GOV:428 "unsolvable" otherwise) */
+                {
+                    const uint64_t bit = 1ULL << (sz & 63);
+                    const int wn = sz >> 6;
+                    for (int r = pr; r < sz; r++)
+                        if ((m1[(size_t)r * W + wn] | m2[(size_t)r * W + wn]) & bit) fail = 1;
+                    if (fail) stat_add(2);
+                    else if (pr < sz) stat_add(4);
+                    if (!fail)
+                        for (int c = 0; c < sz; c++) {
+                            const int q = pivrow[c];  /* free column: 0 */
+                            xval[hinge[members[c]]] = q < 0 ? 0 : (m1[(size_t)q * W + wn] & bit) ? 1 : (m2[(size_t)q * W + wn] & bit) ? 2 : 0;
+                        }
+                }
                 for (int i = 0; i < sz; i++) col_of[members[i]] = -1;
                 free(m1); free(m2);
             }
         }
 #undef BO_SUCC
-        free(tidx); free(tlow); free(tstk); free(cstk); free(cpos); free(onst); free(members); free(col_of);
+        free(tidx); free(tlow); free(tstk); free(cstk); free(cpos); free(onst); free(members); free(col_of); free(pivrow);
         if (fail) return 1;
     }
     /* 4. peeled edges, last round first */

@@ -94,6 +94,11 @@ void bo_bitlist_set(uint64_t *words, uint64_t i, uint32_t width, uint64_t v);
  * The per-bucket solver follows the GOV construction (peel, then F3
  * elimination of the 2-core); its choice among valid solutions is NOT pinned
  * against sux4j 5.4.1 (absent here): see DESIGN.md "parity unpinned". */
+/* Solver counters since the last reset (threads summed): attempts (seeds
+ * tried), unorientable cores, inconsistent blocks, degenerate edges, singular
+ * but consistent blocks solved.  reset != 0 zeroes them after reading. */
+void bo_solve_stats(uint64_t out[5], int reset);
+
 int bo_gov_build(const uint64_t *sig /* 2n, any order */, uint64_t n, uint32_t sig_width,
                  uint64_t *E, uint64_t *values, uint64_t values_words,
                  uint64_t *signatures, uint64_t sig_words);

@@ -79,6 +79,7 @@ def lib() -> C.CDLL:
         L.bo_lookup_batch_mt.argtypes = [C.POINTER(BoMph), _u64p, C.c_uint64, C.c_int, C.POINTER(C.c_int64), C.c_int]
         L.bo_hash_fixed_mt.argtypes = [_u8p, C.c_uint32, C.c_uint64, C.c_uint64, _u64p, C.c_int]
         L.bo_varkey_len.argtypes = [C.c_uint64]; L.bo_varkey_len.restype = C.c_uint32
+        L.bo_solve_stats.argtypes = [_u64p, C.c_int]
         L.bo_gen_keys_var.argtypes = [C.c_uint64, C.c_uint64, _u64p, _u8p]
         L.bo_histogram_genvar_mt.argtypes = [C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64, _u32p, C.c_int]
         L.bo_histogram_genvar_mt.restype = C.c_double
@@ -233,6 +234,14 @@ def gov_build(sig: np.ndarray, width: int):
     sigbits = np.zeros(sw, np.uint64)
     rc = lib().bo_gov_build(_p(sig, _u64p), n, width, _p(E, _u64p), _p(values, _u64p), vw, _p(sigbits, _u64p), sw)
     return rc, E, values, sigbits
+
+
+def solve_stats(reset: bool = True) -> dict:
+    """The oracle solver's counters (bo_solve_stats), optionally reset."""
+    out = np.zeros(5, np.uint64)
+    lib().bo_solve_stats(_p(out, _u64p), 1 if reset else 0)
+    return dict(zip(("attempts", "unorientable", "inconsistent", "degenerate", "singular_solved"),
+                    (int(x) for x in out)))
 
 
 def lookup_batch(sig: np.ndarray, n: int, E: np.ndarray, values: np.ndarray, width: int = 0, sigbits=None,

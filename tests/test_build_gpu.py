@@ -395,3 +395,69 @@ def test_mph_outlives_its_context():
         m.export()
     assert e.value.code == -22
     m.close()  # frees the handle only
+
+
+def _bswap(a):
+    return a.astype(np.uint64).byteswap()
+
+
+@pytest.mark.parametrize("n,width,passes", [(1, 4, 0), (3001, 0, 2), (700_001, 4, 3), (1_000_000, 7, 1),
+                                            (1_000_000, 4, 7)])
+def test_passes_build_fixed_equals_oracle(ctx, n, width, passes):
+    """Sequential bucket-range passes from resident keys (the C4 form): the
+    structure equals the oracle's build, and the solve's index slots equal
+    W:129-145 (slot rank = byte-reversed address) -- to device slots and to a
+    host array copied out pass by pass."""
+    keys = O.gen_keys13(41, n)
+    sig, E, vals, sb = oracle_build(keys, 13, width)
+    dk = dev(keys)
+    base, stride = 0x1000, 48
+    ranks = O.lookup_batch_mt(sig, n, E, vals, width, sb if width else None, False, THREADS)
+    exp = np.zeros(n, np.uint64)
+    exp[ranks] = _bswap(base + stride * np.arange(n, dtype=np.uint64))
+    d_index = torch.zeros(n, dtype=torch.int64, device="cuda")
+    dE, dv, ds, used = ctx.mph_build_index_passes(dk, 13, n, width, passes, addr_base=base, addr_stride=stride,
+                                                 index=d_index)
+    assert used == (passes if passes else used) and used >= 1
+    np.testing.assert_array_equal(u64(dE), E)
+    np.testing.assert_array_equal(u64(dv), vals)
+    if width:
+        np.testing.assert_array_equal(u64(ds)[: sb.size], sb)
+    np.testing.assert_array_equal(u64(d_index), exp)
+    h_index = np.zeros(n, np.uint64)
+    dE2, dv2, _, _ = ctx.mph_build_index_passes(dk, 13, n, width, passes, addr_base=base, addr_stride=stride,
+                                              index=h_index)
+    np.testing.assert_array_equal(u64(dE2), E)
+    np.testing.assert_array_equal(h_index, exp)
+
+
+def test_passes_build_var_keys_and_address_array(ctx):
+    """Variable-length keys (C5 recipe, cb = 16) and addresses from an array."""
+    n, width = 400_000, 16
+    blob, off = O.gen_keys_var(9, n)
+    sig = O.hash_var(blob, off)
+    rc, E, vals, sb, _ = O.gov_build_mt(sig, width, THREADS)
+    assert rc == 0
+    addr = np.random.default_rng(4).integers(1, 2**62, n).astype(np.uint64)
+    ranks = O.lookup_batch(sig, n, E, vals, width, sb, False)
+    exp = np.zeros(n, np.uint64)
+    exp[ranks] = _bswap(addr)
+    d_index = torch.zeros(n, dtype=torch.int64, device="cuda")
+    dE, dv, ds, used = ctx.mph_build_index_passes(dev(blob), 0, n, width, 4, offsets=dev(off.view(np.int64)),
+                                                 addr=dev(addr.view(np.int64)), index=d_index)
+    assert used == 4
+    np.testing.assert_array_equal(u64(dE), E)
+    np.testing.assert_array_equal(u64(dv), vals)
+    np.testing.assert_array_equal(u64(ds)[: sb.size], sb)
+    np.testing.assert_array_equal(u64(d_index), exp)
+
+
+def test_passes_build_duplicates_and_empty(ctx):
+    keys = O.gen_keys13(5, 20_000).reshape(-1, 13)
+    keys[17_000] = keys[3]
+    from bsdb_amd.native import BsdbError
+    with pytest.raises(BsdbError) as e:
+        ctx.mph_build_index_passes(dev(keys.reshape(-1)), 13, 20_000, 4, 2)
+    assert e.value.code == -17  # EDUP (CBHS:969-972)
+    E, v, s, used = ctx.mph_build_index_passes(dev(np.zeros(16, np.uint8)), 13, 0, 4, 0)
+    assert u64(E).tolist() == [0, 0] and used == 1

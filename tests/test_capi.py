@@ -47,7 +47,7 @@ def test_host_only_calls(lib):
     lib.bsdb_num_buckets.argtypes = [C.c_uint64]
     assert lib.bsdb_num_buckets(13_193_787_549) == 8_795_859
     assert lib.bsdb_num_buckets(0) == 1
-    assert lib.bsdb_abi_version() == 2
+    assert lib.bsdb_abi_version() == 3
     lib.bsdb_strerror.restype = C.c_char_p
     assert lib.bsdb_strerror(-17) == b"duplicate key signature"
     lib.bsdb_open.argtypes = [C.c_int, C.POINTER(C.c_void_p)]

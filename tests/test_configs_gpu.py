@@ -76,6 +76,42 @@ def test_c4_full_size_histogram_equals_oracle(ctx):
 
 
 @pytest.mark.timeout(900)
+def test_c4_exact_full_build_one_gpu(ctx):
+    """C4's exact index on ONE GPU: all 13 193 787 549 keys resident (171.5 GB),
+    the GOV structure and index.db by sequential bucket-range passes (the
+    reference's segment-by-segment solve, CBHS:852-978 / GOV:385-448), the
+    index slots (rank -> byte-reversed record address, W:129-145) copied to
+    host memory pass by pass.  Checked: E[m] = n; the device's bijection check
+    of every range's ranks (bsdb_set_verify); checked lookups of 200 000 keys
+    in 20 blocks == the oracle's lookup on the exported structure, and their
+    index slots; no slot left empty."""
+    n, m, width, base, stride = README_N, README_N // 1500 + 1, 4, 0x1000, 48
+    keys = ctx.gen_keys13(0, n)                          # 171.5 GB in HBM
+    index = np.empty(n, np.uint64)                       # 105.6 GB of host memory: index.db
+    ctx.set_verify(True)
+    try:
+        E, vals, sb, used = ctx.mph_build_index_passes(keys, 13, n, width, 0, addr_base=base, addr_stride=stride,
+                                                       index=index)
+    finally:
+        ctx.set_verify(False)
+    del keys
+    hE, hv, hs = u64(E), u64(vals), u64(sb)
+    del E, vals, sb
+    torch.cuda.empty_cache()
+    assert used >= 2 and int(hE[-1]) & ((1 << 56) - 1) == n
+    rng = np.random.default_rng(44)
+    for first in np.sort(rng.integers(0, n - 10_000, 20)):
+        first = int(first)
+        sig = O.hash_fixed(O.gen_keys13(first, 10_000), 13)
+        r = O.lookup_batch_mt(sig, n, hE, hv, width, hs, True, THREADS)
+        assert r.min() >= 0
+        exp = (np.uint64(base) + np.uint64(stride) * np.arange(first, first + 10_000, dtype=np.uint64)).byteswap()
+        np.testing.assert_array_equal(index[r], exp)
+    for lo in range(0, n, 1 << 30):
+        assert np.count_nonzero(index[lo: lo + (1 << 30)] == 0) == 0
+
+
+@pytest.mark.timeout(900)
 def test_c5_full_size_histogram_equals_oracle(ctx):
     n, m = 4_000_000_000, 4_000_000_000 // 1500 + 1
     th, box = in_background(O.histogram_genvar_mt, 0, n, m, THREADS)

@@ -64,3 +64,29 @@ def test_small_sets_all_sizes():
         assert rc == 0, n
         r = O.lookup_batch(sig, n, E, values, 4, sigbits)
         assert np.array_equal(np.sort(r), np.arange(n)), n
+
+
+def test_seed_rule_retries_only_unsolvable_systems():
+    """GOV:425-432: the local seed moves on only when the bucket's system has
+    no solution (unorientable core, or an inconsistent block: sux4j's
+    unorientable / unsolvable counters, GOV:427-428).  A singular but
+    consistent block is solved (free columns 0), so such blocks occur among
+    the solved attempts, and fewer seeds are tried per bucket than under a
+    "fail on singular" rule (2.4 per bucket)."""
+    n = 600_000
+    keys = O.gen_keys13(77, n)
+    sig = O.hash_fixed(keys, 13)
+    O.solve_stats(reset=True)
+    rc, E, values, sigbits = O.gov_build(sig, 4)
+    st = O.solve_stats(reset=True)
+    assert rc == 0
+    m = O.num_buckets(n)
+    assert st["singular_solved"] > 0 and st["inconsistent"] > 0
+    fails = st["unorientable"] + st["inconsistent"] + st["degenerate"]
+    assert st["attempts"] == m + fails  # every bucket ends on its first solvable seed
+    assert st["attempts"] / m < 2.1
+    r = O.lookup_batch(sig, n, E, values, 4, sigbits)
+    assert np.array_equal(np.sort(r), np.arange(n))
+    # the local seed in E's top 8 bits is the number of failed attempts of the bucket
+    seeds = (E[:-1] >> np.uint64(56)).astype(np.int64)
+    assert int(seeds.sum()) == fails
