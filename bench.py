@@ -125,32 +125,90 @@ def e2e_host_to_disk(ctx, n: int, width: int):
             "path": "host keys -> bsdb_mph_build_index_fixed (F2) -> index.db + hash.dump in /tmp"}
 
 
-def e4_multi_device(ctx, n: int, width: int):
-    """E4 in one process over every visible GPU (bsdb_multi_mph_build_index_fixed
+def e4_multi_device(ctx, n: int, width: int, ndev: int):
+    """E4 in one process over `ndev` GPUs (--e4-devices; bsdb_multi_mph_build_index_fixed
     with no index path: hash of input-order shards -> owner partition -> one
     device-to-device exchange -> range solves -> the MPHF fields in host
-    memory), keys in host memory when the clock starts.  On a one-GPU box this
-    is the one-device build through the multi-device entry point; on an 8-GPU
-    node (the driver's N=1 scaling run sees every GPU) it is the E4 build
-    across them."""
+    memory), keys in host memory when the clock starts.  With one device it
+    is the one-device build through the multi-device entry point.  Both calls
+    are reported: the first (cold: it also grows every context's workspace)
+    and the second."""
     import time as _t
     import torch
     from bsdb_amd.native import Multi
-    ndev = max(1, torch.cuda.device_count())
     keys = ctx.gen_keys13(0, n)[: 13 * n].cpu().numpy()
     torch.cuda.empty_cache()
     times = []
     with Multi(ndev) as mc:
-        for _ in range(2):  # best of two (the first call also grows every context's workspace)
+        for _ in range(2):
             t0 = _t.perf_counter()
             E, _, _ = mc.mph_build_index_fixed(keys, 13, width)
             times.append(_t.perf_counter() - t0)
             assert int(E[-1]) & ((1 << 56) - 1) == n
-    dt = min(times)
-    return {"n_keys": n, "checksum_bits": width, "devices": ndev, "keys_per_s": n / dt, "ms": dt * 1e3,
-            "ms_each": [t * 1e3 for t in times],
-            "path": "host keys -> bsdb_multi_mph_build_index_fixed (E4, one process, every visible GPU) -> "
+    return {"n_keys": n, "checksum_bits": width, "devices": ndev, "keys_per_s": n / times[1], "ms": times[1] * 1e3,
+            "cold_keys_per_s": n / times[0], "cold_ms": times[0] * 1e3,
+            "path": f"host keys -> bsdb_multi_mph_build_index_fixed (E4, one process, {ndev} GPU(s)) -> "
                     "E / values / checksum words in host memory"}
+
+
+def c4_exact_passes(ctx, keys, n: int, width: int):
+    """BASELINE C4's exact index on this one GPU, from the headline's resident
+    keys (bsdb_dev_mph_build_index_passes_fixed): sequential bucket-range
+    passes, each re-hashing every key, sorting, solving and signing its range
+    and writing its index.db slots from the solve; each pass's slots are
+    copied to host memory while the next pass runs.  Clock: keys in HBM ->
+    the GOV structure in HBM + all n index slots in host memory.  One call
+    (it also grows the context's workspace)."""
+    import time as _t
+    import numpy as np
+    import torch
+    index = np.empty(n, np.uint64)                # index.db, 8 n bytes of host memory
+    torch.cuda.synchronize()
+    t0 = _t.perf_counter()
+    E, vals, sb, used = ctx.mph_build_index_passes(keys, 13, n, width, 0, addr_base=0x1000, addr_stride=48,
+                                                   index=index)
+    torch.cuda.synchronize()
+    dt = _t.perf_counter() - t0
+    ok = int(E[-1].item()) & ((1 << 56) - 1) == n
+    del E, vals, sb, index
+    torch.cuda.empty_cache()
+    return {"n_keys": n, "checksum_bits": width, "passes": used, "keys_per_s": n / dt, "ms": dt * 1e3,
+            "check": {"E[m]==n": ok},
+            "path": "keys resident in HBM -> bsdb_dev_mph_build_index_passes_fixed (per pass: re-hash + range "
+                    "select, bucket sort, solve + sign + index slots) -> GOV structure in HBM, index.db slots "
+                    "(8 B x n, byte-reversed addr = 0x1000 + 48 i) in host memory"}
+
+
+def c5_varlen_histogram(ctx, n: int, steps: int):
+    """BASELINE C5 shape at its full size on one GPU: 4e9 variable-length keys
+    (8-64 B, Zipf, mean ~17.7 B) resident with u64
+    offsets, the same hash -> bucket -> histogram -> edge offsets step.
+    Algorithmic bytes per key = key bytes + the 8-byte offset."""
+    import torch
+    blob, off = ctx.gen_keys_var(0, n)
+    m = n // 1500 + 1
+    counts = torch.zeros(m, dtype=torch.int32, device="cuda")
+    E = torch.empty(m + 1, dtype=torch.int64, device="cuda")
+    for _ in range(2):
+        counts.zero_()
+        ctx.histogram_var(blob, off, m, counts=counts)
+        ctx.edge_offsets(counts, out=E)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        counts.zero_()
+        ctx.histogram_var(blob, off, m, counts=counts)
+        ctx.edge_offsets(counts, out=E)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / steps
+    nbytes = int(off[-1].item()) + 8 * n
+    ok = int(E[-1].item()) == n
+    del blob, off, counts, E
+    torch.cuda.empty_cache()
+    return {"n_keys": n, "keys_per_s": n / dt, "ms_per_step": dt * 1e3, "steps": steps,
+            "bytes_per_key": nbytes / n, "roofline_frac": nbytes / dt / (HBM_PEAK_GBS * 1e9),
+            "check": {"E[m]==n": ok},
+            "path": "var-len keys + u64 offsets resident in HBM -> histogram (k_pass1_vare + pass 2) -> E"}
 
 
 def full_build_cpu(n: int, width: int, threads: int):
@@ -188,6 +246,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every CPU this process may use")
     ap.add_argument("--no-full-build", action="store_true", help="skip the full-build figures")
+    ap.add_argument("--e4-devices", type=int, default=1,
+                    help="GPUs of the one-process E4 full-build figure (0 = skip it); never more than asked")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="collective backend (nccl = RCCL over xGMI; gloo only to rehearse N ranks on one GPU)")
     args = ap.parse_args()
@@ -309,18 +369,32 @@ def main():
     full = None
     if rank == 0 and world == 1 and not args.no_full_build:
         # the rest of the build beside the histogram
-        # stage: GPU at C2 and C1 size, the CPU port at C1 size
+        # stage: C4's exact index on the resident keys, C5's var-len histogram
+        # at full size, the GPU full build at C2 and C1 size, the CPU port at C1
+        full = {}
+        try:
+            full["gpu_c4_exact_passes"] = c4_exact_passes(ctx, keys, n, 4)
+        except Exception as e:  # recorded, not faked; the headline line is printed regardless
+            full["gpu_c4_exact_passes"] = {"error": repr(e)[:300]}
+        log("C4 exact full build done")
         del keys
         torch.cuda.empty_cache()
-        full = {"gpu_c2": full_build_gpu(ctx, 100_000_000, 4, 2), "gpu_c1": full_build_gpu(ctx, 1_000_000, 4, 3)}
+        try:
+            full["gpu_c5_varlen_histogram"] = c5_varlen_histogram(ctx, 4_000_000_000, 5)
+        except Exception as e:
+            full["gpu_c5_varlen_histogram"] = {"error": repr(e)[:300]}
+        log("C5 histogram done")
+        full["gpu_c2"] = full_build_gpu(ctx, 100_000_000, 4, 2)
+        full["gpu_c1"] = full_build_gpu(ctx, 1_000_000, 4, 3)
         try:
             full["e2e_c2_host_to_disk"] = e2e_host_to_disk(ctx, 100_000_000, 4)
         except OSError as e:  # (no room for 0.8 GB in /tmp: the figure is skipped, not faked)
             full["e2e_c2_host_to_disk"] = {"skipped": str(e)}
-        try:
-            full["e4_c3_multi_device"] = e4_multi_device(ctx, 1_000_000_000, 4)
-        except Exception as e:  # recorded, not faked; the headline line is printed regardless
-            full["e4_c3_multi_device"] = {"error": repr(e)[:300]}
+        if args.e4_devices > 0:
+            try:
+                full["e4_c3_multi_device"] = e4_multi_device(ctx, 1_000_000_000, 4, args.e4_devices)
+            except Exception as e:  # recorded, not faked; the headline line is printed regardless
+                full["e4_c3_multi_device"] = {"error": repr(e)[:300]}
         if not args.no_cpu:
             full["cpu_c1"] = full_build_cpu(1_000_000, 4, args.cpu_threads)
         log("full-build figures done")

@@ -1,0 +1,116 @@
+"""The JNI shim (jni/gpu_jni.c) and its Java class (jni/GpuBuild.java) against
+the C ABI (include/bsdb_mi355x.h) -- CPU only, no JDK needed:
+
+  * every `native` of GpuBuild has exactly one C definition with the JNI
+    arity (JNIEnv*, jclass, then the Java parameters), and vice versa;
+  * every bsdb_* call in the shim names a function the header declares and
+    libbsdb_mi355x.so exports, with the header's number of arguments;
+  * gcc type-checks the shim against the header (-fsyntax-only, -Werror) with
+    tests/jni_stub/jni.h standing in for the JDK's jni.h.
+
+Reference conventions mirrored: src/main/c/native.c:50-68,
+src/main/java/tech/bsdb/io/Native.java:147-156."""
+import ctypes
+import os
+import re
+import shutil
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SHIM = os.path.join(ROOT, "jni", "gpu_jni.c")
+JAVA = os.path.join(ROOT, "jni", "GpuBuild.java")
+HEADER = os.path.join(ROOT, "include", "bsdb_mi355x.h")
+LIB = os.path.join(ROOT, "bsdb_amd", "libbsdb_mi355x.so")
+
+
+def _split_args(s: str):
+    """Top-level comma split of an argument list (no nested commas at depth > 0)."""
+    out, depth, cur = [], 0, ""
+    for ch in s:
+        if ch in "([{":
+            depth += 1
+        elif ch in ")]}":
+            depth -= 1
+        if ch == "," and depth == 0:
+            out.append(cur.strip())
+            cur = ""
+        else:
+            cur += ch
+    if cur.strip():
+        out.append(cur.strip())
+    return out
+
+
+def _strip_comments(s: str) -> str:
+    s = re.sub(r"/\*.*?\*/", "", s, flags=re.S)
+    return re.sub(r"//[^\n]*", "", s)
+
+
+def header_functions():
+    src = _strip_comments(open(HEADER).read())
+    fns = {}
+    for m in re.finditer(r"\b(?:int|uint64_t|const char \*)\s*\*?\s*(bsdb_\w+)\s*\(([^;{]*?)\)\s*;", src, re.S):
+        args = m.group(2).strip()
+        fns[m.group(1)] = 0 if args in ("", "void") else len(_split_args(args))
+    return fns
+
+
+def java_natives():
+    src = _strip_comments(open(JAVA).read())
+    out = {}
+    for m in re.finditer(r"public\s+static\s+native\s+[\w\[\]]+\s+(\w+)\s*\(([^)]*)\)\s*;", src, re.S):
+        assert m.group(1) not in out, f"overloaded native {m.group(1)}"
+        out[m.group(1)] = len(_split_args(m.group(2)))
+    return out
+
+
+def c_definitions():
+    src = _strip_comments(open(SHIM).read())
+    defs = {}
+    heads = list(re.finditer(r"JNIEXPORT\s+\w+\s+JF\((\w+)\)\s*\(([^)]*)\)\s*\{", src, re.S))
+    for i, m in enumerate(heads):
+        body = src[m.end(): heads[i + 1].start() if i + 1 < len(heads) else len(src)]
+        defs[m.group(1)] = (len(_split_args(m.group(2))), body)
+    return defs
+
+
+def test_every_native_has_one_definition_with_the_jni_arity():
+    jn, cd = java_natives(), c_definitions()
+    assert jn and set(jn) == set(cd), (set(jn) ^ set(cd))
+    for name, nparams in jn.items():
+        assert cd[name][0] == nparams + 2, name  # JNIEnv *, jclass, then the Java parameters
+
+
+def test_shim_calls_exported_header_functions_with_their_arity():
+    fns = header_functions()
+    lib = ctypes.CDLL(LIB)
+    called = set()
+    for name, (_, body) in c_definitions().items():
+        calls = list(re.finditer(r"\b(bsdb_\w+)\s*\(", body))
+        assert calls, f"{name} calls no bsdb_* function"
+        for c in calls:
+            fn = c.group(1)
+            assert fn in fns, f"{name}: {fn} is not declared in include/bsdb_mi355x.h"
+            assert hasattr(lib, fn), f"{name}: {fn} is not exported by libbsdb_mi355x.so"
+            depth, j = 1, c.end()
+            while depth:
+                depth += {"(": 1, ")": -1}.get(body[j], 0)
+                j += 1
+            args = body[c.end(): j - 1].strip()
+            n = 0 if not args else len(_split_args(args))
+            assert n == fns[fn], f"{name}: {fn} called with {n} arguments, the header has {fns[fn]}"
+            called.add(fn)
+    # the host-buffer build path a JVM needs is all bound
+    for fn in ("bsdb_open", "bsdb_close", "bsdb_mph_build_index_var", "bsdb_mph_export", "bsdb_index_open",
+               "bsdb_index_put_fixed", "bsdb_index_close", "bsdb_multi_mph_build_index_fixed", "bsdb_mph_free"):
+        assert fn in called, fn
+
+
+@pytest.mark.skipif(shutil.which("gcc") is None, reason="no gcc")
+def test_shim_type_checks_against_the_header():
+    r = subprocess.run(["gcc", "-fsyntax-only", "-std=gnu11", "-Wall", "-Wextra", "-Wno-unused-parameter", "-Werror",
+                        "-I", os.path.join(ROOT, "tests", "jni_stub"), "-I", os.path.join(ROOT, "include"), SHIM],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
