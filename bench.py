@@ -182,8 +182,9 @@ def c4_exact_passes(ctx, keys, n: int, width: int):
 def c5_varlen_histogram(ctx, n: int, steps: int):
     """BASELINE C5 shape at its full size on one GPU: 4e9 variable-length keys
     (8-64 B, Zipf, mean ~17.7 B) resident with u64
-    offsets, the same hash -> bucket -> histogram -> edge offsets step.
-    Algorithmic bytes per key = key bytes + the 8-byte offset."""
+    offsets, the same hash -> bucket -> histogram -> edge offsets step
+    (algorithmic bytes per key = key bytes + the 8-byte offset); then the
+    whole build of the same keys (cb = 16) by bucket-range passes."""
     import torch
     blob, off = ctx.gen_keys_var(0, n)
     m = n // 1500 + 1
@@ -203,12 +204,29 @@ def c5_varlen_histogram(ctx, n: int, steps: int):
     dt = (time.perf_counter() - t0) / steps
     nbytes = int(off[-1].item()) + 8 * n
     ok = int(E[-1].item()) == n
-    del blob, off, counts, E
+    del counts, E
     torch.cuda.empty_cache()
-    return {"n_keys": n, "keys_per_s": n / dt, "ms_per_step": dt * 1e3, "steps": steps,
+    hist = {"n_keys": n, "keys_per_s": n / dt, "ms_per_step": dt * 1e3, "steps": steps,
             "bytes_per_key": nbytes / n, "roofline_frac": nbytes / dt / (HBM_PEAK_GBS * 1e9),
             "check": {"E[m]==n": ok},
             "path": "var-len keys + u64 offsets resident in HBM -> histogram (k_pass1_vare + pass 2) -> E"}
+    # C5's whole build (cb = 16) on the same resident keys, as c4_exact_passes
+    import numpy as np
+    index = np.empty(n, np.uint64)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    E, vals, sb, used = ctx.mph_build_index_passes(blob, 0, n, 16, 0, offsets=off, addr_base=0x2000, addr_stride=64,
+                                                   index=index)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    okb = int(E[-1].item()) & ((1 << 56) - 1) == n
+    del E, vals, sb, index, blob, off
+    torch.cuda.empty_cache()
+    build = {"n_keys": n, "checksum_bits": 16, "passes": used, "keys_per_s": n / dt, "ms": dt * 1e3,
+             "check": {"E[m]==n": okb},
+             "path": "var-len keys resident in HBM -> bsdb_dev_mph_build_index_passes_var -> GOV structure in "
+                     "HBM, index.db slots in host memory"}
+    return hist, build
 
 
 def full_build_cpu(n: int, width: int, threads: int):
@@ -380,7 +398,8 @@ def main():
         del keys
         torch.cuda.empty_cache()
         try:
-            full["gpu_c5_varlen_histogram"] = c5_varlen_histogram(ctx, 4_000_000_000, 5)
+            full["gpu_c5_varlen_histogram"], full["gpu_c5_full_build_passes"] = c5_varlen_histogram(
+                ctx, 4_000_000_000, 5)
         except Exception as e:
             full["gpu_c5_varlen_histogram"] = {"error": repr(e)[:300]}
         log("C5 histogram done")

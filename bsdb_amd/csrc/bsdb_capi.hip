@@ -8,6 +8,8 @@
 
 #include <dlfcn.h>
 #include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -21,6 +23,7 @@
 #include <memory>
 #include <mutex>
 #include <new>
+#include <string>
 #include <thread>
 #include <vector>
 
@@ -74,6 +77,8 @@ struct bsdb_ctx {
     size_t g_big_bytes = 0, g_slabs_bytes = 0;
     void *g_pay = nullptr;  // F2: input position of each sorted signature
     size_t g_pay_bytes = 0;
+    void *g_led = nullptr;  // the solver's seed ledger (SeedLedger)
+    size_t g_led_bytes = 0;
     bool verify = false;
     // ordering of workspace use across streams: the last call's
     // completion event and stream
@@ -585,6 +590,7 @@ int bsdb_close(bsdb_ctx *c) {
     (void)hipFree(c->g_status);
     (void)hipFree(c->g_big);
     (void)hipFree(c->g_pay);
+    (void)hipFree(c->g_led);
     (void)hipFree(c->g_slabs);
     (void)hipFree(c->pack);
     comm_destroy(c);
@@ -769,7 +775,7 @@ static void print_gov_profile(const std::vector<uint64_t> &h, uint32_t solve_gri
                                "n_small_scc_fallbacks", "fvs_select", "fvs_forms", "fvs_gauss_jordan",
                                "n_fail_degenerate", "n_fail_orient", "n_fail_inconsistent", "failed_attempt_cycles",
                                "bfs_flip", "n_bfs_iters", "n_flip_steps", "n_sel_batches", "n_sel_picks",
-                               "sel_pick_cycles", "sel_prep_cycles", "n_singular_solved", "n_null_vectors"};
+                               "sel_pick_cycles", "sel_prep_cycles", "n_singular_solved", "n_null_vectors", "n_speculative_lost"};
     std::vector<double> tot(GP_N, 0.0);
     for (uint32_t w = 0; w < solve_grid; ++w)
         for (int k = 0; k < GP_N; ++k) {
@@ -919,10 +925,25 @@ static int gov_build_impl(bsdb_ctx *c, const GovSrc &src, uint64_t n_global, uin
     uint32_t fvs_max = FVS_NH_MAX;
     if (const char *v = getenv("BSDB_GOV_FVS_MAX")) fvs_max = (uint32_t)std::max(2, std::min(atoi(v), (int)FVS_NH_MAX));
     if (width && full) HIP_OK(hipMemsetAsync(d_sigbits, 0, ((n_global * width + 63) / 64 + 1) * 8, s));
+    // the seed ledger: claim, won, done (u32 per bucket), fail (4 u64 per
+    // bucket), zeroed; active (u32 per workgroup), all ones
+    const size_t led_zero = (size_t)nb * (3 * 4 + 32);
+    if ((rc = grow(&c->g_led, &c->g_led_bytes, led_zero + (size_t)solve_grid * 4 + 64))) return rc;
+    SeedLedger led;
+    {
+        uint8_t *q = (uint8_t *)c->g_led;
+        led.fail = (unsigned long long *)q;
+        led.claim = (uint32_t *)(q + (size_t)nb * 32);
+        led.won = led.claim + nb;
+        led.done = led.won + nb;
+        led.active = led.done + nb;
+        HIP_OK(hipMemsetAsync(q, 0, led_zero, s));
+        HIP_OK(hipMemsetAsync(led.active, 0xFF, (size_t)solve_grid * 4, s));
+    }
     // A8, with A11 (checksum bits at each rank), F2 (ranks) and A13 (index
     // slots) in the solve
     SolveArgs sa{sorted, b_hi, d_E, d_values, (uint64_t *)c->g_scratch, status, d_prof, fvs_max, b_lo, e_lo,
-                 d_sigbits, width, pay, d_rank, ixo.index, ixo.idx_lo, ixo.addr, ixo.addr_base, ixo.addr_stride};
+                 d_sigbits, width, pay, d_rank, ixo.index, ixo.idx_lo, ixo.addr, ixo.addr_base, ixo.addr_stride, led};
     // zeroing status[2] (the bucket queue) above happens before both launches
     k_gov_solve<<<solve_grid, GS_THREADS, 0, s>>>(sa);  // A8
     if (nbig)
@@ -1300,3 +1321,4 @@ int bsdb_hash_var(bsdb_ctx *c, const uint8_t *h_blob, const uint64_t *h_off, uin
 #include "capi_mph.hip"
 #include "capi_multi.hip"
 #include "capi_passes.hip"
+#include "capi_kv.hip"

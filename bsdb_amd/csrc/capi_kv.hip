@@ -1,0 +1,257 @@
+// capi_kv.hip -- F3: the kv.db scan that feeds BSDBWriter.buildIndex, native.
+// Included by bsdb_capi.hip after capi_mph.hip.  Host code only.
+//   W   = src/main/java/tech/bsdb/write/BSDBWriter.java
+//   PKV = src/main/java/tech/bsdb/write/PartitionedKVWriter.java
+//   SCK = src/main/java/tech/bsdb/write/SimpleCompactKVWriter.java
+//   BKV = src/main/java/tech/bsdb/write/BlockedKVWriter.java
+//
+// buildIndex walks every record of the data files through kvWriter.forEach
+// (W:134, PKV:50-70: one task per partition file) and hands each record's
+// (address, key, value) to getLong.  The reference allocates two byte[] per
+// record (SCK:62-66, BKV:98-103) and re-scans the files once per index pass.
+// Here each partition file is mapped and parsed by a host thread into packed
+// arrays -- key blob (+ offsets unless every key has one length), record
+// address, the first <= 8 value bytes and their count (index_a.db) -- in
+// partition order, ready for the one-call build (F2: ranks from the solve,
+// index slots scattered on the device, one write of each file).
+//
+// Formats (the two uncompressed kv.db layouts):
+//   0 compact  SimpleCompactKVWriter: records [kLen u8][vLen u16 BE][key][value]
+//              back to back, kLen 0 or end of file ends the partition (SCK:55-70);
+//              address = partition << 56 | byte offset (SCK:67).
+//   1 blocked  SimpleBlockedKVWriter: blocks of block_size bytes, records never
+//              straddle a block, a 0 byte ends a block's records (BKV:67-74);
+//              a record longer than a block sits alone in a page-aligned large
+//              block (BKV:50-58); address = partition << 56 | block pages << 48
+//              | block position in pages << 16 | offset in the block (BKV:124-136).
+//              The reference hands a large record's value as null (BKV:105-109,
+//              so approximate mode fails there); here its bytes are read.
+// The zstd-compressed layout (KVWriterCompressed) is not read: out of scope.
+
+struct bsdb_kv_records {
+    uint64_t n = 0;
+    uint32_t fixed_len = 0;  // every key this long; 0 when lengths differ (or n == 0)
+    std::vector<uint8_t> blob;
+    std::vector<uint64_t> off;  // n + 1
+    std::vector<uint64_t> addr, value8;
+    std::vector<uint8_t> vlen;
+};
+
+namespace {
+
+constexpr uint32_t KV_PAGE = 4096;  // NativeFileIO.PAGE_SIZE
+
+struct KvPart {
+    std::vector<uint8_t> blob;
+    std::vector<uint64_t> len_end;  // running key-byte totals (offsets without the leading 0)
+    std::vector<uint64_t> addr, value8;
+    std::vector<uint8_t> vlen;
+    int rc = BSDB_OK;
+    void add(uint64_t a, const uint8_t *key, uint32_t kl, const uint8_t *val, uint32_t vl) {
+        blob.insert(blob.end(), key, key + kl);
+        len_end.push_back(blob.size());
+        addr.push_back(a);
+        uint64_t v = 0;
+        const uint32_t h = vl < 8 ? vl : 8;
+        for (uint32_t i = 0; i < h; ++i) v |= (uint64_t)val[i] << (8 * i);
+        value8.push_back(v);
+        vlen.push_back((uint8_t)h);
+    }
+};
+
+struct Mapped {
+    const uint8_t *p = nullptr;
+    size_t size = 0;
+    ~Mapped() {
+        if (p && size) munmap((void *)p, size);
+    }
+};
+
+int map_file(const std::string &path, Mapped &m) {
+    const int fd = open(path.c_str(), O_RDONLY);
+    if (fd < 0) return BSDB_EFILE;
+    struct stat st;
+    if (fstat(fd, &st) != 0) {
+        close(fd);
+        return BSDB_EFILE;
+    }
+    m.size = (size_t)st.st_size;
+    if (m.size) {
+        void *q = mmap(nullptr, m.size, PROT_READ, MAP_PRIVATE, fd, 0);
+        if (q == MAP_FAILED) {
+            close(fd);
+            m.size = 0;
+            return BSDB_EFILE;
+        }
+        (void)madvise(q, m.size, MADV_SEQUENTIAL);
+        m.p = (const uint8_t *)q;
+    }
+    close(fd);
+    return BSDB_OK;
+}
+
+// SCK:55-70
+int scan_compact(const Mapped &m, uint64_t part, KvPart &out) {
+    uint64_t pos = 0;
+    while (pos < m.size) {
+        const uint32_t kl = m.p[pos];
+        if (kl == 0) break;
+        if (pos + 3 > m.size) return BSDB_EFILE;
+        const uint32_t vl = ((uint32_t)m.p[pos + 1] << 8) | m.p[pos + 2];
+        if (pos + 3 + kl + vl > m.size) return BSDB_EFILE;
+        out.add(part << 56 | pos, m.p + pos + 3, kl, m.p + pos + 3 + kl, vl);
+        pos += 3 + (uint64_t)kl + vl;
+    }
+    return BSDB_OK;
+}
+
+// BKV:84-121
+int scan_blocked(const Mapped &m, uint64_t part, uint32_t block, KvPart &out) {
+    uint64_t position = 0;
+    while (position < m.size) {
+        const uint64_t end = std::min<uint64_t>(m.size, position + block);  // readBlockAt: up to one block
+        uint64_t next = block;
+        uint64_t o = position;
+        while (o < end) {
+            const uint32_t kl = m.p[o];
+            if (kl == 0) break;
+            if (o + 3 + kl > end) return BSDB_EFILE;
+            const uint32_t vl = ((uint32_t)m.p[o + 1] << 8) | m.p[o + 2];
+            const uint32_t rec_off = (uint32_t)(o - position);
+            if (o + 3 + kl + vl <= end) {
+                out.add(part << 56 | (uint64_t)(block / KV_PAGE) << 48 | (position / KV_PAGE) << 16 | rec_off,
+                        m.p + o + 3, kl, m.p + o + 3 + kl, vl);
+                o += 3 + (uint64_t)kl + vl;
+            } else {
+                // a large record alone in a page-aligned block (BKV:104-109)
+                const uint64_t rec = 3 + (uint64_t)kl + vl;
+                next = (rec + KV_PAGE - 1) / KV_PAGE * KV_PAGE;
+                if (position + rec > m.size) return BSDB_EFILE;
+                out.add(part << 56 | (next / KV_PAGE) << 48 | (position / KV_PAGE) << 16 | rec_off, m.p + o + 3, kl,
+                        m.p + o + 3 + kl, vl);
+                break;
+            }
+        }
+        position += next;
+    }
+    return BSDB_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int bsdb_kv_scan(const char *kv_base, int partitions, int format, uint32_t block_size, int threads,
+                 bsdb_kv_records **out) {
+    if (!kv_base || !out || partitions < 1 || (format != 0 && format != 1) ||
+        (format == 1 && (block_size == 0 || block_size % KV_PAGE)))
+        return BSDB_EINVAL;
+    *out = nullptr;
+    std::vector<KvPart> parts(partitions);
+    const int T = std::max(1, std::min(threads > 0 ? threads : (int)std::thread::hardware_concurrency(), partitions));
+    std::atomic<int> next{0};
+    auto worker = [&] {
+        for (int p; (p = next.fetch_add(1)) < partitions;) {
+            Mapped m;
+            const std::string path = std::string(kv_base) + "." + std::to_string(p);  // PKV:79-81
+            int rc = map_file(path, m);
+            if (!rc) rc = format == 0 ? scan_compact(m, (uint64_t)p, parts[p]) : scan_blocked(m, (uint64_t)p, block_size, parts[p]);
+            parts[p].rc = rc;
+        }
+    };
+    std::vector<std::thread> th;
+    for (int t = 1; t < T; ++t) th.emplace_back(worker);
+    worker();
+    for (auto &t : th) t.join();
+    for (auto &p : parts)
+        if (p.rc) return p.rc;
+    bsdb_kv_records *r = new (std::nothrow) bsdb_kv_records();
+    if (!r) return BSDB_ENOMEM;
+    uint64_t n = 0, bytes = 0;
+    for (auto &p : parts) {
+        n += p.addr.size();
+        bytes += p.blob.size();
+    }
+    try {
+        r->n = n;
+        r->blob.reserve(bytes + 16);
+        r->off.reserve(n + 1);
+        r->addr.reserve(n);
+        r->value8.reserve(n);
+        r->vlen.reserve(n);
+        r->off.push_back(0);
+        uint32_t fixed = 0;
+        bool same = true;
+        for (auto &p : parts) {
+            const uint64_t base = r->blob.size();
+            uint64_t prev = 0;
+            for (uint64_t e : p.len_end) {
+                const uint64_t l = e - prev;
+                prev = e;
+                if (!fixed) fixed = (uint32_t)l;
+                same = same && l == fixed;
+                r->off.push_back(base + e);
+            }
+            r->blob.insert(r->blob.end(), p.blob.begin(), p.blob.end());
+            r->addr.insert(r->addr.end(), p.addr.begin(), p.addr.end());
+            r->value8.insert(r->value8.end(), p.value8.begin(), p.value8.end());
+            r->vlen.insert(r->vlen.end(), p.vlen.begin(), p.vlen.end());
+            std::vector<uint8_t>().swap(p.blob);  // (peak memory: one partition twice)
+        }
+        r->fixed_len = n && same ? fixed : 0;
+        r->blob.resize(bytes + 16, 0);  // readable slack past the last key
+        r->blob.resize(bytes);
+    } catch (const std::bad_alloc &) {
+        delete r;
+        return BSDB_ENOMEM;
+    }
+    *out = r;
+    return BSDB_OK;
+}
+
+int bsdb_kv_records_info(const bsdb_kv_records *r, uint64_t *n, uint64_t *key_bytes, uint32_t *fixed_len) {
+    if (!r) return BSDB_EINVAL;
+    if (n) *n = r->n;
+    if (key_bytes) *key_bytes = r->blob.size();
+    if (fixed_len) *fixed_len = r->fixed_len;
+    return BSDB_OK;
+}
+
+int bsdb_kv_records_arrays(const bsdb_kv_records *r, const uint8_t **blob, const uint64_t **off,
+                           const uint64_t **addr, const uint64_t **value8, const uint8_t **vlen) {
+    if (!r) return BSDB_EINVAL;
+    if (blob) *blob = r->blob.data();
+    if (off) *off = r->off.data();
+    if (addr) *addr = r->addr.data();
+    if (value8) *value8 = r->value8.data();
+    if (vlen) *vlen = r->vlen.data();
+    return BSDB_OK;
+}
+
+int bsdb_kv_records_free(bsdb_kv_records *r) {
+    if (!r) return BSDB_EINVAL;
+    delete r;
+    return BSDB_OK;
+}
+
+// W:91-155 from the data files: scan, then the one-call build (hash, GOV
+// build with ranks and checksum bits, index scatter, index.db / index_a.db)
+int bsdb_kv_build_index(bsdb_ctx *c, const char *kv_base, int partitions, int format, uint32_t block_size,
+                        int threads, uint32_t width, int approximate, const char *index_path, const char *index_a_path,
+                        bsdb_mph **out) {
+    if (!c || !out || !index_path || width > 64) return BSDB_EINVAL;
+    *out = nullptr;
+    bsdb_kv_records *r = nullptr;
+    int rc = bsdb_kv_scan(kv_base, partitions, format, block_size, threads, &r);
+    if (rc) return rc;
+    std::unique_ptr<bsdb_kv_records, int (*)(bsdb_kv_records *)> guard(r, bsdb_kv_records_free);
+    const uint64_t *v8 = approximate ? r->value8.data() : nullptr;
+    const uint8_t *vl = approximate ? r->vlen.data() : nullptr;
+    if (r->fixed_len)
+        return bsdb_mph_build_index_fixed(c, r->blob.data(), r->fixed_len, r->n, width, r->addr.data(), v8, vl,
+                                          approximate, index_path, index_a_path, out);
+    return bsdb_mph_build_index_var(c, r->blob.data(), r->off.data(), r->n, width, r->addr.data(), v8, vl, approximate,
+                                    index_path, index_a_path, out);
+}
+
+}  // extern "C"

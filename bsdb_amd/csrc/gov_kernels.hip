@@ -216,6 +216,21 @@ __global__ __launch_bounds__(GB_THREADS) void k_bucket_sort_big(uint64_t *sig, c
 }
 
 // ---- A8: per-bucket solve --------------------------------------------------
+// Seeds of one bucket may be tried by several workgroups at once.  claim[b]
+// hands out seed numbers in increasing order; a failed seed sets its bit in
+// fail[b] (256 bits); a solved one max-es won[b] with 256 - seed (so won holds
+// the lowest solved seed) and waits until every lower seed has failed (it is
+// the bucket's seed: it stores the solution) or a lower one solved (it drops
+// its own).  A lower seed's workgroup never waits on a higher one, and every
+// handed-out seed is being tried by a resident workgroup, so the waits end.
+struct SeedLedger {
+    uint32_t *claim;          // [nb] next seed to hand out
+    uint32_t *won;            // [nb] 256 - lowest solved seed, 0 = none yet
+    unsigned long long *fail; // [nb][4] failed seeds
+    uint32_t *done;           // [nb] 1 once the bucket's solution is stored (or its seeds ran out)
+    uint32_t *active;         // [grid] the bucket each workgroup works on (0xFFFFFFFF = none)
+};
+
 struct SolveArgs {
     const uint64_t *sig;  // sorted signatures of buckets [b0, m), the first at global offset e0
     uint64_t m;           // end of the bucket range
@@ -240,7 +255,13 @@ struct SolveArgs {
     uint64_t idx_lo;
     const uint64_t *addr;
     uint64_t addr_base, addr_stride;
+    // the seed ledger of k_gov_solve (per bucket of the range, zeroed; active
+    // per workgroup, all ones): workgroups with no bucket left try the next
+    // seeds of buckets still being solved; the bucket's seed is still the
+    // first one that solves it (GOV:425-432)
+    SeedLedger led;
 };
+
 
 // phase counters (cycles, or counts for the GP_N_* slots)
 enum GovProf { GP_EDGES, GP_PEEL, GP_GREEDY, GP_BFS, GP_TARJAN, GP_SINGLE, GP_DENSE, GP_BACK, GP_STORE,
@@ -248,7 +269,7 @@ enum GovProf { GP_EDGES, GP_PEEL, GP_GREEDY, GP_BFS, GP_TARJAN, GP_SINGLE, GP_DE
                GP_N_SCC_SWEEPS, GP_N_SMALL_S, GP_FVS_SEL, GP_FVS_FORMS, GP_FVS_GJ,
                GP_N_FAIL_DEGEN, GP_N_FAIL_ORIENT, GP_N_FAIL_INCONS, GP_FAILED_CYCLES, GP_BFS_FLIP, GP_N_BFS_ITERS,
                GP_N_FLIP_STEPS, GP_N_SEL_BATCHES, GP_N_SEL_PICKS, GP_SEL_PICK_CYCLES, GP_SEL_PREP_CYCLES,
-               GP_N_SING_SOLVED, GP_N_NULL_VECS, GP_N };
+               GP_N_SING_SOLVED, GP_N_NULL_VECS, GP_N_SPEC_LOST, GP_N };
 
 // Solver state for buckets of up to CMAX_ keys: LDS for GS_CMAX, a global
 // slab per workgroup for GB_CMAX (same code; indices fit int16 either way).
@@ -1588,6 +1609,9 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
     return true;
 }
 
+template <class Lds>
+__device__ __forceinline__ void store_bucket(Lds &L, const SolveArgs &a, uint64_t b, uint32_t j, PhaseClock &pc);
+
 // Solves bucket b with state L (LDS or a global slab) and stores its values
 // and local seed.  Workgroup-uniform.
 template <class Lds>
@@ -1613,6 +1637,19 @@ __device__ __forceinline__ void solve_bucket(Lds &L, const SolveArgs &a, uint64_
         if (threadIdx.x == 0) atomicOr(a.status, (uint32_t)GOV_SEEDS);
         return;
     }
+    store_bucket(L, a, b, j, pc);
+}
+
+// Stores bucket b's solution (L after a successful try_seed with seed j):
+// its 2-bit values, the seed in E[b]'s top byte and the F2 / A11 / A13
+// outputs.  Workgroup-uniform.
+template <class Lds>
+__device__ __forceinline__ void store_bucket(Lds &L, const SolveArgs &a, uint64_t b, uint32_t j, PhaseClock &pc) {
+    const uint64_t lo = a.E[b] & OFFSET_MASK, hi = a.E[b + 1] & OFFSET_MASK;
+    const uint32_t cnt = (uint32_t)(hi - lo);
+    const uint64_t vo = vertex_offset(lo);
+    const uint32_t nv = (uint32_t)(vertex_offset(hi) - vo);
+    const ulonglong2 *sig = reinterpret_cast<const ulonglong2 *>(a.sig) + (lo - a.e0);
     // values: hinge -> xval or 3, other vertices 0; words shared with the
     // neighbouring buckets are OR-ed
     const uint64_t w0 = vo >> 5, w1 = (vo + nv + 31) >> 5;
@@ -1658,23 +1695,126 @@ __device__ __forceinline__ void solve_bucket(Lds &L, const SolveArgs &a, uint64_
     pc.lap(GP_STORE);
 }
 
+__device__ __forceinline__ uint32_t ld_agent(const uint32_t *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned long long ld_agent64(const unsigned long long *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// all seeds below s of local bucket lb failed
+__device__ __forceinline__ bool lower_seeds_failed(const SeedLedger &g, uint32_t lb, uint32_t s) {
+    for (uint32_t w = 0; w * 64 < s; ++w) {
+        const unsigned long long want = s >= (w + 1) * 64 ? ~0ULL : ((1ULL << (s - w * 64)) - 1);
+        if ((ld_agent64(g.fail + 4 * (size_t)lb + w) & want) != want) return false;
+    }
+    return true;
+}
+
 __global__ __launch_bounds__(GS_THREADS, GS_THREADS * GS_PER_CU / 256) void k_gov_solve(SolveArgs a) {
     __shared__ SolveLds L;
     uint64_t *scr = a.scratch + (size_t)blockIdx.x * solve_scratch_words<SolveLds>();
     PhaseClock pc{a.prof ? a.prof + (size_t)blockIdx.x * GP_N : nullptr, 0};
+    const SeedLedger &g = a.led;
+    const uint32_t nb = (uint32_t)(a.m - a.b0);
     // buckets from a queue (status[2], zeroed with the status word): seed
     // retries make per-bucket cost uneven, a static stride left the slowest
-    // workgroup ~13 % (C2) to ~40 % (1e7 keys) behind the mean
-    __shared__ uint32_t next_b;
+    // workgroup ~13 % (C2) to ~40 % (1e7 keys) behind the mean.  A workgroup
+    // stays on its bucket until it is done; with the queue empty it tries
+    // the next seeds of other workgroups' buckets (the seed ledger).
+    __shared__ uint32_t sh_lb, sh_s, sh_win;
+    uint32_t cur = 0xFFFFFFFFu;  // (thread 0) this workgroup's bucket
+    bool queue_open = true;      // (thread 0)
     for (;;) {
         __syncthreads();
-        if (threadIdx.x == 0) next_b = atomicAdd(a.status + 2, 1u);
+        if (threadIdx.x == 0) {
+            uint32_t lb = 0xFFFFFFFFu, sd = 0;
+            // 1. more seeds of my own bucket
+            if (cur != 0xFFFFFFFFu && !ld_agent(g.done + cur) && ld_agent(g.won + cur) == 0) {
+                sd = atomicAdd(g.claim + cur, 1u);
+                if (sd < 256) lb = cur;
+            }
+            // 2. a new bucket from the queue
+            while (lb == 0xFFFFFFFFu && queue_open) {
+                const uint32_t q = atomicAdd(a.status + 2, 1u);
+                if (q >= nb) {
+                    queue_open = false;
+                    break;
+                }
+                const uint64_t b = a.b0 + q;
+                if ((a.E[b + 1] & OFFSET_MASK) - (a.E[b] & OFFSET_MASK) > (uint64_t)GS_CMAX) continue;  // k_gov_solve_big
+                cur = q;
+                __hip_atomic_store(g.active + blockIdx.x, q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                sd = atomicAdd(g.claim + q, 1u);
+                if (sd < 256) lb = q;
+            }
+            // 3. the next seed of a bucket another workgroup still solves
+            for (uint32_t k = 0; lb == 0xFFFFFFFFu && !queue_open && k < gridDim.x; ++k) {
+                const uint32_t o = ld_agent(g.active + (blockIdx.x + k) % gridDim.x);
+                if (o == 0xFFFFFFFFu || ld_agent(g.done + o) || ld_agent(g.won + o)) continue;
+                sd = atomicAdd(g.claim + o, 1u);
+                if (sd < 256) lb = o;
+            }
+            sh_lb = lb;
+            sh_s = sd;
+        }
         __syncthreads();
-        const uint64_t b = a.b0 + next_b;
-        if (b >= a.m) break;
-        const uint64_t cnt = (a.E[b + 1] & OFFSET_MASK) - (a.E[b] & OFFSET_MASK);
-        if (cnt > (uint64_t)GS_CMAX) continue;  // k_gov_solve_big
-        solve_bucket(L, a, b, scr, pc);
+        const uint32_t lb = sh_lb, sd = sh_s;
+        if (lb == 0xFFFFFFFFu) break;
+        const uint64_t b = a.b0 + lb;
+        const uint64_t lo = a.E[b] & OFFSET_MASK, hi = a.E[b + 1] & OFFSET_MASK;
+        const uint32_t cnt = (uint32_t)(hi - lo);
+        const uint32_t nv = (uint32_t)(vertex_offset(hi) - vertex_offset(lo));
+        if (cnt == 0) {  // nothing to solve: seed 0, no values
+            if (threadIdx.x == 0 && sd == 0) __hip_atomic_store(g.done + lb, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            continue;
+        }
+        if (nv > (uint32_t)SolveLds::NVMAX) {
+            if (threadIdx.x == 0) {
+                atomicOr(a.status, (uint32_t)GOV_TOO_BIG);
+                __hip_atomic_store(g.done + lb, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            continue;
+        }
+        const ulonglong2 *sig = reinterpret_cast<const ulonglong2 *>(a.sig) + (lo - a.e0);
+        const uint64_t t_try = pc.acc ? clock64() : 0;
+        const bool ok = try_seed(L, sig, cnt, nv, (uint64_t)sd << 56, scr, pc, a.fvs_max);
+        if (threadIdx.x == 0) {
+            uint32_t win = 0;
+            if (!ok) {
+                atomicOr(g.fail + 4 * (size_t)lb + sd / 64, 1ULL << (sd & 63));
+                if (lower_seeds_failed(g, lb, 256)) {  // every seed failed (GOV:431); the last to fail sees it
+                    atomicOr(a.status, (uint32_t)GOV_SEEDS);
+                    __hip_atomic_store(g.done + lb, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+            } else {
+                atomicMax(g.won + lb, 256u - sd);
+                for (;;) {  // the bucket's seed only when every lower seed failed
+                    if (ld_agent(g.won + lb) > 256u - sd) break;  // a lower seed solved it
+                    if (lower_seeds_failed(g, lb, sd)) {
+                        win = 1;
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(4);
+                }
+            }
+            sh_win = win;
+        }
+        __syncthreads();
+        if (!ok) {
+            if (pc.acc) pc.add(GP_FAILED_CYCLES, clock64() - t_try);
+            continue;
+        }
+        if (!sh_win) {
+            pc.add(GP_N_SPEC_LOST, 1);
+            continue;
+        }
+        pc.start();
+        store_bucket(L, a, b, sd, pc);
+        if (threadIdx.x == 0) {
+            __threadfence();
+            __hip_atomic_store(g.done + lb, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
     }
 }
 

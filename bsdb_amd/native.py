@@ -97,6 +97,13 @@ SIGNATURES = [
     ("bsdb_index_put_fixed", _i, [_vp, _vp, _u32, _u64, _vp, _vp, _vp]),
     ("bsdb_index_end_pass", _i, [_vp]),
     ("bsdb_index_close", _i, [_vp]),
+    ("bsdb_kv_scan", _i, [C.c_char_p, _i, _i, _u32, _i, C.POINTER(_vp)]),
+    ("bsdb_kv_records_info", _i, [_vp, C.POINTER(_u64), C.POINTER(_u64), C.POINTER(_u32)]),
+    ("bsdb_kv_records_arrays", _i, [_vp, C.POINTER(_vp), C.POINTER(_vp), C.POINTER(_vp), C.POINTER(_vp),
+                                    C.POINTER(_vp)]),
+    ("bsdb_kv_records_free", _i, [_vp]),
+    ("bsdb_kv_build_index", _i, [_vp, C.c_char_p, _i, _i, _u32, _i, _u32, _i, C.c_char_p, C.c_char_p,
+                                 C.POINTER(_vp)]),
 ]
 
 HIST_AUTO, HIST_PARTITIONED, HIST_ATOMIC = 0, 1, 2
@@ -404,6 +411,16 @@ class Context:
             v8.ctypes.data if v8 is not None else None, vl.ctypes.data if vl is not None else None,
             1 if approximate else 0, index_path.encode(), index_a_path.encode() if index_a_path else None,
             C.byref(h)))
+        return Mph(h, self)
+
+    def kv_build_index(self, kv_base: str, partitions: int, width: int, index_path: str,
+                       index_a_path: Optional[str] = None, approximate: bool = False, fmt: int = 0,
+                       block_size: int = 4096, threads: int = 0) -> "Mph":
+        """W:91-155 from the data files: native kv.db scan + the one-call build."""
+        h = C.c_void_p()
+        _check("bsdb_kv_build_index", lib().bsdb_kv_build_index(
+            self._h, kv_base.encode(), partitions, fmt, block_size, threads, width, 1 if approximate else 0,
+            index_path.encode(), index_a_path.encode() if index_a_path else None, C.byref(h)))
         return Mph(h, self)
 
     def mph_build_index_var(self, blob_np, off_np, width: int, addr_np, index_path: str,
@@ -752,6 +769,31 @@ class Multi:
             1 if approximate else 0, index_path.encode() if index_path else None,
             index_a_path.encode() if index_a_path else None, E.ctypes.data, vals.ctypes.data, _np_ptr(sb)))
         return E, vals, sb
+
+
+def kv_scan(kv_base: str, partitions: int, fmt: int = 0, block_size: int = 4096, threads: int = 0) -> dict:
+    """The native kv.db scan (bsdb_kv_scan): dict of numpy copies -- blob,
+    offsets, addr, value8, vlen, fixed_len.  Host only (no device needed)."""
+    import numpy as np
+    h = C.c_void_p()
+    _check("bsdb_kv_scan", lib().bsdb_kv_scan(kv_base.encode(), partitions, fmt, block_size, threads, C.byref(h)))
+    try:
+        n, nb, fl = C.c_uint64(), C.c_uint64(), C.c_uint32()
+        _check("bsdb_kv_records_info", lib().bsdb_kv_records_info(h, C.byref(n), C.byref(nb), C.byref(fl)))
+        ptrs = [C.c_void_p() for _ in range(5)]
+        _check("bsdb_kv_records_arrays", lib().bsdb_kv_records_arrays(h, *[C.byref(q) for q in ptrs]))
+
+        def arr(q, count, dt):
+            if count == 0 or not q.value:
+                return np.zeros(0, dt)
+            return np.ctypeslib.as_array(C.cast(q, C.POINTER(np.ctypeslib.as_ctypes_type(dt))),
+                                         shape=(count,)).copy()
+        N = n.value
+        return {"blob": arr(ptrs[0], nb.value, np.uint8), "offsets": arr(ptrs[1], N + 1, np.uint64),
+                "addr": arr(ptrs[2], N, np.uint64), "value8": arr(ptrs[3], N, np.uint64),
+                "vlen": arr(ptrs[4], N, np.uint8), "fixed_len": fl.value}
+    finally:
+        lib().bsdb_kv_records_free(h)
 
 
 def _np_ptr(a):

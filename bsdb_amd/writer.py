@@ -23,9 +23,14 @@ fallback.  ``fused_index=True`` builds hash + index in one call whose solve
 returns every key's rank (bsdb_mph_build_index_var): no
 per-pass rescan, the same files.  ``devices=[...]`` makes that one call the
 multi-device build over those GPUs (bsdb_multi_mph_build_index_var, E4).
+``from_files=True`` builds from the data files it wrote instead: the native
+kv.db scan (bsdb_kv_build_index, F3) reads every kv.db.<p> back as
+buildIndex's kvWriter.forEach does (W:134) and runs the same one-call build.
 ``put`` is per record and safe to call from concurrent threads, as the
 reference's Builder does (Builder.java:144-160); ``put_batch`` takes a whole
-key blob at once.
+key blob at once.  The kv.db writer is the minimal compact layout of
+bsdb_amd/kvfiles.py (numpy, whole arrays): a test and bench harness for the
+index path, not a replacement of the reference's KV writers.
 """
 from __future__ import annotations
 
@@ -34,6 +39,7 @@ from typing import Optional
 
 import numpy as np
 
+from . import kvfiles
 from .native import Context, Mph
 
 SLOT_SIZE = 8          # Common.java SLOT_SIZE
@@ -45,7 +51,8 @@ class BSDBWriter:
     def __init__(self, base_path: str, tmp_dir: Optional[str] = None, checksum_bits: int = 4,
                  pass_cache_size: int = 1 << 30, compact: bool = True, compress: bool = False,
                  compress_block_size: int = 8192, shared_dict_size: int = 0, approximate_mode: bool = False,
-                 partitions: int = 1, device: int = 0, fused_index: bool = False, devices=None):
+                 partitions: int = 1, device: int = 0, fused_index: bool = False, devices=None,
+                 from_files: bool = False):
         if compress or not compact:
             raise NotImplementedError("only the compact kv.db layout is mirrored (kv.db formats are out of scope)")
         self.base = base_path
@@ -55,7 +62,8 @@ class BSDBWriter:
         self.approximate = approximate_mode
         self.partitions = partitions
         self.compress_block_size = compress_block_size
-        self.fused_index = fused_index or devices is not None
+        self.fused_index = fused_index or devices is not None or from_files
+        self.from_files = from_files
         self.devices = list(devices) if devices is not None else None
         self._puts: list = []  # (key, value) pairs: one list.append per put, atomic across threads
         self._batches: list = []  # (blob, offsets, value8, vlen, value bytes total)
@@ -99,22 +107,9 @@ class BSDBWriter:
 
     def _write_kv(self, blob, off, vals):
         """kv.db.<p>: record i goes to partition i % partitions; returns addresses."""
-        n = off.size - 1
-        addr = np.zeros(n, np.uint64)
-        files = [open(os.path.join(self.base, f"kv.db.{p}"), "wb") for p in range(self.partitions)]
-        pos = [0] * self.partitions
-        try:
-            for i in range(n):
-                p = i % self.partitions
-                k = blob[int(off[i]): int(off[i + 1])].tobytes()
-                v = vals[i]
-                files[p].write(bytes([len(k)]) + len(v).to_bytes(2, "big") + k + v)
-                addr[i] = (p << 56) | pos[p]
-                pos[p] += RECORD_HEADER + len(k) + len(v)
-        finally:
-            for f in files:
-                f.close()
-        return addr
+        vblob, voff = kvfiles.pack_values(vals)
+        self._vblob, self._voff = vblob, voff
+        return kvfiles.write_compact(os.path.join(self.base, "kv.db"), self.partitions, blob, off, vblob, voff)
 
     def _write_config(self, off, vals):
         n = off.size - 1
@@ -138,8 +133,13 @@ class BSDBWriter:
         self._write_config(off, vals)
         self._blob, self._off, self._vals = blob, off, vals
         if self.fused_index:
-            value8, vlen = self._value_heads()
             paths = (os.path.join(self.base, "index.db"), os.path.join(self.base, "index_a.db"))
+            if self.from_files:  # F3: the native scan of the data files just written
+                mph = self.ctx.kv_build_index(os.path.join(self.base, "kv.db"), self.partitions, self.checksum_bits,
+                                              *paths, self.approximate)
+                mph.dump(os.path.join(self.base, "hash.dump"))
+                return mph
+            value8, vlen = self._value_heads()
             if self.devices is not None:
                 from .native import Multi
                 with Multi(len(self.devices), self.devices) as mc:
@@ -181,11 +181,13 @@ class BSDBWriter:
         n = self._off.size - 1
         value8 = np.zeros(n, np.uint64)
         vlen = np.zeros(n, np.uint8)
-        if self.approximate:
-            for i, v in enumerate(self._vals):
-                head = v[:8]
-                value8[i] = int.from_bytes(head, "little")
-                vlen[i] = len(head)
+        if self.approximate and n:
+            voff = self._voff.astype(np.int64)
+            vlen = np.minimum(np.diff(voff), 8).astype(np.uint8)
+            padded = np.concatenate([self._vblob, np.zeros(8, np.uint8)])
+            heads = padded[voff[:-1, None] + np.arange(8)[None, :]]       # 8 bytes from each value's start
+            heads[np.arange(8)[None, :] >= vlen[:, None]] = 0             # bytes past the value: 0
+            value8 = heads.copy().view(np.uint64).reshape(n)
         return value8, vlen
 
     def close(self):

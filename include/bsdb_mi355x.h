@@ -408,6 +408,31 @@ int bsdb_index_put_fixed(bsdb_index *ix, const uint8_t *h_keys, uint32_t key_len
 int bsdb_index_end_pass(bsdb_index *ix);
 int bsdb_index_close(bsdb_index *ix);
 
+/* ---------------------------------------------------------------------------
+ * F3: the kv.db scan that feeds buildIndex (W:134, PartitionedKVWriter.forEach
+ * PKV:50-70), native: every partition file <kv_base>.<p> (PKV:79-81) is mapped
+ * and parsed by a host thread into packed arrays in partition order -- the key
+ * blob (+ offsets), each record's address as the reference computes it, the
+ * first <= 8 value bytes (LE) and their count (index_a.db, W:140-142).
+ * format 0 = SimpleCompactKVWriter (SimpleCompactKVWriter.java:55-70),
+ * 1 = SimpleBlockedKVWriter with block_size-byte blocks (BlockedKVWriter.java:
+ * 84-136).  threads <= 0: every hardware thread.  Host only (no device).
+ * ------------------------------------------------------------------------- */
+typedef struct bsdb_kv_records bsdb_kv_records;
+int bsdb_kv_scan(const char *kv_base, int partitions, int format, uint32_t block_size, int threads,
+                 bsdb_kv_records **out);
+/* n records, their key bytes, and fixed_len = the common key length (0 when lengths differ) */
+int bsdb_kv_records_info(const bsdb_kv_records *r, uint64_t *n, uint64_t *key_bytes, uint32_t *fixed_len);
+/* borrowed pointers, valid until bsdb_kv_records_free: blob, offsets[n+1], addr[n], value8[n], vlen[n] */
+int bsdb_kv_records_arrays(const bsdb_kv_records *r, const uint8_t **blob, const uint64_t **offsets,
+                           const uint64_t **addr, const uint64_t **value8, const uint8_t **vlen);
+int bsdb_kv_records_free(bsdb_kv_records *r);
+/* W:91-155 straight from the data files: scan, then bsdb_mph_build_index_*
+ * (hash, GOV build, ranks from the solve, index.db / index_a.db). */
+int bsdb_kv_build_index(bsdb_ctx *ctx, const char *kv_base, int partitions, int format, uint32_t block_size,
+                        int threads, uint32_t width, int approximate, const char *index_path,
+                        const char *index_a_path, bsdb_mph **out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -139,6 +139,40 @@ def test_c5_full_size_histogram_equals_oracle(ctx):
     np.testing.assert_array_equal(b_np, exp)
 
 
+@pytest.mark.timeout(900)
+def test_c5_full_build_one_gpu(ctx):
+    """C5 at its full size on ONE GPU: 4e9 variable-length keys (8-64 B Zipf,
+    ~103 GB with offsets), hash.checksum.bits = 16, the whole GOV structure and
+    index by sequential bucket-range passes; index slots to host memory.
+    Checked as C4: E[m] = n, the device's bijection check, checked lookups of
+    100 000 keys in 10 blocks == the oracle's on the exported structure (with
+    their 16 checksum bits), their index slots, no slot left empty."""
+    n, width, base, stride = 4_000_000_000, 16, 0x2000, 64
+    blob, off = ctx.gen_keys_var(0, n)
+    index = np.empty(n, np.uint64)
+    ctx.set_verify(True)
+    try:
+        E, vals, sb, used = ctx.mph_build_index_passes(blob, 0, n, width, 0, offsets=off, addr_base=base,
+                                                       addr_stride=stride, index=index)
+    finally:
+        ctx.set_verify(False)
+    del blob, off
+    hE, hv, hs = u64(E), u64(vals), u64(sb)
+    del E, vals, sb
+    torch.cuda.empty_cache()
+    assert int(hE[-1]) & ((1 << 56) - 1) == n
+    rng = np.random.default_rng(45)
+    for first in np.sort(rng.integers(0, n - 10_000, 10)):
+        first = int(first)
+        kb, ko = O.gen_keys_var(first, 10_000)
+        r = O.lookup_batch_mt(O.hash_var(kb, ko), n, hE, hv, width, hs, True, THREADS)
+        assert r.min() >= 0
+        exp = (np.uint64(base) + np.uint64(stride) * np.arange(first, first + 10_000, dtype=np.uint64)).byteswap()
+        np.testing.assert_array_equal(index[r], exp)
+    for lo in range(0, n, 1 << 30):
+        assert np.count_nonzero(index[lo: lo + (1 << 30)] == 0) == 0
+
+
 @pytest.mark.timeout(600)
 def test_c5_checksum16_build_on_a_sample(ctx):
     """cb = 16 (C5's hash.checksum.bits) on the first 2e6 C5 keys, device

@@ -1,0 +1,103 @@
+"""F3: the native kv.db scan (bsdb_kv_scan) over the two uncompressed layouts
+of the reference's data files -- host code, CPU only.  The expected records
+are the writer's own (bsdb_amd/kvfiles.py restates SimpleCompactKVWriter /
+BlockedKVWriter's layouts); the scan must return them in partition order
+(PartitionedKVWriter.forEach, one partition after another) with the
+addresses the reference's partitionForEach hands to buildIndex
+(SimpleCompactKVWriter.java:55-70, BlockedKVWriter.java:84-136)."""
+import os
+
+import numpy as np
+import pytest
+
+from bsdb_amd import kvfiles
+from bsdb_amd.native import BsdbError, kv_scan
+
+
+def records(n, seed, key_len=None, big_every=0):
+    rng = np.random.default_rng(seed)
+    klen = np.full(n, key_len) if key_len else rng.integers(1, 256, n)
+    vlen = rng.integers(1, 120, n)
+    if big_every:
+        vlen[::big_every] = rng.integers(4200, 9000, vlen[::big_every].size)
+    koff = np.zeros(n + 1, np.uint64)
+    koff[1:] = np.cumsum(klen)
+    voff = np.zeros(n + 1, np.uint64)
+    voff[1:] = np.cumsum(vlen)
+    kblob = rng.integers(0, 256, int(koff[-1]), dtype=np.uint8)
+    vblob = rng.integers(0, 256, int(voff[-1]), dtype=np.uint8)
+    return kblob, koff, vblob, voff
+
+
+def expected(kblob, koff, vblob, voff, addr, partitions):
+    """Records in scan order: partition by partition, each in file order
+    (a large record reaches the file before the block still being filled,
+    BlockedKVWriter.java:48-59)."""
+    n = koff.size - 1
+    per = []
+    for p in range(partitions):
+        idx = np.arange(p, n, partitions)
+        pos = ((addr[idx] >> np.uint64(16)) & np.uint64(0xFFFFFFFF)) * np.uint64(1 << 16) + (addr[idx] & np.uint64(0xFFFF))
+        per.append(idx[np.argsort(pos, kind="stable")])
+    order = np.concatenate(per).astype(np.int64)
+    keys = [kblob[int(koff[i]): int(koff[i + 1])].tobytes() for i in order]
+    heads = [vblob[int(voff[i]): int(min(voff[i + 1], voff[i] + 8))].tobytes() for i in order]
+    return order, keys, heads
+
+
+def check(scan, kblob, koff, vblob, voff, addr, partitions):
+    order, keys, heads = expected(kblob, koff, vblob, voff, addr, partitions)
+    off = scan["offsets"]
+    assert off.size == len(keys) + 1
+    got_keys = [scan["blob"][int(off[i]): int(off[i + 1])].tobytes() for i in range(len(keys))]
+    assert got_keys == keys
+    np.testing.assert_array_equal(scan["addr"], addr[order])
+    np.testing.assert_array_equal(scan["vlen"], [len(h) for h in heads])
+    np.testing.assert_array_equal(scan["value8"], [int.from_bytes(h, "little") for h in heads])
+
+
+@pytest.mark.parametrize("partitions", [1, 3, 8])
+def test_compact_layout(tmp_path, partitions):
+    kb, ko, vb, vo = records(20_000, 1)
+    base = str(tmp_path / "kv.db")
+    addr = kvfiles.write_compact(base, partitions, kb, ko, vb, vo)
+    s = kv_scan(base, partitions, 0, threads=4)
+    check(s, kb, ko, vb, vo, addr, partitions)
+    assert s["fixed_len"] == 0
+
+
+def test_compact_fixed_keys_and_empty_partitions(tmp_path):
+    kb, ko, vb, vo = records(5, 2, key_len=13)
+    base = str(tmp_path / "kv.db")
+    addr = kvfiles.write_compact(base, 8, kb, ko, vb, vo)   # partitions 5..7 stay empty
+    s = kv_scan(base, 8, 0)
+    check(s, kb, ko, vb, vo, addr, 8)
+    assert s["fixed_len"] == 13
+    assert os.path.getsize(base + ".7") == 0
+
+
+@pytest.mark.parametrize("block", [4096, 8192])
+def test_blocked_layout_with_large_records(tmp_path, block):
+    kb, ko, vb, vo = records(6_000, 3, big_every=97)
+    base = str(tmp_path / "kv.db")
+    addr = kvfiles.write_blocked(base, 3, kb, ko, vb, vo, block)
+    s = kv_scan(base, 3, 1, block, threads=2)
+    check(s, kb, ko, vb, vo, addr, 3)
+    # a record's address names its block (pages, position) and offset (BlockedKVWriter.java:124-136)
+    a = s["addr"]
+    assert set(((a >> np.uint64(48)) & np.uint64(0xFF)).tolist()) >= {block // 4096, 2, 3}
+
+
+def test_bad_inputs(tmp_path):
+    kb, ko, vb, vo = records(100, 4)
+    base = str(tmp_path / "kv.db")
+    kvfiles.write_compact(base, 1, kb, ko, vb, vo)
+    data = open(base + ".0", "rb").read()
+    open(base + ".0", "wb").write(data[:-5])  # a truncated record
+    with pytest.raises(BsdbError) as e:
+        kv_scan(base, 1, 0)
+    assert e.value.code == -9  # EFILE
+    with pytest.raises(BsdbError):
+        kv_scan(str(tmp_path / "missing.db"), 1, 0)
+    with pytest.raises(BsdbError):
+        kv_scan(base, 1, 1, 1000)  # block size not a multiple of 4096

@@ -21,10 +21,12 @@ def read_record(base, addr):
         return f.read(kl), f.read(vl)
 
 
-@pytest.mark.parametrize("approx,partitions,pass_cache,fused", [(False, 3, 8 * 40_000, False), (True, 1, 1 << 30, False),
-                                                                (True, 2, 0, False), (True, 2, 0, True),
-                                                                (False, 1, 0, True)])
-def test_build_and_read_back(tmp_path, approx, partitions, pass_cache, fused):
+@pytest.mark.parametrize("approx,partitions,pass_cache,fused,files", [
+    (False, 3, 8 * 40_000, False, False), (True, 1, 1 << 30, False, False), (True, 2, 0, False, False),
+    (True, 2, 0, True, False), (False, 1, 0, True, False), (True, 3, 0, True, True), (False, 4, 0, True, True)])
+def test_build_and_read_back(tmp_path, approx, partitions, pass_cache, fused, files):
+    """files: the index built from the data files through the native kv.db
+    scan (bsdb_kv_build_index, F3) instead of the records held in memory."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     from bsdb_amd.writer import BSDBWriter
@@ -34,7 +36,7 @@ def test_build_and_read_back(tmp_path, approx, partitions, pass_cache, fused):
     vals = [rng.integers(0, 256, int(rng.integers(1, 60)), dtype=np.uint8).tobytes() for _ in range(n)]
     base = str(tmp_path / "db")
     w = BSDBWriter(base, checksum_bits=4, pass_cache_size=pass_cache, approximate_mode=approx,
-                   partitions=partitions, fused_index=fused)
+                   partitions=partitions, fused_index=fused, from_files=files)
     for k, v in zip(keys[: n // 2], vals[: n // 2]):
         w.put(k, v)
     rest = keys[n // 2:]
@@ -124,6 +126,38 @@ def test_build_index_in_one_call_equals_the_pass_loop(tmp_path, var, approx, n):
         assert open(a, "rb").read() == open(b, "rb").read()
     assert os.path.getsize(ip1) == 8 * n and os.path.getsize(ap1) == (8 * n if approx else 0)
     m1.close(); m2.close(); ctx.close()
+
+
+@pytest.mark.parametrize("block", [4096, 8192])
+def test_kv_build_from_blocked_files(tmp_path, block):
+    """F3 over SimpleBlockedKVWriter's layout (large records included): the
+    scan's addresses land in index.db at each key's rank; read back through
+    the block address (BlockedKVWriter.java:124-136)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import oracle as O
+    from bsdb_amd import Context, kvfiles
+    n = 30_000
+    rng = np.random.default_rng(8)
+    kb, ko = O.gen_keys_var(5, n)
+    vals = [rng.integers(0, 256, int(rng.integers(1, 200)) if i % 53 else 5000, dtype=np.uint8).tobytes()
+            for i in range(n)]
+    vb, vo = kvfiles.pack_values(vals)
+    base = str(tmp_path / "kv.db")
+    addr = kvfiles.write_blocked(base, 3, kb, ko, vb, vo, block)
+    ctx = Context(0)
+    ip, ap = str(tmp_path / "index.db"), str(tmp_path / "index_a.db")
+    mph = ctx.kv_build_index(base, 3, 4, ip, ap, approximate=True, fmt=1, block_size=block)
+    r = mph.lookup_var(kb, ko, check=True)
+    assert np.array_equal(np.sort(r), np.arange(n))
+    idx = np.fromfile(ip, ">u8")
+    np.testing.assert_array_equal(idx[r], addr)
+    ia = np.fromfile(ap, np.uint8).reshape(n, 8)
+    for i in range(0, n, 211):
+        head = vals[i][:8]
+        assert ia[r[i]].tobytes() == head + bytes(8 - len(head))
+    mph.close()
+    ctx.close()
 
 
 def test_empty_key_set(tmp_path):
