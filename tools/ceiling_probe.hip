@@ -1,0 +1,111 @@
+// Ceiling probe for the headline (measurement tool, not product code): what
+// any histogram design for BASELINE C4 must at least spend on this chip.
+// At the C4 size (13 193 787 549 x 13 B = 171.5 GB resident):
+//   k16     every key byte read once, perfectly coalesced 16-B nontemporal
+//           loads, no compute: the HBM read ceiling of the key stream
+//   k13     the same bytes as each key's dword-aligned 16-B window (the
+//           production front end's load pattern)
+//   hash    k13's loads + SpookyHash-short (spooky.c tail case 13 + ShortEnd,
+//           seed 0) + the bucket multiplyHigh: the hash stage alone, with no
+//           histogram at all (a xor of the buckets keeps it live)
+// Each kernel is timed with HIP events (best of 3).  The keys are a fixed
+// byte pattern: the hash's cost does not depend on the values.
+//   hipcc --offload-arch=gfx950 -O3 -I bsdb_amd/csrc tools/ceiling_probe.hip -o tools/ceiling_probe
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+
+#include "spooky_dev.hpp"
+
+using namespace bsdb;
+typedef unsigned int u32x4a __attribute__((ext_vector_type(4), aligned(4)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int NT = 512, KPT = 16;
+
+__global__ __launch_bounds__(NT) void k16(const uint8_t *p, uint64_t nvec, uint32_t *out) {
+    uint32_t x = 0;
+    const uint64_t stride = (uint64_t)gridDim.x * NT * KPT;
+    for (uint64_t base = (uint64_t)blockIdx.x * NT * KPT; base < nvec; base += stride) {
+        u32x4 w[KPT];
+#pragma unroll
+        for (int j = 0; j < KPT; ++j) {
+            const uint64_t v = base + threadIdx.x + (uint64_t)j * NT;
+            w[j] = v < nvec ? __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(p) + v) : u32x4{0, 0, 0, 0};
+        }
+#pragma unroll
+        for (int j = 0; j < KPT; ++j) x ^= w[j].x ^ w[j].y ^ w[j].z ^ w[j].w;
+    }
+    if (x == 0x12345678u) out[threadIdx.x] = x;
+}
+
+template <bool HASH>
+__global__ __launch_bounds__(NT) void k13(const uint8_t *p, uint64_t nkeys, uint32_t mult, uint32_t *out) {
+    uint32_t x = 0;
+    const uint64_t stride = (uint64_t)gridDim.x * NT * KPT;
+    for (uint64_t base = (uint64_t)blockIdx.x * NT * KPT; base < nkeys; base += stride) {
+        u32x4a w[KPT];
+#pragma unroll
+        for (int j = 0; j < KPT; ++j) {
+            const uint64_t k = base + threadIdx.x + (uint64_t)j * NT;
+            const uint64_t byte = (k < nkeys ? k : 0) * 13;
+            w[j] = __builtin_nontemporal_load(reinterpret_cast<const u32x4a *>(p + (byte & ~3ULL)));
+        }
+#pragma unroll
+        for (int j = 0; j < KPT; ++j) {
+            const uint64_t k = base + threadIdx.x + (uint64_t)j * NT;
+            if (HASH) {
+                const uint32_t sh = (uint32_t)((k * 13) & 3) * 8;
+                W64 s0, s1;
+                spooky13_u(w[j].x, w[j].y, w[j].z, w[j].w, sh, 0, s0, s1);
+                x ^= bucket_of_w(s0, mult);
+            } else {
+                x ^= w[j].x ^ w[j].y ^ w[j].z ^ w[j].w;
+            }
+        }
+    }
+    if (x == 0x12345678u) out[threadIdx.x] = x;
+}
+
+int main(int argc, char **argv) {
+    const uint64_t n = argc > 1 ? strtoull(argv[1], nullptr, 10) : 13193787549ULL;
+    const uint64_t bytes = n * 13, m = n / 1500 + 1;
+    uint8_t *p = nullptr;
+    uint32_t *o = nullptr;
+    if (hipMalloc(&p, bytes + 64) != hipSuccess || hipMalloc(&o, 4096) != hipSuccess) {
+        fprintf(stderr, "allocation of %.1f GB failed\n", bytes / 1e9);
+        return 1;
+    }
+    (void)hipMemset(p, 0x5b, bytes + 64);
+    (void)hipDeviceSynchronize();
+    int cus = 256;
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
+    hipEvent_t a, b;
+    (void)hipEventCreate(&a);
+    (void)hipEventCreate(&b);
+    printf("{\"n_keys\": %llu, \"key_bytes\": %.1f, \"cus\": %d", (unsigned long long)n, bytes / 1e9, cus);
+    for (int kind = 0; kind < 3; ++kind) {
+        for (int per_cu : {2, 4, 8}) {
+            const int grid = cus * per_cu;
+            float best = 1e30f;
+            for (int rep = 0; rep < 4; ++rep) {
+                (void)hipEventRecord(a);
+                if (kind == 0) k16<<<grid, NT>>>(p, bytes / 16, o);
+                else if (kind == 1) k13<false><<<grid, NT>>>(p, n, (uint32_t)(2 * m), o);
+                else k13<true><<<grid, NT>>>(p, n, (uint32_t)(2 * m), o);
+                (void)hipEventRecord(b);
+                (void)hipEventSynchronize(b);
+                float ms = 0;
+                (void)hipEventElapsedTime(&ms, a, b);
+                if (rep && ms < best) best = ms;
+            }
+            const char *name = kind == 0 ? "k16" : kind == 1 ? "k13" : "hash";
+            printf(", \"%s_wg%d\": {\"ms\": %.3f, \"TBps\": %.3f, \"Gkeys_per_s\": %.1f, \"roofline_frac\": %.3f}", name,
+                   per_cu, best, bytes / best / 1e9, n / best / 1e6, bytes / best / 1e9 / 8.0);
+            fflush(stdout);
+        }
+    }
+    printf("}\n");
+    return hipGetLastError() == hipSuccess ? 0 : 2;
+}
