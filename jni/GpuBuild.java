@@ -60,4 +60,9 @@ public final class GpuBuild {
     public static native void indexPutFixed(long ix, long keys, int keyLen, long count, long addr, long value8, long vlen);
     public static native void indexEndPass(long ix);
     public static native void indexClose(long ix);
+    // F3: build() straight from the data files: native kv.db scan (compact = 0 / blocked = 1 layouts)
+    // + the one-call build; returns the MPHF handle (export it for hash.db as buildHash does)
+    public static native long kvBuildIndex(long ctx, String kvBase, int partitions, int format, int blockSize,
+                                           int threads, int checksumBits, boolean approximate, String indexPath,
+                                           String indexAPath);
 }

@@ -171,3 +171,12 @@ JNIEXPORT void JF(indexPutFixed)(JNIEnv *env, jclass c, jlong ix, jlong keys, ji
 }
 JNIEXPORT void JF(indexEndPass)(JNIEnv *env, jclass c, jlong ix) { CHECK(bsdb_index_end_pass(P(ix))); }
 JNIEXPORT void JF(indexClose)(JNIEnv *env, jclass c, jlong ix) { CHECK(bsdb_index_close(P(ix))); }
+JNIEXPORT jlong JF(kvBuildIndex)(JNIEnv *env, jclass c, jlong ctx, jstring kv, jint parts, jint fmt, jint bs,
+                                 jint threads, jint w, jboolean approx, jstring ip, jstring ap) {
+    const char *k = utf(env, kv), *i = utf(env, ip), *a = utf(env, ap);
+    bsdb_mph *m = NULL;
+    int rc = bsdb_kv_build_index(P(ctx), k, parts, fmt, (uint32_t)bs, threads, (uint32_t)w, approx, i, a, &m);
+    unutf(env, kv, k); unutf(env, ip, i); unutf(env, ap, a);
+    if (rc) { fail(env, rc); return 0; }
+    return (jlong)(intptr_t)m;
+}
