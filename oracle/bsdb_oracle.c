@@ -427,8 +427,9 @@ uint64_t bo_values_words(uint64_t n) { return (2 * (1 + ((n * 281) >> 8)) + 63) 
  * unpinned; validity is checked through the reference's mph.c lookup.     *
  *   1. peeling in rounds: every vertex of degree 1 at the start of a round *
  *      claims its edge, the smallest such vertex of an edge wins;          *
- *   2. the 2-core is oriented by greedy matching in edge order (first free *
- *      vertex e0,e1,e2) plus BFS augmenting paths in edge order;           *
+ *   2. the 2-core is oriented by greedy matching in edge order (the free   *
+ *      vertex with the fewest core edges still to come) plus BFS          *
+ *      augmenting paths in edge order;                                     *
  *   3. the core system (unknowns = core hinges, non-hinge vertices = 0) is *
  *      solved over F3 block by block on the SCCs of its dependency graph   *
  *      (Gauss-Jordan per block, columns in increasing edge order);         *
@@ -540,15 +541,22 @@ static int solve_bucket(const uint64_t *sig, uint32_t cnt, uint32_t nv, uint64_t
         rounds++;
     }
 
-    /* 2. orientation of the 2-core: greedy, then BFS augmenting paths */
+    /* 2. orientation of the 2-core: greedy, then BFS augmenting paths.  The
+     * greedy takes core edges in increasing order; each takes, among its free
+     * vertices, the one with the fewest core edges still to come (deg: the
+     * peel's degrees, decremented as edges pass; ties: first in the edge). */
     uint32_t ncore = 0;
     for (uint32_t k = 0; k < cnt; k++) {
         if (round_of[k] >= 0) continue;
         ncore++;
+        int32_t best = -1;
+        uint32_t bd = 0xFFFFFFFFu;
         for (int i = 0; i < 3; i++) {
             const uint32_t v = e[3 * k + i];
-            if (vowner[v] < 0) { vowner[v] = (int32_t)k; hinge[k] = (int32_t)v; break; }
+            if (vowner[v] < 0 && deg[v] < bd) { bd = deg[v]; best = (int32_t)v; }
         }
+        for (int i = 0; i < 3; i++) deg[e[3 * k + i]]--;
+        if (best >= 0) { vowner[best] = (int32_t)k; hinge[k] = best; }
     }
     for (uint32_t k0 = 0; k0 < cnt; k0++) {
         if (round_of[k0] >= 0 || hinge[k0] >= 0) continue;
