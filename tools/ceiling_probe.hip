@@ -8,6 +8,14 @@
 //   hash    k13's loads + SpookyHash-short (spooky.c tail case 13 + ShortEnd,
 //           seed 0) + the bucket multiplyHigh: the hash stage alone, with no
 //           histogram at all (a xor of the buckets keeps it live)
+//   lds     hash + ONE LDS atomic increment per key into a per-workgroup
+//           8192-counter table (bucket mod 8192): the cheapest on-chip count
+//           any histogram design needs, with no id exchange at all (a
+//           lower bound: the real 35 MB table fits no LDS)
+//   ldscf   the same count with a bank-conflict-free address (row = bucket
+//           bits, column = the lane: every lane of a wave on its own bank)
+//   ldsrtn  the random count with the returned old value used (ds_add_rtn,
+//           the pass-1 kernel's rank atomic)
 // Each kernel is timed with HIP events (best of 3).  The keys are a fixed
 // byte pattern: the hash's cost does not depend on the values.
 //   hipcc --offload-arch=gfx950 -O3 -I bsdb_amd/csrc tools/ceiling_probe.hip -o tools/ceiling_probe
@@ -40,8 +48,16 @@ __global__ __launch_bounds__(NT) void k16(const uint8_t *p, uint64_t nvec, uint3
     if (x == 0x12345678u) out[threadIdx.x] = x;
 }
 
-template <bool HASH>
+constexpr int LDS_BINS = 8192;
+
+// LDS: 0 none, 1 random ds_add, 2 conflict-free ds_add, 3 random ds_add_rtn
+template <bool HASH, int LDS = 0>
 __global__ __launch_bounds__(NT) void k13(const uint8_t *p, uint64_t nkeys, uint32_t mult, uint32_t *out) {
+    __shared__ uint32_t tab[LDS ? LDS_BINS : 1];
+    if (LDS) {
+        for (int i = threadIdx.x; i < LDS_BINS; i += NT) tab[i] = 0;
+        __syncthreads();
+    }
     uint32_t x = 0;
     const uint64_t stride = (uint64_t)gridDim.x * NT * KPT;
     for (uint64_t base = (uint64_t)blockIdx.x * NT * KPT; base < nkeys; base += stride) {
@@ -59,11 +75,24 @@ __global__ __launch_bounds__(NT) void k13(const uint8_t *p, uint64_t nkeys, uint
                 const uint32_t sh = (uint32_t)((k * 13) & 3) * 8;
                 W64 s0, s1;
                 spooky13_u(w[j].x, w[j].y, w[j].z, w[j].w, sh, 0, s0, s1);
-                x ^= bucket_of_w(s0, mult);
+                const uint32_t b = bucket_of_w(s0, mult);
+                if (LDS == 1) {
+                    if (k < nkeys) atomicAdd(&tab[b & (LDS_BINS - 1)], 1u);
+                } else if (LDS == 2) {
+                    if (k < nkeys) atomicAdd(&tab[((b >> 6) & (LDS_BINS / 64 - 1)) * 64 + (threadIdx.x & 63)], 1u);
+                } else if (LDS == 3) {
+                    if (k < nkeys) x += atomicAdd(&tab[b & (LDS_BINS - 1)], 1u);
+                } else {
+                    x ^= b;
+                }
             } else {
                 x ^= w[j].x ^ w[j].y ^ w[j].z ^ w[j].w;
             }
         }
+    }
+    if (LDS) {
+        __syncthreads();
+        for (int i = threadIdx.x; i < LDS_BINS; i += NT) x ^= tab[i] * (uint32_t)(i + 1);
     }
     if (x == 0x12345678u) out[threadIdx.x] = x;
 }
@@ -85,7 +114,7 @@ int main(int argc, char **argv) {
     (void)hipEventCreate(&a);
     (void)hipEventCreate(&b);
     printf("{\"n_keys\": %llu, \"key_bytes\": %.1f, \"cus\": %d", (unsigned long long)n, bytes / 1e9, cus);
-    for (int kind = 0; kind < 3; ++kind) {
+    for (int kind = 0; kind < 6; ++kind) {
         for (int per_cu : {2, 4, 8}) {
             const int grid = cus * per_cu;
             float best = 1e30f;
@@ -93,14 +122,17 @@ int main(int argc, char **argv) {
                 (void)hipEventRecord(a);
                 if (kind == 0) k16<<<grid, NT>>>(p, bytes / 16, o);
                 else if (kind == 1) k13<false><<<grid, NT>>>(p, n, (uint32_t)(2 * m), o);
-                else k13<true><<<grid, NT>>>(p, n, (uint32_t)(2 * m), o);
+                else if (kind == 2) k13<true><<<grid, NT>>>(p, n, (uint32_t)(2 * m), o);
+                else if (kind == 3) k13<true, 1><<<grid, NT>>>(p, n, (uint32_t)(2 * m), o);
+                else if (kind == 4) k13<true, 2><<<grid, NT>>>(p, n, (uint32_t)(2 * m), o);
+                else k13<true, 3><<<grid, NT>>>(p, n, (uint32_t)(2 * m), o);
                 (void)hipEventRecord(b);
                 (void)hipEventSynchronize(b);
                 float ms = 0;
                 (void)hipEventElapsedTime(&ms, a, b);
                 if (rep && ms < best) best = ms;
             }
-            const char *name = kind == 0 ? "k16" : kind == 1 ? "k13" : "hash";
+            const char *name = kind == 0 ? "k16" : kind == 1 ? "k13" : kind == 2 ? "hash" : kind == 3 ? "lds" : kind == 4 ? "ldscf" : "ldsrtn";
             printf(", \"%s_wg%d\": {\"ms\": %.3f, \"TBps\": %.3f, \"Gkeys_per_s\": %.1f, \"roofline_frac\": %.3f}", name,
                    per_cu, best, bytes / best / 1e9, n / best / 1e6, bytes / best / 1e9 / 8.0);
             fflush(stdout);
