@@ -768,6 +768,22 @@ static uint32_t grid_for(const bsdb_ctx *c, uint64_t n) {
 // ---- GOV build on the device (A5, A6, A8, A11) -------------------------------
 uint64_t bsdb_values_words(uint64_t n) { return (2 * (1 + ((n * 281) >> 8)) + 63) / 64; }
 
+// SolveArgs::spec from BSDB_GOV_SPEC = "K[,P]": at most K seeds of a bucket in
+// flight before a speculating workgroup adds one (0: no limit), P = 1: the
+// speculative attempts at a lower wave priority.  Default K = 2: at C1 (667
+// buckets on 512 workgroups) the solve takes 5.1 ms against 6.4 ms with no
+// limit (every extra seed in flight shares a CU with the attempt that decides
+// its bucket); the priority did not help (6.6 ms).
+static uint32_t gov_spec_policy() {
+    uint32_t spec = 2;
+    if (const char *v = getenv("BSDB_GOV_SPEC")) {
+        const int k = atoi(v);
+        spec = (uint32_t)std::max(0, std::min(k, 255));
+        if (const char *c = strchr(v, ','); c && atoi(c + 1)) spec |= 0x100u;
+    }
+    return spec;
+}
+
 static void print_gov_profile(const std::vector<uint64_t> &h, uint32_t solve_grid, uint64_t m) {
     const char *names[GP_N] = {"edges", "peel", "greedy", "bfs", "tarjan", "singletons", "dense", "back",
                                "store", "n_seeds", "n_bfs", "n_bfs_pops", "n_dense_rows", "n_dense_max",
@@ -943,7 +959,8 @@ static int gov_build_impl(bsdb_ctx *c, const GovSrc &src, uint64_t n_global, uin
     // A8, with A11 (checksum bits at each rank), F2 (ranks) and A13 (index
     // slots) in the solve
     SolveArgs sa{sorted, b_hi, d_E, d_values, (uint64_t *)c->g_scratch, status, d_prof, fvs_max, b_lo, e_lo,
-                 d_sigbits, width, pay, d_rank, ixo.index, ixo.idx_lo, ixo.addr, ixo.addr_base, ixo.addr_stride, led};
+                 d_sigbits, width, pay, d_rank, ixo.index, ixo.idx_lo, ixo.addr, ixo.addr_base, ixo.addr_stride, led,
+                 gov_spec_policy()};
     // zeroing status[2] (the bucket queue) above happens before both launches
     k_gov_solve<<<solve_grid, GS_THREADS, 0, s>>>(sa);  // A8
     if (nbig)

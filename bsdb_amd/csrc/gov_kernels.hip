@@ -260,6 +260,11 @@ struct SolveArgs {
     // seeds of buckets still being solved; the bucket's seed is still the
     // first one that solves it (GOV:425-432)
     SeedLedger led;
+    // speculation policy: bits 0-7 = most seeds of one bucket in flight at
+    // once for a speculating workgroup to add one (0 = no limit); bit 8 =
+    // speculative attempts at a lower wave priority than a workgroup's own
+    // bucket (BSDB_GOV_SPEC)
+    uint32_t spec;
 };
 
 
@@ -1786,18 +1791,31 @@ __global__ __launch_bounds__(GS_THREADS, GS_THREADS * GS_PER_CU / 256) void k_go
                 if (sd < 256) lb = q;
             }
             // 3. the next seed of a bucket another workgroup still solves
+            // (with fewer than spec & 0xFF of its seeds in flight)
+            const uint32_t cap = a.spec & 0xFFu;
             for (uint32_t k = 0; lb == 0xFFFFFFFFu && !queue_open && k < gridDim.x; ++k) {
                 const uint32_t o = ld_agent(g.active + (blockIdx.x + k) % gridDim.x);
                 if (o == 0xFFFFFFFFu || ld_agent(g.done + o) || ld_agent(g.won + o)) continue;
+                if (cap) {
+                    const uint32_t cl = ld_agent(g.claim + o);
+                    uint32_t nf = 0;
+                    for (uint32_t w = 0; w * 64 < cl && w < 4; ++w) nf += (uint32_t)__builtin_popcountll(ld_agent64(g.fail + 4 * (size_t)o + w));
+                    if (cl - nf >= cap) continue;
+                }
                 sd = atomicAdd(g.claim + o, 1u);
                 if (sd < 256) lb = o;
             }
             sh_lb = lb;
             sh_s = sd;
+            sh_win = lb != cur;  // (a speculative attempt)
         }
         __syncthreads();
         const uint32_t lb = sh_lb, sd = sh_s;
         if (lb == 0xFFFFFFFFu) break;
+        if (a.spec & 0x100u) {
+            if (sh_win) __builtin_amdgcn_s_setprio(0);
+            else __builtin_amdgcn_s_setprio(2);
+        }
         const uint64_t b = a.b0 + lb;
         const uint64_t lo = a.E[b] & OFFSET_MASK, hi = a.E[b + 1] & OFFSET_MASK;
         const uint32_t cnt = (uint32_t)(hi - lo);
