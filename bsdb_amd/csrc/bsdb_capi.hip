@@ -869,6 +869,9 @@ static int gov_build_impl(bsdb_ctx *c, const GovSrc &src, uint64_t n_global, uin
                 counts, nullptr, nullptr, nullptr};
     if (from_keys) {
         if (src.n) launch_sel<0>(c, src, sel, s);
+    } else if (src.n && nb <= SMALL_NB) {
+        k_bucket_count_small<<<(uint32_t)((src.n + SMALL_CHUNK - 1) / SMALL_CHUNK), 256, 0, s>>>(src.sig, src.n, mult, (uint32_t)b_lo,
+                                                                                               (uint32_t)nb, counts);
     } else if (src.n) {
         k_bucket_count<<<grid_for(c, src.n), 256, 0, s>>>(src.sig, src.n, mult, (uint32_t)b_lo, counts);
     }
@@ -903,6 +906,9 @@ static int gov_build_impl(bsdb_ctx *c, const GovSrc &src, uint64_t n_global, uin
         sel.sorted = sorted;
         sel.pay = pay;
         if (src.n) launch_sel<1>(c, src, sel, s);
+    } else if (n_local && nb <= SMALL_NB) {
+        k_bucket_scatter_small<<<(uint32_t)((n_local + SMALL_CHUNK - 1) / SMALL_CHUNK), 256, 0, s>>>(
+            src.sig, n_local, mult, (uint32_t)b_lo, (uint32_t)nb, (unsigned long long *)c->g_cursor, sorted, pay);
     } else if (n_local) {
         k_bucket_scatter<<<grid_for(c, n_local), 256, 0, s>>>(src.sig, n_local, mult, (uint32_t)b_lo,
                                                               (unsigned long long *)c->g_cursor, sorted, pay);
