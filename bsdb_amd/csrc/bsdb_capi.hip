@@ -79,6 +79,11 @@ struct bsdb_ctx {
     size_t g_pay_bytes = 0;
     void *g_led = nullptr;  // the solver's seed ledger (SeedLedger)
     size_t g_led_bytes = 0;
+    void *g_mid = nullptr;  // mid-size ranges: per-workgroup counts (u16) and bases (u32)
+    size_t g_mid_bytes = 0;
+    // the oversized buckets' solver runs on its own stream beside k_gov_solve
+    hipStream_t big_stream = nullptr;
+    hipEvent_t big_ev[2] = {nullptr, nullptr};  // [0] inputs ready on s, [1] big solve done
     bool verify = false;
     // ordering of workspace use across streams: the last call's
     // completion event and stream
@@ -582,6 +587,10 @@ int bsdb_close(bsdb_ctx *c) {
         if (f.done) (void)hipEventDestroy(f.done);
     }
     if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
+    if (c->big_stream) (void)hipStreamSynchronize(c->big_stream);
+    for (hipEvent_t e : c->big_ev)
+        if (e) (void)hipEventDestroy(e);
+    if (c->big_stream) (void)hipStreamDestroy(c->big_stream);
     (void)hipFree(c->d_out);
     (void)hipFree(c->g_sorted);
     (void)hipFree(c->g_counts);
@@ -591,6 +600,7 @@ int bsdb_close(bsdb_ctx *c) {
     (void)hipFree(c->g_big);
     (void)hipFree(c->g_pay);
     (void)hipFree(c->g_led);
+    (void)hipFree(c->g_mid);
     (void)hipFree(c->g_slabs);
     (void)hipFree(c->pack);
     comm_destroy(c);
@@ -857,21 +867,38 @@ static int gov_build_impl(bsdb_ctx *c, const GovSrc &src, uint64_t n_global, uin
     const uint32_t mult = (uint32_t)(2 * m);
     const bool from_keys = src.sig == nullptr;
     int rc;
-    if ((rc = grow(&c->g_counts, &c->g_counts_bytes, std::max<uint64_t>(nb, 1) * 4))) return rc;
+    if ((rc = grow(&c->g_counts, &c->g_counts_bytes, (nb + 1) * 4))) return rc;  // (+1: k_bucket_count_mid's flag)
     if ((rc = grow(&c->g_cursor, &c->g_cursor_bytes, std::max<uint64_t>(nb, 1) * 8))) return rc;
     if ((rc = grow(&c->g_status, &c->g_status_bytes, 16))) return rc;
     uint32_t *counts = (uint32_t *)c->g_counts, *status = (uint32_t *)c->g_status;
-    HIP_OK(hipMemsetAsync(counts, 0, std::max<uint64_t>(nb, 1) * 4, s));
+    HIP_OK(hipMemsetAsync(counts, 0, (nb + 1) * 4, s));
     HIP_OK(hipMemsetAsync(status, 0, 16, s));
     if (full) HIP_OK(hipMemsetAsync(d_values, 0, bsdb_values_words(n_global) * 8, s));
     uint64_t *Eb = d_E + b_lo;
     SelArgs sel{src.keys, src.off, src.blob_bytes, src.n, src.key_len, mult, (uint32_t)b_lo, (uint32_t)nb,
                 counts, nullptr, nullptr, nullptr};
+    // mid-size ranges from signatures: per-workgroup counts and bases, no
+    // per-key global atomics (k_bucket_count_mid)
+    const bool mid = !from_keys && src.n && nb > SMALL_NB && nb <= MID_NB && src.n < (1ULL << 32);
+    const uint32_t mid_g = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)c->num_cus, src.n / 65536));
+    uint16_t *mid_cw = nullptr;
+    uint32_t *mid_base = nullptr;
+    if (mid) {
+        const size_t cw_bytes = ((size_t)mid_g * nb * 2 + 255) & ~(size_t)255;
+        if ((rc = grow(&c->g_mid, &c->g_mid_bytes, cw_bytes + (size_t)mid_g * nb * 4))) return rc;
+        mid_cw = (uint16_t *)c->g_mid;
+        mid_base = (uint32_t *)((uint8_t *)c->g_mid + cw_bytes);
+    }
     if (from_keys) {
         if (src.n) launch_sel<0>(c, src, sel, s);
     } else if (src.n && nb <= SMALL_NB) {
         k_bucket_count_small<<<(uint32_t)((src.n + SMALL_CHUNK - 1) / SMALL_CHUNK), 256, 0, s>>>(src.sig, src.n, mult, (uint32_t)b_lo,
                                                                                                (uint32_t)nb, counts);
+    } else if (mid) {
+        k_bucket_count_mid<<<mid_g, MID_THREADS, 0, s>>>(src.sig, src.n, mult, (uint32_t)b_lo, (uint32_t)nb, mid_cw,
+                                                         counts + nb);
+        k_mid_colsum<<<(uint32_t)((nb + 255) / 256), 256, 0, s>>>(mid_cw, mid_g, (uint32_t)nb, counts);
+        k_bucket_count_redo<<<1, 256, 0, s>>>(src.sig, src.n, mult, (uint32_t)b_lo, (uint32_t)nb, counts, counts + nb);
     } else if (src.n) {
         k_bucket_count<<<grid_for(c, src.n), 256, 0, s>>>(src.sig, src.n, mult, (uint32_t)b_lo, counts);
     }
@@ -906,6 +933,10 @@ static int gov_build_impl(bsdb_ctx *c, const GovSrc &src, uint64_t n_global, uin
         sel.sorted = sorted;
         sel.pay = pay;
         if (src.n) launch_sel<1>(c, src, sel, s);
+    } else if (mid) {
+        k_mid_colscan<<<(uint32_t)((nb + 255) / 256), 256, 0, s>>>(mid_cw, mid_g, (uint32_t)nb, Eb, e_lo, mid_base);
+        k_bucket_scatter_mid<<<mid_g, MID_THREADS, 0, s>>>(src.sig, n_local, mult, (uint32_t)b_lo, (uint32_t)nb, mid_base,
+                                                           counts + nb, (unsigned long long *)c->g_cursor, sorted, pay);
     } else if (n_local && nb <= SMALL_NB) {
         k_bucket_scatter_small<<<(uint32_t)((n_local + SMALL_CHUNK - 1) / SMALL_CHUNK), 256, 0, s>>>(
             src.sig, n_local, mult, (uint32_t)b_lo, (uint32_t)nb, (unsigned long long *)c->g_cursor, sorted, pay);
@@ -967,11 +998,24 @@ static int gov_build_impl(bsdb_ctx *c, const GovSrc &src, uint64_t n_global, uin
     SolveArgs sa{sorted, b_hi, d_E, d_values, (uint64_t *)c->g_scratch, status, d_prof, fvs_max, b_lo, e_lo,
                  d_sigbits, width, pay, d_rank, ixo.index, ixo.idx_lo, ixo.addr, ixo.addr_base, ixo.addr_stride, led,
                  gov_spec_policy()};
-    // zeroing status[2] (the bucket queue) above happens before both launches
+    // zeroing status[2] (the bucket queue) above happens before both launches.
+    // The oversized buckets (C2: ~3 of 66 667, 2.8 ms of one workgroup each)
+    // are solved on a stream of their own, queued first, so their few
+    // workgroups run beside k_gov_solve's instead of after them (they touch
+    // other buckets; shared value words and checksum words are OR-ed).
+    if (nbig) {
+        if (!c->big_stream) {
+            HIP_OK(hipStreamCreateWithFlags(&c->big_stream, hipStreamNonBlocking));
+            for (hipEvent_t &e : c->big_ev) HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        }
+        HIP_OK(hipEventRecord(c->big_ev[0], s));
+        HIP_OK(hipStreamWaitEvent(c->big_stream, c->big_ev[0], 0));
+        k_gov_solve_big<<<big_grid, GS_THREADS, 0, c->big_stream>>>(sa, (const uint32_t *)c->g_big, nbig,
+                                                                    (uint8_t *)c->g_slabs, big_slab_bytes());
+        HIP_OK(hipEventRecord(c->big_ev[1], c->big_stream));
+    }
     k_gov_solve<<<solve_grid, GS_THREADS, 0, s>>>(sa);  // A8
-    if (nbig)
-        k_gov_solve_big<<<big_grid, GS_THREADS, 0, s>>>(sa, (const uint32_t *)c->g_big, nbig, (uint8_t *)c->g_slabs,
-                                                        big_slab_bytes());
+    if (nbig) HIP_OK(hipStreamWaitEvent(s, c->big_ev[1], 0));
     if (gprof) {
         std::vector<uint64_t> h((size_t)solve_grid * GP_N);
         HIP_OK(hipMemcpyAsync(h.data(), d_prof, h.size() * 8, hipMemcpyDeviceToHost, s));

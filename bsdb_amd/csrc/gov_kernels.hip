@@ -151,54 +151,213 @@ __global__ __launch_bounds__(256) void k_bucket_scatter_small(const uint64_t *si
     }
 }
 
+// Mid-size ranges (SMALL_NB < nb <= MID_NB, C2: 66 667 buckets), with no
+// per-key global atomics (1e8 of them on random addresses: 4.1 ms for the
+// count, 6.9 ms with the scatter's stores at C2):
+//  1. k_bucket_count_mid: g workgroups (one per CU) each count their keys
+//     (a fixed grid-stride share) into 16-bit LDS counters (two per word,
+//     the whole range in 160 KB) and store them as cw[w][b];
+//  2. k_mid_colsum: counts[b] = sum over w of cw[w][b];
+//  3. (the offsets scan: E)
+//  4. k_mid_colscan: base[w][b] = E[b] - e0 + sum over w' < w of cw[w'][b];
+//  5. k_bucket_scatter_mid: the same workgroups, the same shares, place each
+//     key at base[w][b] + its LDS rank among w's keys of bucket b.
+// Positions are then a function of the input alone.  A counter that reaches
+// 0x8000 in one workgroup (an adversarial set; random keys put ~3 per bucket
+// in a share) raises *flag before its half could carry into its neighbour:
+// k_bucket_count_redo then recounts with per-key atomics and the scatter
+// falls back to cursor atomics.
+constexpr uint32_t MID_NB = 80000, MID_THREADS = 1024;
+
+__global__ __launch_bounds__(MID_THREADS) void k_bucket_count_mid(const uint64_t *sig, uint64_t n, uint32_t mult,
+                                                                  uint32_t b0, uint32_t nb, uint16_t *cw,
+                                                                  uint32_t *flag) {
+    __shared__ uint32_t c2[MID_NB / 2];
+    const uint32_t nw = (nb + 1) / 2;
+    for (uint32_t i = threadIdx.x; i < nw; i += MID_THREADS) c2[i] = 0;
+    __syncthreads();
+    bool over = false;
+    const uint64_t stride = (uint64_t)gridDim.x * MID_THREADS;
+    for (uint64_t i = (uint64_t)blockIdx.x * MID_THREADS + threadIdx.x; i < n; i += stride) {
+        const uint32_t b = bucket_of_w(w64(sig[2 * i]), mult) - b0, sh = (b & 1) * 16;
+        const uint32_t old = atomicAdd(&c2[b >> 1], 1u << sh);
+        over |= ((old >> sh) & 0xFFFFu) >= 0x7FFFu;
+    }
+    if (over) atomicOr(flag, 1u);
+    __syncthreads();
+    uint16_t *row = cw + (size_t)blockIdx.x * nb;
+    for (uint32_t b = threadIdx.x; b < nb; b += MID_THREADS) row[b] = (uint16_t)(c2[b >> 1] >> ((b & 1) * 16));
+}
+
+__global__ __launch_bounds__(256) void k_mid_colsum(const uint16_t *cw, uint32_t g, uint32_t nb, uint32_t *counts) {
+    const uint32_t b = blockIdx.x * 256 + threadIdx.x;
+    if (b >= nb) return;
+    uint32_t t = 0;
+    for (uint32_t w = 0; w < g; ++w) t += cw[(size_t)w * nb + b];
+    counts[b] = t;
+}
+
+__global__ __launch_bounds__(256) void k_mid_colscan(const uint16_t *cw, uint32_t g, uint32_t nb, const uint64_t *Eb,
+                                                     uint64_t e0, uint32_t *base) {
+    const uint32_t b = blockIdx.x * 256 + threadIdx.x;
+    if (b >= nb) return;
+    uint32_t run = (uint32_t)((Eb[b] & OFFSET_MASK) - e0);
+    for (uint32_t w = 0; w < g; ++w) {
+        base[(size_t)w * nb + b] = run;
+        run += cw[(size_t)w * nb + b];
+    }
+}
+
+__global__ __launch_bounds__(256) void k_bucket_count_redo(const uint64_t *sig, uint64_t n, uint32_t mult, uint32_t b0,
+                                                           uint32_t nb, uint32_t *counts, const uint32_t *flag) {
+    if (*flag == 0) return;  // (the normal case: nothing to do)
+    // one workgroup clears, then counts (a grid-wide order one launch cannot give)
+    if (blockIdx.x != 0) return;
+    for (uint32_t b = threadIdx.x; b < nb; b += 256) counts[b] = 0;
+    __syncthreads();
+    for (uint64_t i = threadIdx.x; i < n; i += 256) atomicAdd(counts + (bucket_of_w(w64(sig[2 * i]), mult) - b0), 1u);
+}
+
+__global__ __launch_bounds__(MID_THREADS) void k_bucket_scatter_mid(const uint64_t *sig, uint64_t n, uint32_t mult,
+                                                                    uint32_t b0, uint32_t nb, const uint32_t *base,
+                                                                    const uint32_t *flag, unsigned long long *cursor,
+                                                                    uint64_t *out, uint64_t *pay_out) {
+    __shared__ uint32_t c2[MID_NB / 2];
+    const uint64_t stride = (uint64_t)gridDim.x * MID_THREADS;
+    if (*flag) {  // (uniform) the counts were redone: per-key cursor atomics
+        for (uint64_t i = (uint64_t)blockIdx.x * MID_THREADS + threadIdx.x; i < n; i += stride) {
+            const ulonglong2 s = reinterpret_cast<const ulonglong2 *>(sig)[i];
+            const uint64_t pos = atomicAdd(cursor + (bucket_of_w(w64(s.x), mult) - b0), 1ULL);
+            reinterpret_cast<ulonglong2 *>(out)[pos] = s;
+            if (pay_out) pay_out[pos] = i;
+        }
+        return;
+    }
+    const uint32_t nw = (nb + 1) / 2;
+    for (uint32_t i = threadIdx.x; i < nw; i += MID_THREADS) c2[i] = 0;
+    __syncthreads();
+    const uint32_t *bw = base + (size_t)blockIdx.x * nb;
+    for (uint64_t i = (uint64_t)blockIdx.x * MID_THREADS + threadIdx.x; i < n; i += stride) {
+        const ulonglong2 s = reinterpret_cast<const ulonglong2 *>(sig)[i];
+        const uint32_t b = bucket_of_w(w64(s.x), mult) - b0, sh = (b & 1) * 16;
+        const uint32_t rk = (atomicAdd(&c2[b >> 1], 1u << sh) >> sh) & 0xFFFFu;
+        const uint64_t pos = (uint64_t)bw[b] + rk;
+        reinterpret_cast<ulonglong2 *>(out)[pos] = s;
+        if (pay_out) pay_out[pos] = i;
+    }
+}
+
 __device__ __forceinline__ bool sig_less(ulonglong2 a, ulonglong2 b) { return a.x < b.x || (a.x == b.x && a.y < b.y); }
 
-// Bitonic sort of one bucket in LDS (padded with all-ones sentinels) +
-// duplicate check on neighbours (CBHS:969-972).
+// Sort of one bucket (<= GS_CMAX keys) by unsigned (sig0, sig1) + duplicate
+// check on neighbours (CBHS:969-972).  A bucket's sig0 are spread evenly over
+// its slice of the 64-bit range (bucket = the high part of sig0 * 2m), so a
+// counting sort on the top 11 bits of sig0 - min(sig0) puts ~0.8 keys in each
+// of 2 048 sub-bins; each sub-bin is then insertion-sorted by one thread.  A
+// handful of barriers per bucket instead of the 66 stages of a padded bitonic
+// sort (10.4 ms at C2, bound by its LDS traffic).  Keys in registers (7 per
+// thread), the placed keys in LDS: 48 KB, 3 workgroups per CU.  Adversarial
+// sets (many keys in one sub-bin) only make that sub-bin's insertion slower.
 __global__ __launch_bounds__(256) void k_bucket_sort(uint64_t *sig, const uint64_t *Eb, uint64_t nb, uint64_t e0,
                                                      uint32_t *status, uint64_t *pay) {
-    constexpr int P2MAX = 1 << (32 - __builtin_clz(GS_CMAX - 1));  // the bitonic sort pads to a power of 2
-    __shared__ ulonglong2 s[P2MAX];
-    __shared__ uint64_t sp[P2MAX];  // payloads (pay != nullptr), moved with their signatures
+    constexpr uint32_t KPT = (GS_CMAX + 255) / 256, NBIN = 2048, BPT = NBIN / 256;
+    __shared__ ulonglong2 o[GS_CMAX];
+    __shared__ uint64_t op[GS_CMAX];  // payloads (pay != nullptr), moved with their signatures
+    __shared__ uint32_t bin_off[NBIN + 1];
+    __shared__ unsigned long long mn_mx[2];
+    __shared__ uint32_t wsum[4];
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     for (uint64_t b = blockIdx.x; b < nb; b += gridDim.x) {
         const uint64_t lo = (Eb[b] & OFFSET_MASK) - e0, hi = (Eb[b + 1] & OFFSET_MASK) - e0;
         const uint32_t cnt = (uint32_t)(hi - lo);
         if (cnt > GS_CMAX) continue;  // k_bucket_sort_big
-        uint32_t p2 = 1;
-        while (p2 < cnt) p2 <<= 1;
+        if (cnt < 2) continue;        // (uniform) nothing to order
         ulonglong2 *g = reinterpret_cast<ulonglong2 *>(sig) + lo;
-        __syncthreads();
-        for (uint32_t i = threadIdx.x; i < p2; i += 256) {
-            s[i] = i < cnt ? g[i] : make_ulonglong2(~0ULL, ~0ULL);
-            if (pay) sp[i] = i < cnt ? pay[lo + i] : 0u;
+        __syncthreads();  // (the previous bucket's LDS reads are done)
+        for (uint32_t i = tid; i < NBIN; i += 256) bin_off[i] = 0;
+        if (tid == 0) {
+            mn_mx[0] = ~0ULL;
+            mn_mx[1] = 0;
         }
-        __syncthreads();
-        for (uint32_t k = 2; k <= p2; k <<= 1) {
-            for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-                for (uint32_t i = threadIdx.x; i < p2; i += 256) {
-                    const uint32_t l = i ^ j;
-                    if (l > i) {
-                        const ulonglong2 a = s[i], c = s[l];
-                        const bool up = (i & k) == 0;
-                        if (up ? sig_less(c, a) : sig_less(a, c)) {
-                            s[i] = c;
-                            s[l] = a;
-                            if (pay) {
-                                const uint64_t t = sp[i];
-                                sp[i] = sp[l];
-                                sp[l] = t;
-                            }
-                        }
-                    }
-                }
-                __syncthreads();
+        ulonglong2 v[KPT];
+        uint64_t pv[KPT];
+        unsigned long long lmn = ~0ULL, lmx = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < KPT; ++j) {
+            const uint32_t i = tid + 256 * j;
+            v[j] = i < cnt ? g[i] : make_ulonglong2(0, 0);
+            pv[j] = i < cnt && pay ? pay[lo + i] : 0;
+            if (i < cnt) {
+                lmn = min(lmn, (unsigned long long)v[j].x);
+                lmx = max(lmx, (unsigned long long)v[j].x);
             }
         }
+        __syncthreads();
+        atomicMin(&mn_mx[0], lmn);
+        atomicMax(&mn_mx[1], lmx);
+        __syncthreads();
+        const uint64_t mn = mn_mx[0], span = mn_mx[1] - mn;
+        const uint32_t bits = span ? 64u - (uint32_t)__builtin_clzll(span) : 0u;  // span < 2^bits
+        const uint32_t shift = bits > 11 ? bits - 11 : 0;                      // (x - mn) >> shift < 2048
+        uint32_t rk[KPT];
+#pragma unroll
+        for (uint32_t j = 0; j < KPT; ++j)
+            if (tid + 256 * j < cnt) rk[j] = atomicAdd(&bin_off[(uint32_t)((v[j].x - mn) >> shift)], 1u);
+        __syncthreads();
+        // exclusive scan of the 2 048 sub-bin counts: BPT per thread, then the waves
+        uint32_t loc[BPT], tot = 0;
+#pragma unroll
+        for (uint32_t q = 0; q < BPT; ++q) {
+            loc[q] = tot;
+            tot += bin_off[tid * BPT + q];
+        }
+        uint32_t inc = tot;
+#pragma unroll
+        for (uint32_t d = 1; d < 64; d <<= 1) {
+            const uint32_t y = (uint32_t)__shfl_up((int)inc, d, 64);
+            if (lane >= d) inc += y;
+        }
+        if (lane == 63) wsum[wave] = inc;
+        __syncthreads();
+        uint32_t wbase = 0;
+        for (uint32_t w = 0; w < wave; ++w) wbase += wsum[w];
+        const uint32_t base = wbase + inc - tot;
+#pragma unroll
+        for (uint32_t q = 0; q < BPT; ++q) bin_off[tid * BPT + q] = base + loc[q];
+        if (tid == 0) bin_off[NBIN] = cnt;
+        __syncthreads();
+#pragma unroll
+        for (uint32_t j = 0; j < KPT; ++j)
+            if (tid + 256 * j < cnt) {
+                const uint32_t p = bin_off[(uint32_t)((v[j].x - mn) >> shift)] + rk[j];
+                o[p] = v[j];
+                if (pay) op[p] = pv[j];
+            }
+        __syncthreads();
+        // each sub-bin in order (insertion sort); equal neighbours are duplicates
         bool dup = false;
-        for (uint32_t i = threadIdx.x; i < cnt; i += 256) {
-            g[i] = s[i];
-            if (pay) pay[lo + i] = sp[i];
-            if (i && s[i].x == s[i - 1].x && s[i].y == s[i - 1].y) dup = true;
+#pragma unroll
+        for (uint32_t q = 0; q < BPT; ++q) {
+            const uint32_t a0 = bin_off[tid * BPT + q], a1 = bin_off[tid * BPT + q + 1];
+            for (uint32_t x = a0 + 1; x < a1; ++x) {
+                const ulonglong2 key = o[x];
+                const uint64_t kp = pay ? op[x] : 0;
+                uint32_t y = x;
+                while (y > a0 && sig_less(key, o[y - 1])) {
+                    o[y] = o[y - 1];
+                    if (pay) op[y] = op[y - 1];
+                    --y;
+                }
+                o[y] = key;
+                if (pay) op[y] = kp;
+            }
+            for (uint32_t x = a0 + 1; x < a1; ++x)
+                if (o[x].x == o[x - 1].x && o[x].y == o[x - 1].y) dup = true;
+        }
+        __syncthreads();
+        for (uint32_t i = tid; i < cnt; i += 256) {
+            g[i] = o[i];
+            if (pay) pay[lo + i] = op[i];
         }
         if (dup) atomicOr(status, (uint32_t)GOV_DUP);
     }

@@ -9,6 +9,7 @@ import numpy as np
 import pytest
 
 import oracle as O
+from bsdb_amd.native import BsdbError
 
 pytestmark = pytest.mark.gpu
 
@@ -223,6 +224,37 @@ def test_oversized_bucket_matches_oracle(ctx, n_total, big):
     np.testing.assert_array_equal(u64(E_d), E)
     np.testing.assert_array_equal(u64(v_d), vals)
     np.testing.assert_array_equal(u64(s_d)[: sb.size], sb)
+
+
+def test_mid_range_count_matches_oracle(ctx):
+    """7e6 keys: 4 667 buckets, counted by the 16-bit LDS counters of
+    k_bucket_count_mid (SMALL_NB < m <= MID_NB); output bit-identical."""
+    n = 7_000_000
+    keys = O.gen_keys13(41, n)
+    sig = O.hash_fixed_mt(keys, 13, THREADS)
+    rc, E, vals, sb, _ = O.gov_build_mt(sig, 4, THREADS)
+    assert rc == 0
+    E_d, v_d, s_d = ctx.gov_build(dev(sig.view(np.int64)), 4)
+    np.testing.assert_array_equal(u64(E_d), E)
+    np.testing.assert_array_equal(u64(v_d), vals)
+    np.testing.assert_array_equal(u64(s_d)[: sb.size], sb)
+
+
+def test_mid_range_counter_overflow_is_recounted(ctx):
+    """Every signature in bucket 0 of m = 4 135: each counting workgroup sees
+    far more than 0x7FFF keys of one bucket, raises the overflow flag, and
+    k_bucket_count_redo recounts; the build then reports the bucket as too
+    big (BSDB_E2BIG, > 16 384 keys) instead of misplacing any key."""
+    n = 6_200_000
+    m = O.num_buckets(n)
+    assert 4096 < m <= 80_000
+    rng = np.random.default_rng(5)
+    sig = rng.integers(0, 1 << 40, (n, 2), dtype=np.uint64)  # sig0 < 2^40: bucket 0
+    sig[:, 1] = rng.integers(0, 1 << 63, n, dtype=np.uint64)
+    assert set(O.buckets(sig[:1000], m).tolist()) == {0}
+    with pytest.raises(BsdbError) as e:
+        ctx.gov_build(dev(sig.view(np.int64)), 4)
+    assert e.value.code == -7  # E2BIG
 
 
 def test_fvs_limit_fallback_is_identical(ctx, monkeypatch):
