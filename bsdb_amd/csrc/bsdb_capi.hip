@@ -923,7 +923,11 @@ static int gov_build_impl(bsdb_ctx *c, const GovSrc &src, uint64_t n_global, uin
     }
     const uint32_t big_cap = (uint32_t)(n_local / (GS_CMAX + 1) + 1);
     if ((rc = grow(&c->g_big, &c->g_big_bytes, (size_t)big_cap * 4))) return rc;
-    const uint32_t solve_grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(nb, (uint64_t)c->num_cus * GS_PER_CU));
+    // BSDB_GOV_ONE_PER_CU=1 (measurement only): one solver workgroup per CU
+    // (grid and LDS padding), to price the second one
+    const bool one_per_cu = getenv("BSDB_GOV_ONE_PER_CU") != nullptr;
+    const uint32_t solve_grid = (uint32_t)std::max<uint64_t>(
+        1, std::min<uint64_t>(nb, (uint64_t)c->num_cus * (one_per_cu ? 1 : GS_PER_CU)));
     if ((rc = grow(&c->g_scratch, &c->g_scratch_bytes, (size_t)solve_grid * solve_scratch_words<SolveLds>() * 8)))
         return rc;
     uint64_t *sorted = (uint64_t *)c->g_sorted;
@@ -1014,7 +1018,8 @@ static int gov_build_impl(bsdb_ctx *c, const GovSrc &src, uint64_t n_global, uin
                                                                     (uint8_t *)c->g_slabs, big_slab_bytes());
         HIP_OK(hipEventRecord(c->big_ev[1], c->big_stream));
     }
-    k_gov_solve<<<solve_grid, GS_THREADS, 0, s>>>(sa);  // A8
+    if (one_per_cu) HIP_OK(hipFuncSetAttribute((const void *)k_gov_solve, hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024));
+    k_gov_solve<<<solve_grid, GS_THREADS, one_per_cu ? 64 * 1024 : 0, s>>>(sa);  // A8
     if (nbig) HIP_OK(hipStreamWaitEvent(s, c->big_ev[1], 0));
     if (gprof) {
         std::vector<uint64_t> h((size_t)solve_grid * GP_N);
