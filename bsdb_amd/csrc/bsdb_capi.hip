@@ -829,6 +829,9 @@ struct GovSrc {
     const uint64_t *off = nullptr;
     uint64_t blob_bytes = 0;
     uint32_t key_len = 0;
+    // (key sources) every bucket's count over the whole key set, when known:
+    // a range build then takes its counts from here instead of re-hashing
+    const uint32_t *counts_all = nullptr;
 };
 
 // A13 fused into the solve: slot r - idx_lo of index_out gets key p's
@@ -890,7 +893,10 @@ static int gov_build_impl(bsdb_ctx *c, const GovSrc &src, uint64_t n_global, uin
         mid_base = (uint32_t *)((uint8_t *)c->g_mid + cw_bytes);
     }
     if (from_keys) {
-        if (src.n) launch_sel<0>(c, src, sel, s);
+        if (src.counts_all)
+            HIP_OK(hipMemcpyAsync(counts, src.counts_all + b_lo, nb * 4, hipMemcpyDeviceToDevice, s));
+        else if (src.n)
+            launch_sel<0>(c, src, sel, s);
     } else if (src.n && nb <= SMALL_NB) {
         k_bucket_count_small<<<(uint32_t)((src.n + SMALL_CHUNK - 1) / SMALL_CHUNK), 256, 0, s>>>(src.sig, src.n, mult, (uint32_t)b_lo,
                                                                                                (uint32_t)nb, counts);
