@@ -29,6 +29,7 @@
 
 #include "../../include/bsdb_mi355x.h"
 #include "hash_kernels.hip"
+#include "fused_kernels.hip"
 #include "mph_kernels.hip"
 #include "gov_kernels.hip"
 
@@ -54,6 +55,10 @@ struct bsdb_ctx {
     int d13_threads = 512;  // workgroup size of the pipelined 13-byte kernel (BSDB_D13_THREADS=256|512)
     int d13_copies = 8;     // region copies of the binned 13-byte kernel (BSDB_D13_COPIES=8|16|32)
     uint64_t chunk_keys = 0;
+    int fused = -1;  // 13-byte keys, single-pass kernel: -1 = what mode 0 picks (BSDB_FUSED), 0 off, 1 on
+    void *fu_ring = nullptr;  // its ring (FU_SLOTS x 10.5 MB) + sync words
+    size_t fu_ring_bytes = 0;
+    uint64_t fu_launches = 0;  // single-pass launches enqueued (bsdb_fused_status)
     std::mutex mu;
     // workspace
     void *ids = nullptr;
@@ -328,11 +333,94 @@ PartPlan plan_partitions(const bsdb_ctx *c, uint64_t chunk, uint64_t m, bool d13
     return p;
 }
 
+// The single-pass kernel (fused_kernels.hip) over the whole super-tiles of a
+// 13-byte key set: *done = the keys it covers (a multiple of 256 * 16384);
+// 0 when the set does not qualify.  Enqueue only.
+constexpr uint64_t FU_MIN_SUPER = 4;  // super-tiles per workgroup, at least
+
+int fused13_impl(bsdb_ctx *c, const uint8_t *keys, uint64_t blob_bytes, uint64_t n, uint64_t seed, uint64_t m,
+                 uint32_t *counts, hipStream_t s, uint64_t *done) {
+    *done = 0;
+    const uint64_t per = (uint64_t)FU_OWNERS * FU_TILE;
+    if (c->num_cus != FU_OWNERS || m == 0 || m > (uint64_t)FU_OWNERS * (FU_TCAP - 2)) return BSDB_OK;
+    // a key's 16-byte window ends 3 bytes past it: whole super-tiles whose
+    // windows stay inside the blob
+    if (blob_bytes < 3) return BSDB_OK;
+    const uint64_t nsuper = std::min(n / per, (blob_bytes - 3) / 13 / per);
+    if (nsuper < FU_MIN_SUPER) return BSDB_OK;
+    // the owner tables count in u16: keep the mean bucket count far below 2^16
+    // (a wrap is detected and recounted, but costs the whole launch)
+    if (n / m > 16384) return BSDB_OK;
+    static int per_cu = -1;
+    if (per_cu < 0 && hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_hist13_fused<true>, FU_NT, 0) != hipSuccess)
+        per_cu = 0;
+    if (per_cu < 1) return BSDB_OK;  // every workgroup must be resident
+    const size_t sync_bytes = FU_SYNC_U64 * sizeof(uint64_t);
+    const size_t ring_bytes = (size_t)FU_SLOTS * FU_SLOT_BYTES;
+    int variant = 0;
+    if (const char *v = getenv("BSDB_FU_VARIANT")) variant = atoi(v);
+    int rc = grow(&c->fu_ring, &c->fu_ring_bytes, ring_bytes + sync_bytes);
+    if (rc) return rc;
+    FusedArgs fa{};
+    fa.keys = keys;
+    fa.nsuper = nsuper;
+    fa.seed = seed;
+    fa.mult = (uint32_t)(2 * m);
+    fa.m = (uint32_t)m;
+    fa.ring = (uint8_t *)c->fu_ring;
+    fa.sync = (uint64_t *)((uint8_t *)c->fu_ring + ring_bytes);
+    fa.overflow = c->overflow;
+    fa.counts = counts;
+    HIP_OK(hipMemsetAsync(fa.sync, 0, sync_bytes, s));
+    HIP_OK(hipMemsetAsync(c->overflow, 0, sizeof(uint32_t), s));
+    ++c->fu_launches;
+    {
+        ProfScope ps(c, s, 0, nsuper * per);
+        // BSDB_FU_VARIANT (profiling, fused_kernels.hip): 1, 2, 4 results invalid, 8 phase stamps
+        if (variant == 1) k_hist13_fused<true, 1><<<FU_OWNERS, FU_NT, 0, s>>>(fa);
+        else if (variant == 2) k_hist13_fused<true, 2><<<FU_OWNERS, FU_NT, 0, s>>>(fa);
+        else if (variant == 4) k_hist13_fused<true, 4><<<FU_OWNERS, FU_NT, 0, s>>>(fa);
+        else if (variant == 8) k_hist13_fused<true, 8><<<FU_OWNERS, FU_NT, 0, s>>>(fa);
+        else if (seed == 0 && !getenv("BSDB_NO_SEED0"))
+            k_hist13_fused<true><<<FU_OWNERS, FU_NT, 0, s>>>(fa);
+        else
+            k_hist13_fused<false><<<FU_OWNERS, FU_NT, 0, s>>>(fa);
+    }
+    // an overflow anywhere (adversarial sets): nothing was added; recount
+    P1Args af{};
+    af.keys = keys;
+    af.blob_bytes = blob_bytes;
+    af.key_len = 13;
+    af.n = nsuper * per;
+    af.seed = seed;
+    af.multiplier = 2 * m;
+    af.counts = counts;
+    af.overflow = c->overflow;
+    k_overflow_fallback<SRC_FIXED_DIRECT, 0><<<1024, P1_THREADS, 0, s>>>(af);
+    if ((rc = launch_status())) return rc;
+    *done = nsuper * per;
+    return BSDB_OK;
+}
+
+bool fused_wanted(const bsdb_ctx *c) {
+    if (c->hist_mode == 3) return true;
+    if (c->hist_mode != 0) return false;
+    if (c->fused >= 0) return c->fused == 1;
+    return false;
+}
+
 int histogram_impl(bsdb_ctx *c, const uint8_t *keys, const uint64_t *offsets, uint64_t blob_bytes,
                    uint32_t key_len, uint64_t n, uint64_t seed, uint64_t m, uint32_t *counts,
                    hipStream_t s) {
     if (n == 0) return BSDB_OK;
     const bool var = offsets != nullptr;
+    if (!var && key_len == 13 && fused_wanted(c)) {
+        uint64_t done = 0;
+        const int rc = fused13_impl(c, keys, blob_bytes, n, seed, m, counts, s, &done);
+        if (rc) return rc;
+        if (done) return histogram_impl(c, keys + done * 13, nullptr, blob_bytes - done * 13, 13, n - done, seed, m,
+                                        counts, s);  // the rest (< one super-tile round): two-pass
+    }
     P1Args a{};
     a.keys = keys;
     a.offsets = offsets;
@@ -343,6 +431,7 @@ int histogram_impl(bsdb_ctx *c, const uint8_t *keys, const uint64_t *offsets, ui
     a.counts = counts;
     const uint32_t nparts = (uint32_t)((m + PART_BUCKETS - 1) / PART_BUCKETS);
     const bool atomic_mode = c->hist_mode == 2 || nparts > (uint32_t)MAX_PARTS;
+    // (mode 3 on a set the fused kernel does not take: the two-pass path)
     if (atomic_mode) {
         a.n = n;
         ProfScope ps(c, s, 0, n);
@@ -547,6 +636,7 @@ int bsdb_open(int device, bsdb_ctx **out) {
     if (!c) return BSDB_ENOMEM;
     c->device = device;
     if (const char *v = std::getenv("BSDB_D13_VARIANT")) c->d13_variant = std::atoi(v);
+    if (const char *v = std::getenv("BSDB_FUSED")) c->fused = std::atoi(v) ? 1 : 0;
     if (const char *v = std::getenv("BSDB_D13_THREADS")) c->d13_threads = std::atoi(v) == 256 ? 256 : 512;
     if (const char *v = std::getenv("BSDB_D13_COPIES")) {
         const int k = std::atoi(v);
@@ -578,6 +668,7 @@ int bsdb_close(bsdb_ctx *c) {
     (void)hipFree(c->ids);
     (void)hipFree(c->cursor);
     (void)hipFree(c->p2_pref);
+    (void)hipFree(c->fu_ring);
     (void)hipFree(c->overflow);
     (void)hipFree(c->scan_part);
     if (c->copy_stream) (void)hipStreamSynchronize(c->copy_stream);
@@ -613,7 +704,7 @@ int bsdb_close(bsdb_ctx *c) {
 }
 
 int bsdb_set_histogram_mode(bsdb_ctx *c, int mode) {
-    if (!c || mode < 0 || mode > 2) return BSDB_EINVAL;
+    if (!c || mode < 0 || mode > 3) return BSDB_EINVAL;
     std::lock_guard<std::mutex> g(c->mu);
     c->hist_mode = mode;
     return BSDB_OK;
@@ -634,6 +725,18 @@ int bsdb_fallback_count(bsdb_ctx *c, uint64_t *out) {
     uint32_t v = 0;
     HIP_OK(hipMemcpy(&v, c->overflow + 2, sizeof(v), hipMemcpyDeviceToHost));
     *out = v;
+    return BSDB_OK;
+}
+
+int bsdb_fused_status(bsdb_ctx *c, uint64_t *launches, uint64_t *timeouts) {
+    if (!c || !launches || !timeouts) return BSDB_EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    HIP_OK(hipSetDevice(c->device));
+    HIP_OK(hipDeviceSynchronize());
+    uint32_t v = 0;
+    HIP_OK(hipMemcpy(&v, c->overflow + 3, sizeof(v), hipMemcpyDeviceToHost));
+    *launches = c->fu_launches;
+    *timeouts = v;
     return BSDB_OK;
 }
 

@@ -402,6 +402,34 @@ __device__ __forceinline__ uint32_t short_end_bucket(uint64_t h0, uint64_t h1, u
     return (uint32_t)(t >> 32);
 }
 
+// short_end_bucket that also returns the top 8 bits of x = sig0 >>> 1 (the
+// fused histogram's bucket owner, k_hist13_fused): buckets are monotone in x,
+// so owner w's buckets are [floor(w m / 256), floor((w + 1) m / 256)].
+__device__ __forceinline__ uint32_t short_end_bucket_owner(uint64_t h0, uint64_t h1, uint64_t h2, uint64_t h3,
+                                                           uint32_t mult, uint32_t &owner) {
+#define BSDB_END_STEP_U(D, C, K) D ^= C; C = rotl_u<K>(C); D = add_u(D, C);
+    BSDB_END_STEP_U(h3, h2, 15) BSDB_END_STEP_U(h0, h3, 52) BSDB_END_STEP_U(h1, h0, 26)
+    BSDB_END_STEP_U(h2, h1, 51) BSDB_END_STEP_U(h3, h2, 28) BSDB_END_STEP_U(h0, h3, 9)
+    BSDB_END_STEP_U(h1, h0, 47) BSDB_END_STEP_U(h2, h1, 54)
+    h3 ^= h2;
+    h3 = add_swapped(h3, h2);
+    BSDB_END_STEP_U(h0, h3, 25)
+#undef BSDB_END_STEP_U
+    const uint32_t hl = (uint32_t)h0, hh = (uint32_t)(h0 >> 32);
+    const uint32_t xl = __builtin_amdgcn_alignbit(hh, hl, 2);
+    const uint32_t xh = __builtin_amdgcn_alignbit(hl, hh, 2) & 0x7FFFFFFFu;
+    owner = xh >> 23;
+    const uint64_t t = (uint64_t)xh * mult + __umulhi(xl, mult);  // GOV:559, as bucket_of_w
+    return (uint32_t)(t >> 32);
+}
+
+__device__ __forceinline__ uint32_t spooky13_bucket_owner(uint32_t d0, uint32_t d1, uint32_t d2, uint32_t d3,
+                                                          uint32_t sh, uint64_t seed, uint32_t mult, uint32_t &owner) {
+    const uint64_t w0 = ((uint64_t)__builtin_amdgcn_alignbit(d2, d1, sh) << 32) | __builtin_amdgcn_alignbit(d1, d0, sh);
+    const uint64_t w1 = ((uint64_t)((d3 >> sh) & 0xFFu) << 32) | __builtin_amdgcn_alignbit(d3, d2, sh);
+    return short_end_bucket_owner(seed + 13 * 8, seed, add_u(SC, w0), add_u(SC, w1), mult, owner);
+}
+
 // SURVEY.md §8(d) D2 synthetic keys (bench input generator only).
 __host__ __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
     uint64_t z = x + 0x9e3779b97f4a7c15ULL;

@@ -55,6 +55,7 @@ SIGNATURES = [
     ("bsdb_set_frontend", _i, [_vp, _i]),
     ("bsdb_set_chunk_keys", _i, [_vp, _u64]),
     ("bsdb_fallback_count", _i, [_vp, C.POINTER(_u64)]),
+    ("bsdb_fused_status", _i, [_vp, C.POINTER(_u64), C.POINTER(_u64)]),
     ("bsdb_set_profiling", _i, [_vp, _i]),
     ("bsdb_profile_read", _i, [_vp, _i, C.POINTER(C.c_double), C.POINTER(_u64), C.POINTER(_u64)]),
     ("bsdb_histogram_fixed", _i, [_vp, _vp, _u32, _u64, _u64, _u64, _vp]),
@@ -198,6 +199,12 @@ class Context:
         v = C.c_uint64()
         _check("bsdb_fallback_count", lib().bsdb_fallback_count(self._h, C.byref(v)))
         return v.value
+
+    def fused_status(self):
+        """(single-pass launches since open, launches that timed out) -- synchronises."""
+        a, b = C.c_uint64(), C.c_uint64()
+        _check("bsdb_fused_status", lib().bsdb_fused_status(self._h, C.byref(a), C.byref(b)))
+        return a.value, b.value
 
     # ---- live per-kernel timing (HIP events on the launch stream)
     PASS1, PASS2, SCAN = 0, 1, 2

@@ -202,7 +202,11 @@ int bsdb_dev_partition_owners(bsdb_ctx *ctx, const uint64_t *d_sig, const uint64
 int bsdb_set_verify(bsdb_ctx *ctx, int enable);
 
 /* Histogram path selection for bsdb_dev_histogram_* (benchmarks/tests):
- *   0 = auto (partitioned two-pass), 1 = partitioned two-pass, 2 = direct atomics. */
+ *   0 = auto, 1 = partitioned two-pass, 2 = direct atomics,
+ *   3 = single pass (13-byte keys on a 256-CU device, m <= 9 436 672 buckets,
+ *       >= 4 * 256 * 16384 keys, <= 16384 keys per bucket on average: bucket owners per CU, ids exchanged through an
+ *       on-die ring; other key sets, and the tail past its whole super-tiles,
+ *       take the two-pass path).  Results are identical in every mode. */
 int bsdb_set_histogram_mode(bsdb_ctx *ctx, int mode);
 /* Key-load front end (for comparison runs; results are identical):
  * 0 = auto: 13-byte keys by the persistent binned kernel (dword-aligned
@@ -217,6 +221,10 @@ int bsdb_set_chunk_keys(bsdb_ctx *ctx, uint64_t chunk_keys);
  * because a partition region or LDS bin overflowed (adversarial key sets,
  * e.g. many duplicates).  Synchronises the device.  0 for normal inputs. */
 int bsdb_fallback_count(bsdb_ctx *ctx, uint64_t *out);
+/* Single-pass histogram (mode 3): launches enqueued since open, and those
+ * whose bounded waits timed out (a workgroup never became resident; nothing
+ * was added and the keys were recounted).  Synchronises the device. */
+int bsdb_fused_status(bsdb_ctx *ctx, uint64_t *launches, uint64_t *timeouts);
 
 /* Live per-kernel timing with HIP events recorded on the launch stream around
  * every pass-1 (hash+partition) and pass-2 (partition histogram) launch.

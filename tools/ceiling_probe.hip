@@ -16,8 +16,15 @@
 //           bits, column = the lane: every lane of a wave on its own bank)
 //   ldsrtn  the random count with the returned old value used (ds_add_rtn,
 //           the pass-1 kernel's rank atomic)
-// Each kernel is timed with HIP events (best of 3).  The keys are a fixed
-// byte pattern: the hash's cost does not depend on the values.
+// Each kernel is timed with HIP events (best of 3).  The keys are random
+// bytes (a splitmix64 fill): the hash's cost does not depend on the values,
+// but the LDS atomics' does -- with a constant fill (round 3's first runs)
+// every key has one of four buckets, so a wave's 64 atomics hit ~4 words and
+// serialise; those 'lds' rows measured same-word contention, not random
+// banks.
+//   ldsu16  hash + one u16-packed LDS count per key into a 34 360-bucket
+//           table (68.7 KB, ds_add_u32 of 1 or 1<<16): the consumer side of
+//           the fused single-pass design
 //   hipcc --offload-arch=gfx950 -O3 -I bsdb_amd/csrc tools/ceiling_probe.hip -o tools/ceiling_probe
 #include <hip/hip_runtime.h>
 
@@ -50,12 +57,25 @@ __global__ __launch_bounds__(NT) void k16(const uint8_t *p, uint64_t nvec, uint3
 
 constexpr int LDS_BINS = 8192;
 
-// LDS: 0 none, 1 random ds_add, 2 conflict-free ds_add, 3 random ds_add_rtn
+constexpr int U16_BUCKETS = 34360, U16_WORDS = U16_BUCKETS / 2;
+
+__global__ void k_fill(uint64_t *p, uint64_t nwords) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < nwords; i += (uint64_t)gridDim.x * blockDim.x) {
+        uint64_t z = (i + 1) * 0x9E3779B97F4A7C15ull;
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        p[i] = z ^ (z >> 31);
+    }
+}
+
+// LDS: 0 none, 1 random ds_add, 2 conflict-free ds_add, 3 random ds_add_rtn,
+// 4 u16-packed count into a 34 360-bucket table
 template <bool HASH, int LDS = 0>
 __global__ __launch_bounds__(NT) void k13(const uint8_t *p, uint64_t nkeys, uint32_t mult, uint32_t *out) {
-    __shared__ uint32_t tab[LDS ? LDS_BINS : 1];
+    constexpr int TAB = LDS == 4 ? U16_WORDS : LDS ? LDS_BINS : 1;
+    __shared__ uint32_t tab[TAB];
     if (LDS) {
-        for (int i = threadIdx.x; i < LDS_BINS; i += NT) tab[i] = 0;
+        for (int i = threadIdx.x; i < TAB; i += NT) tab[i] = 0;
         __syncthreads();
     }
     uint32_t x = 0;
@@ -82,6 +102,10 @@ __global__ __launch_bounds__(NT) void k13(const uint8_t *p, uint64_t nkeys, uint
                     if (k < nkeys) atomicAdd(&tab[((b >> 6) & (LDS_BINS / 64 - 1)) * 64 + (threadIdx.x & 63)], 1u);
                 } else if (LDS == 3) {
                     if (k < nkeys) x += atomicAdd(&tab[b & (LDS_BINS - 1)], 1u);
+                } else if (LDS == 4) {
+                    const uint32_t o = __umulhi(b, 0x80000000u / U16_BUCKETS * 2) ;  // (b mod-ish table slot)
+                    const uint32_t t = b - o * U16_BUCKETS;
+                    if (k < nkeys) atomicAdd(&tab[(t >> 1) % U16_WORDS], 1u << ((t & 1) << 4));
                 } else {
                     x ^= b;
                 }
@@ -92,7 +116,7 @@ __global__ __launch_bounds__(NT) void k13(const uint8_t *p, uint64_t nkeys, uint
     }
     if (LDS) {
         __syncthreads();
-        for (int i = threadIdx.x; i < LDS_BINS; i += NT) x ^= tab[i] * (uint32_t)(i + 1);
+        for (int i = threadIdx.x; i < TAB; i += NT) x ^= tab[i] * (uint32_t)(i + 1);
     }
     if (x == 0x12345678u) out[threadIdx.x] = x;
 }
@@ -107,6 +131,7 @@ int main(int argc, char **argv) {
         return 1;
     }
     (void)hipMemset(p, 0x5b, bytes + 64);
+    k_fill<<<4096, 256>>>(reinterpret_cast<uint64_t *>(p), bytes / 8);
     (void)hipDeviceSynchronize();
     int cus = 256;
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
@@ -114,8 +139,9 @@ int main(int argc, char **argv) {
     (void)hipEventCreate(&a);
     (void)hipEventCreate(&b);
     printf("{\"n_keys\": %llu, \"key_bytes\": %.1f, \"cus\": %d", (unsigned long long)n, bytes / 1e9, cus);
-    for (int kind = 0; kind < 6; ++kind) {
-        for (int per_cu : {2, 4, 8}) {
+    const int kind0 = argc > 2 ? atoi(argv[2]) : 0;
+    for (int kind = kind0; kind < 7; ++kind) {
+        for (int per_cu : {2, 4}) {
             const int grid = cus * per_cu;
             float best = 1e30f;
             for (int rep = 0; rep < 4; ++rep) {
@@ -125,14 +151,15 @@ int main(int argc, char **argv) {
                 else if (kind == 2) k13<true><<<grid, NT>>>(p, n, (uint32_t)(2 * m), o);
                 else if (kind == 3) k13<true, 1><<<grid, NT>>>(p, n, (uint32_t)(2 * m), o);
                 else if (kind == 4) k13<true, 2><<<grid, NT>>>(p, n, (uint32_t)(2 * m), o);
-                else k13<true, 3><<<grid, NT>>>(p, n, (uint32_t)(2 * m), o);
+                else if (kind == 5) k13<true, 3><<<grid, NT>>>(p, n, (uint32_t)(2 * m), o);
+                else k13<true, 4><<<grid, NT>>>(p, n, (uint32_t)(2 * m), o);
                 (void)hipEventRecord(b);
                 (void)hipEventSynchronize(b);
                 float ms = 0;
                 (void)hipEventElapsedTime(&ms, a, b);
                 if (rep && ms < best) best = ms;
             }
-            const char *name = kind == 0 ? "k16" : kind == 1 ? "k13" : kind == 2 ? "hash" : kind == 3 ? "lds" : kind == 4 ? "ldscf" : "ldsrtn";
+            const char *name = kind == 0 ? "k16" : kind == 1 ? "k13" : kind == 2 ? "hash" : kind == 3 ? "lds" : kind == 4 ? "ldscf" : kind == 5 ? "ldsrtn" : "ldsu16";
             printf(", \"%s_wg%d\": {\"ms\": %.3f, \"TBps\": %.3f, \"Gkeys_per_s\": %.1f, \"roofline_frac\": %.3f}", name,
                    per_cu, best, bytes / best / 1e9, n / best / 1e6, bytes / best / 1e9 / 8.0);
             fflush(stdout);
