@@ -56,6 +56,11 @@ struct bsdb_ctx {
     int d13_copies = 8;     // region copies of the binned 13-byte kernel (BSDB_D13_COPIES=8|16|32)
     uint64_t chunk_keys = 0;
     int fused = -1;  // 13-byte keys, single-pass kernel: -1 = what mode 0 picks (BSDB_FUSED), 0 off, 1 on
+    int pipe = -1;   // pass 2 of a chunk beside pass 1 of the next: -1 default, 0 off, 1 on (BSDB_PIPE)
+    uint64_t pipe_chunks = 0;  // chunks of the pipelined histogram (0 = default; BSDB_PIPE_CHUNKS)
+    uint32_t pipe_cus = 0;     // CUs pass 2 keeps while pass 1 runs (0 = default; BSDB_PIPE_P2CUS)
+    hipStream_t p2_stream = nullptr;
+    hipEvent_t pipe_ev[6] = {};  // [b] pass 1 into buffer b done, [2 + b] buffer b read, [4] start, [5] end
     void *fu_ring = nullptr;  // its ring (FU_SLOTS x 10.5 MB) + sync words
     size_t fu_ring_bytes = 0;
     uint64_t fu_launches = 0;  // single-pass launches enqueued (bsdb_fused_status)
@@ -321,6 +326,8 @@ PartPlan plan_partitions(const bsdb_ctx *c, uint64_t chunk, uint64_t m, bool d13
         per_cu = std::min(per_cu, 2048 / sel.nt);  // at most 32 waves per CU
         const uint64_t tiles = (chunk + sel.tile - 1) / sel.tile;
         p.grid_d13 = (uint32_t)std::min<uint64_t>(tiles, (uint64_t)c->num_cus * per_cu);
+        // measurement aid: fewer persistent workgroups (BSDB_D13_GRID, e.g. CUs left for other work)
+        if (const char *v = getenv("BSDB_D13_GRID")) p.grid_d13 = (uint32_t)std::max<int64_t>(1, std::min<int64_t>(p.grid_d13, atoll(v)));
         if (binned) {
             const double tiles_per_copy = (double)tiles / p.nmain + 1;
             p.cap = round64(e * 1.02 + 8.0 * std::sqrt(e) + 7.0 * tiles_per_copy + 2 * P1_TILE + 64);
@@ -402,6 +409,13 @@ int fused13_impl(bsdb_ctx *c, const uint8_t *keys, uint64_t blob_bytes, uint64_t
     return BSDB_OK;
 }
 
+bool pipe_wanted(const bsdb_ctx *c) { return c->pipe == 1; }
+
+uint32_t pipe_p2_cus(const bsdb_ctx *c) {
+    const uint32_t k = c->pipe_cus ? c->pipe_cus : (uint32_t)c->num_cus / 8;  // 4 per XCD
+    return std::max<uint32_t>(1, std::min<uint32_t>(k, (uint32_t)c->num_cus / 2));
+}
+
 bool fused_wanted(const bsdb_ctx *c) {
     if (c->hist_mode == 3) return true;
     if (c->hist_mode != 0) return false;
@@ -456,29 +470,52 @@ int histogram_impl(bsdb_ctx *c, const uint8_t *keys, const uint64_t *offsets, ui
         sel = D13Sel{k_pass1_d13<512>, 512, 512 * P1_KEYS_PER_THREAD, 1024, false, 0};
         d13 = nparts <= sel.maxp;
     }
+    const bool pipe_pl = pipe_wanted(c) && d13 && windowed && sel.binned;
+    if (pipe_pl && !c->chunk_keys) {
+        // equal chunks of whole tiles: pass 2 of each beside pass 1 of the next
+        const uint64_t nch = c->pipe_chunks ? c->pipe_chunks : 8;
+        chunk = std::max<uint64_t>(sel.tile, ((n + nch - 1) / nch + sel.tile - 1) / sel.tile * sel.tile);
+    }
     PartPlan pp = plan_partitions(c, chunk, m, d13, sel);
-    // the id buffer takes at most half of the device memory left (workspace
+    // the id buffers take at most half of the device memory left (workspace
     // included); the 13-byte kernel addresses one region set (P segments)
     // with 32-bit offsets
     size_t free_b = 0, total_b = 0;
     if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) free_b = 0;
-    const size_t budget = (free_b + c->ids_bytes) / 2;
+    const size_t budget = (free_b + c->ids_bytes) / 2 / (pipe_pl ? 2 : 1);
     while (chunk > 2 * P1_TILE && (pp.ids_elems() * sizeof(uint16_t) > budget ||
                                    (uint64_t)pp.nparts * pp.cap >= (1ULL << 32))) {
         chunk = std::max<uint64_t>(P1_TILE, chunk / 2 / P1_TILE * P1_TILE);
         pp = plan_partitions(c, chunk, m, d13, sel);
     }
     const uint32_t R = pp.nmain + pp.ntail;
-    int rc = grow(&c->ids, &c->ids_bytes, pp.ids_elems() * sizeof(uint16_t));
+    // Pass 2 of chunk i overlapped with pass 1 of chunk i + 1 (13-byte
+    // windowed keys, several chunks): two id buffers; pass 1 on the caller's
+    // stream over all CUs but the ones pass 2 keeps (its workgroups hold 128
+    // KiB of LDS, pass 1's 146 KiB: one per CU each, so the two launches
+    // split the chip); pass 2 on the context's second stream.  The first
+    // pass 1 and the last pass 2 get the whole chip.
+    const bool pipe = pipe_wanted(c) && d13 && windowed && sel.binned && n > chunk;
+    const int nbuf = pipe ? 2 : 1;
+    const size_t ids_per_buf = pp.ids_elems(), cur_per_buf = (size_t)pp.nparts * R;
+    int rc = grow(&c->ids, &c->ids_bytes, nbuf * ids_per_buf * sizeof(uint16_t));
     if (rc) return rc;
-    rc = grow((void **)&c->cursor, &c->cursor_bytes, ((size_t)pp.nparts * R + P1_SCRATCH_WG + (size_t)P1_SCRATCH_MAXWG * 1024) * sizeof(uint32_t));
+    rc = grow((void **)&c->cursor, &c->cursor_bytes,
+              (nbuf * cur_per_buf + P1_SCRATCH_WG + (size_t)P1_SCRATCH_MAXWG * 1024) * sizeof(uint32_t));
     if (rc) return rc;
-    rc = grow((void **)&c->p2_pref, &c->p2_pref_bytes, ((size_t)pp.nparts * R + 1) * sizeof(uint64_t));
+    rc = grow((void **)&c->p2_pref, &c->p2_pref_bytes, nbuf * (cur_per_buf + 1) * sizeof(uint64_t));
     if (rc) return rc;
-    a.ids = (uint16_t *)c->ids;
-    a.cursor = c->cursor;
-    a.scratch = c->cursor + (size_t)pp.nparts * R;
-    a.overflow = c->overflow;
+    hipStream_t s2 = s;
+    if (pipe) {
+        if (!c->p2_stream && hipStreamCreateWithFlags(&c->p2_stream, hipStreamNonBlocking) != hipSuccess) return BSDB_EIO;
+        for (auto &e : c->pipe_ev)
+            if (!e && hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return BSDB_EIO;
+        s2 = c->p2_stream;
+        HIP_OK(hipEventRecord(c->pipe_ev[4], s));  // the caller's earlier work
+        HIP_OK(hipStreamWaitEvent(s2, c->pipe_ev[4], 0));
+    }
+    const uint32_t p2_cus = pipe ? pipe_p2_cus(c) : 0;
+    a.scratch = c->cursor + nbuf * cur_per_buf;
     a.cap = pp.cap;
     a.nparts = pp.nparts;
     a.nregions = pp.nmain;
@@ -486,30 +523,42 @@ int histogram_impl(bsdb_ctx *c, const uint8_t *keys, const uint64_t *offsets, ui
     a.ncopy = pp.nmain;
     a.bin_shift = pp.bin_shift;
     a.capb = pp.capb;
-    P2Layout L{};
-    L.ids = (const uint16_t *)c->ids;
-    L.cursor = c->cursor;
-    L.overflow = c->overflow;
-    L.cap = pp.cap;
-    L.cap_tail = pp.cap_tail;
-    L.nparts = pp.nparts;
-    L.nmain = pp.nmain;
-    L.ntail = pp.ntail;
-    L.bshift = PART_SHIFT - pp.bin_shift;
-    L.num_buckets = m;
-    L.counts = counts;
-    for (uint64_t k0 = 0; k0 < n; k0 += chunk) {
+    P2Layout L0{};
+    L0.cap = pp.cap;
+    L0.cap_tail = pp.cap_tail;
+    L0.nparts = pp.nparts;
+    L0.nmain = pp.nmain;
+    L0.ntail = pp.ntail;
+    L0.bshift = PART_SHIFT - pp.bin_shift;
+    L0.num_buckets = m;
+    L0.counts = counts;
+    uint64_t i = 0;
+    for (uint64_t k0 = 0; k0 < n; k0 += chunk, ++i) {
         const uint64_t nk = std::min(chunk, n - k0);
+        const bool first = k0 == 0, last = k0 + nk >= n;
+        const uint32_t b = pipe ? (uint32_t)(i & 1) : 0;
+        // buffer b's ids, cursors, pass-2 plan and overflow flag
         P1Args ac = a;
+        ac.ids = (uint16_t *)c->ids + b * ids_per_buf;
+        ac.cursor = c->cursor + b * cur_per_buf;
+        ac.overflow = c->overflow + 4 * b;
+        uint64_t *pref = c->p2_pref + b * (cur_per_buf + 1);
+        P2Layout L = L0;
+        L.ids = ac.ids;
+        L.cursor = ac.cursor;
+        L.overflow = ac.overflow;
         ac.n = nk;
         if (var) {
             ac.offsets = offsets + k0;
         } else {
             ac.keys = keys + k0 * key_len;
-            ac.blob_bytes = nk * key_len;
+            // a window past the chunk reads the next chunk's bytes (the blob
+            // goes on): only the blob's end limits the persistent kernel
+            ac.blob_bytes = pipe ? blob_bytes - k0 * key_len : nk * key_len;
         }
-        HIP_OK(hipMemsetAsync(c->cursor, 0, sizeof(uint32_t) * R * pp.nparts, s));
-        HIP_OK(hipMemsetAsync(c->overflow, 0, sizeof(uint32_t), s));
+        if (pipe && i >= 2) HIP_OK(hipStreamWaitEvent(s, c->pipe_ev[2 + b], 0));  // pass 2 of chunk i - 2 read buffer b
+        HIP_OK(hipMemsetAsync(ac.cursor, 0, sizeof(uint32_t) * cur_per_buf, s));
+        HIP_OK(hipMemsetAsync(ac.overflow, 0, sizeof(uint32_t), s));
         {
             ProfScope ps(c, s, 0, nk);
             const uint64_t tiles = (nk + P1_TILE - 1) / P1_TILE;
@@ -525,8 +574,8 @@ int histogram_impl(bsdb_ctx *c, const uint8_t *keys, const uint64_t *offsets, ui
                 if (done < nk) {
                     P1Args at = ac;
                     at.n = nk - done;
-                    at.ids = a.ids + (size_t)pp.nmain * pp.nparts * pp.cap;
-                    at.cursor = a.cursor + (size_t)pp.nmain * pp.nparts;
+                    at.ids = ac.ids + (size_t)pp.nmain * pp.nparts * pp.cap;
+                    at.cursor = ac.cursor + (size_t)pp.nmain * pp.nparts;
                     at.cap = pp.cap_tail;
                     at.nregions = pp.ntail;
                     if (var) {
@@ -539,15 +588,16 @@ int histogram_impl(bsdb_ctx *c, const uint8_t *keys, const uint64_t *offsets, ui
                     }
                 }
             } else if (d13) {
-                // full tiles whose 16-byte windows stay inside the chunk go to the
-                // persistent kernel (a key's window ends 16 - L bytes past it at
-                // most); the rest (< 2 of its tiles) to the bounds-checked
-                // kernel, in the tail regions
+                // full tiles whose 16-byte windows stay inside the readable
+                // blob go to the persistent kernel (a key's window ends 16 - L
+                // bytes past it at most); the rest (< 2 of its tiles) to the
+                // bounds-checked kernel, in the tail regions
                 const uint64_t dtile = sel.tile, over = 16 - key_len;
                 uint64_t nfast = 0;
                 if (ac.blob_bytes >= over) nfast = std::min(nk / dtile, ((ac.blob_bytes - over) / key_len) / dtile);
                 if (nfast) {
-                    const uint32_t grid = (uint32_t)std::min<uint64_t>(nfast, pp.grid_d13);
+                    uint32_t grid = (uint32_t)std::min<uint64_t>(nfast, pp.grid_d13);
+                    if (pipe && !first) grid = std::max<uint32_t>(1, std::min<uint32_t>(grid, (uint32_t)c->num_cus - p2_cus));
                     sel.k<<<grid, sel.nt, 0, s>>>(ac, nfast);
                 }
                 const uint64_t done = nfast * dtile;
@@ -556,8 +606,8 @@ int histogram_impl(bsdb_ctx *c, const uint8_t *keys, const uint64_t *offsets, ui
                     at.keys = ac.keys + done * key_len;
                     at.n = nk - done;
                     at.blob_bytes = at.n * key_len;
-                    at.ids = a.ids + (size_t)pp.nmain * pp.nparts * pp.cap;
-                    at.cursor = a.cursor + (size_t)pp.nmain * pp.nparts;
+                    at.ids = ac.ids + (size_t)pp.nmain * pp.nparts * pp.cap;
+                    at.cursor = ac.cursor + (size_t)pp.nmain * pp.nparts;
                     at.cap = pp.cap_tail;
                     at.nregions = pp.ntail;
                     launch_pass1<EPI_PARTITION>(at, false, key_len, (at.n + P1_TILE - 1) / P1_TILE, s, 0);
@@ -566,17 +616,28 @@ int histogram_impl(bsdb_ctx *c, const uint8_t *keys, const uint64_t *offsets, ui
                 launch_pass1<EPI_PARTITION>(ac, var, key_len, tiles, s, c->frontend);
             }
         }
+        if (pipe) {
+            HIP_OK(hipEventRecord(c->pipe_ev[b], s));  // pass 1 of chunk i done
+            HIP_OK(hipStreamWaitEvent(s2, c->pipe_ev[b], 0));
+        }
         {
-            ProfScope ps(c, s, 1, nk);
-            k_pass2_plan<<<1, SCAN_THREADS, 0, s>>>(L, c->p2_pref);
-            k_pass2b<<<(uint32_t)c->num_cus, P2_THREADS, 0, s>>>(L, c->p2_pref);
+            ProfScope ps(c, s2, 1, nk);
+            k_pass2_plan<<<1, SCAN_THREADS, 0, s2>>>(L, pref);
+            const uint32_t g2 = pipe && !last ? p2_cus : (uint32_t)c->num_cus;
+            k_pass2b<<<g2, P2_THREADS, 0, s2>>>(L, pref);
         }
         if (var) {
-            k_overflow_fallback<SRC_VAR, 0><<<1024, P1_THREADS, 0, s>>>(ac);
+            k_overflow_fallback<SRC_VAR, 0><<<1024, P1_THREADS, 0, s2>>>(ac);
         } else {
-            k_overflow_fallback<SRC_FIXED_DIRECT, 0><<<1024, P1_THREADS, 0, s>>>(ac);
+            k_overflow_fallback<SRC_FIXED_DIRECT, 0><<<1024, P1_THREADS, 0, s2>>>(ac);
         }
+        if (pipe) HIP_OK(hipEventRecord(c->pipe_ev[2 + b], s2));  // buffer b free again
         if ((rc = launch_status())) return rc;
+    }
+    if (pipe) {
+        // the caller's stream continues after the last pass 2
+        HIP_OK(hipEventRecord(c->pipe_ev[5], s2));
+        HIP_OK(hipStreamWaitEvent(s, c->pipe_ev[5], 0));
     }
     return BSDB_OK;
 }
@@ -637,6 +698,9 @@ int bsdb_open(int device, bsdb_ctx **out) {
     c->device = device;
     if (const char *v = std::getenv("BSDB_D13_VARIANT")) c->d13_variant = std::atoi(v);
     if (const char *v = std::getenv("BSDB_FUSED")) c->fused = std::atoi(v) ? 1 : 0;
+    if (const char *v = std::getenv("BSDB_PIPE")) c->pipe = std::atoi(v) ? 1 : 0;
+    if (const char *v = std::getenv("BSDB_PIPE_CHUNKS")) c->pipe_chunks = std::strtoull(v, nullptr, 10);
+    if (const char *v = std::getenv("BSDB_PIPE_P2CUS")) c->pipe_cus = (uint32_t)std::atoi(v);
     if (const char *v = std::getenv("BSDB_D13_THREADS")) c->d13_threads = std::atoi(v) == 256 ? 256 : 512;
     if (const char *v = std::getenv("BSDB_D13_COPIES")) {
         const int k = std::atoi(v);
@@ -649,8 +713,10 @@ int bsdb_open(int device, bsdb_ctx **out) {
         delete c;
         return BSDB_EIO;
     }
-    if (hipMalloc(&c->overflow, sizeof(uint32_t) * 4) != hipSuccess ||
-        hipMemset(c->overflow, 0, sizeof(uint32_t) * 4) != hipSuccess) {
+    // [0] / [4]: overflow flags of id buffers 0 / 1, [2] / [6]: their fallback
+    // counts, [3]: single-pass timeouts
+    if (hipMalloc(&c->overflow, sizeof(uint32_t) * 8) != hipSuccess ||
+        hipMemset(c->overflow, 0, sizeof(uint32_t) * 8) != hipSuccess) {
         bsdb_close(c);
         return BSDB_ENOMEM;
     }
@@ -669,6 +735,10 @@ int bsdb_close(bsdb_ctx *c) {
     (void)hipFree(c->cursor);
     (void)hipFree(c->p2_pref);
     (void)hipFree(c->fu_ring);
+    if (c->p2_stream) (void)hipStreamSynchronize(c->p2_stream);
+    for (hipEvent_t e : c->pipe_ev)
+        if (e) (void)hipEventDestroy(e);
+    if (c->p2_stream) (void)hipStreamDestroy(c->p2_stream);
     (void)hipFree(c->overflow);
     (void)hipFree(c->scan_part);
     if (c->copy_stream) (void)hipStreamSynchronize(c->copy_stream);
@@ -722,9 +792,18 @@ int bsdb_fallback_count(bsdb_ctx *c, uint64_t *out) {
     std::lock_guard<std::mutex> g(c->mu);
     HIP_OK(hipSetDevice(c->device));
     HIP_OK(hipDeviceSynchronize());
-    uint32_t v = 0;
-    HIP_OK(hipMemcpy(&v, c->overflow + 2, sizeof(v), hipMemcpyDeviceToHost));
-    *out = v;
+    uint32_t v[8] = {};
+    HIP_OK(hipMemcpy(v, c->overflow, sizeof(v), hipMemcpyDeviceToHost));
+    *out = (uint64_t)v[2] + v[6];
+    return BSDB_OK;
+}
+
+int bsdb_set_pipeline(bsdb_ctx *c, int mode, uint64_t chunks, uint32_t p2_cus) {
+    if (!c || mode < -1 || mode > 1) return BSDB_EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    c->pipe = mode;
+    c->pipe_chunks = chunks;
+    c->pipe_cus = p2_cus;
     return BSDB_OK;
 }
 

@@ -54,6 +54,7 @@ SIGNATURES = [
     ("bsdb_set_histogram_mode", _i, [_vp, _i]),
     ("bsdb_set_frontend", _i, [_vp, _i]),
     ("bsdb_set_chunk_keys", _i, [_vp, _u64]),
+    ("bsdb_set_pipeline", _i, [_vp, _i, _u64, _u32]),
     ("bsdb_fallback_count", _i, [_vp, C.POINTER(_u64)]),
     ("bsdb_fused_status", _i, [_vp, C.POINTER(_u64), C.POINTER(_u64)]),
     ("bsdb_set_profiling", _i, [_vp, _i]),
@@ -190,6 +191,10 @@ class Context:
 
     def set_frontend(self, frontend: int):
         _check("bsdb_set_frontend", lib().bsdb_set_frontend(self._h, frontend))
+
+    def set_pipeline(self, mode: int, chunks: int = 0, p2_cus: int = 0):
+        """Pass 2 of chunk i beside pass 1 of chunk i + 1 (13-byte keys): -1 default, 0 off, 1 on."""
+        _check("bsdb_set_pipeline", lib().bsdb_set_pipeline(self._h, mode, chunks, p2_cus))
 
     def set_chunk_keys(self, n: int):
         _check("bsdb_set_chunk_keys", lib().bsdb_set_chunk_keys(self._h, n))

@@ -215,6 +215,12 @@ int bsdb_set_histogram_mode(bsdb_ctx *ctx, int mode);
  * 1 = the one-tile-per-workgroup kernel with LDS-staged sub-tiles;
  * 2 = the one-tile-per-workgroup kernel with direct reads. */
 int bsdb_set_frontend(bsdb_ctx *ctx, int frontend);
+/* Two-pass path, 13-byte keys: pass 2 of chunk i runs beside pass 1 of chunk
+ * i + 1 (two id buffers; pass 2 keeps `p2_cus` CUs, pass 1 the rest; the
+ * first pass 1 and the last pass 2 use the whole chip).  mode -1 = default,
+ * 0 = serial chunks, 1 = pipelined; chunks / p2_cus 0 = defaults (8 chunks,
+ * CUs / 8).  Results are identical either way. */
+int bsdb_set_pipeline(bsdb_ctx *ctx, int mode, uint64_t chunks, uint32_t p2_cus);
 /* Per-chunk key count of the partitioned path (0 = default). */
 int bsdb_set_chunk_keys(bsdb_ctx *ctx, uint64_t chunk_keys);
 /* Chunks the partitioned path recounted with direct atomics since open

@@ -108,3 +108,45 @@ def test_fused_small_sets_take_two_pass(ctx):
         if n:
             np.testing.assert_array_equal(got.cpu().numpy().view(np.uint32),
                                           O.histogram_fixed(keys[: 13 * n].cpu().numpy(), 13, m))
+
+
+# ---- pass 2 of chunk i beside pass 1 of chunk i + 1 (bsdb_set_pipeline) ----
+
+def pipelined(ctx, keys, n, m, on, chunks=0, p2_cus=0):
+    ctx.set_pipeline(1 if on else 0, chunks, p2_cus)
+    try:
+        return ctx.histogram_fixed(keys, 13, m, n=n)
+    finally:
+        ctx.set_pipeline(-1)
+
+
+@pytest.mark.parametrize("chunks,p2_cus", [(2, 32), (5, 16), (16, 64)])
+def test_pipelined_chunks_equal_oracle(ctx, chunks, p2_cus):
+    n = 3_000_017  # ragged: chunk ends mid-tile, the last tile bounds-checked
+    m = 8_795_859
+    keys = ctx.gen_keys13(31, n)
+    got = pipelined(ctx, keys, n, m, True, chunks, p2_cus).cpu().numpy().view(np.uint32)
+    np.testing.assert_array_equal(got, O.histogram_fixed(keys[: 13 * n].cpu().numpy(), 13, m))
+
+
+def test_pipelined_equals_serial_large(ctx):
+    n = (1 << 30) + 12_345
+    m = n // 1500 + 1
+    keys = ctx.gen_keys13(7_000_000_000, n)
+    a = pipelined(ctx, keys, n, m, True, 8, 32)
+    b = pipelined(ctx, keys, n, m, False)
+    assert torch.equal(a, b)
+    assert int(a.to(torch.int64).sum().item()) == n
+
+
+def test_pipelined_overflow_falls_back(ctx):
+    # one key repeated: both id buffers overflow, each chunk is recounted
+    n = 600_000
+    key = b"abcdefghijklm"
+    keys = torch.from_numpy(np.tile(np.frombuffer(key, np.uint8), n)).cuda()
+    m = 8_795_859
+    before = ctx.fallback_count()
+    counts = pipelined(ctx, keys, n, m, True, 4, 32).cpu().numpy().view(np.uint32)
+    b = O.bucket(O.spooky_short(key)[0], m)
+    assert counts[b] == n and counts.sum() == n
+    assert ctx.fallback_count() >= before + 4
