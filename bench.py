@@ -324,13 +324,25 @@ def main():
 
     from bsdb_amd import Context
     ctx = Context(dev)
+    collective = "rccl-in-abi"
     if world > 1 and args.backend == "nccl":
         # the one collective runs inside the C ABI (bsdb_dev_histogram_finalize,
         # RCCL over xGMI); the 128-byte communicator id travels over the
-        # process group once, outside the timed region
-        obj = [Context.comm_unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(obj, src=0)
-        ctx.comm_init(world, rank, obj[0])
+        # process group once, outside the timed region.  If the library's own
+        # communicator cannot be set up on every rank, the same all-reduce
+        # runs through torch.distributed (also RCCL), and the line says so.
+        ok_local = 1
+        try:
+            obj = [Context.comm_unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(obj, src=0)
+            ctx.comm_init(world, rank, obj[0])
+        except Exception as e:  # recorded in the line, not hidden
+            print(f"[bench r{rank}] bsdb_comm_init failed: {e!r}", file=sys.stderr, flush=True)
+            ok_local = 0
+        flag = torch.tensor([ok_local], dtype=torch.int32, device="cuda")
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        if int(flag.item()) == 0:
+            collective = "torch.distributed all_reduce (RCCL)"
     if args.mode:
         ctx.set_histogram_mode(args.mode)
     if args.chunk:
@@ -360,6 +372,11 @@ def main():
             h = counts.cpu()
             dist.all_reduce(h)
             counts.copy_(h)
+            ctx.edge_offsets(counts, out=E)
+        elif world > 1 and collective != "rccl-in-abi":
+            counts.zero_()
+            ctx.histogram_fixed(keys, KEY_LEN, m, counts=counts, n=nloc)
+            dist.all_reduce(counts)
             ctx.edge_offsets(counts, out=E)
         elif world > 1:
             counts.zero_()
@@ -480,6 +497,7 @@ def main():
                 "keys_per_gpu": nloc if world == 1 else f"~{n // world}",
                 "parallelism": f"key-shard x{world}" + ((" + RCCL all-reduce(histogram)" if args.backend == "nccl"
                                                          else " + gloo all-reduce (rehearsal)") if world > 1 else ""),
+                "collective": (collective if args.backend == "nccl" else "gloo") if world > 1 else None,
                 "histogram_mode": "atomic" if args.mode == 2 else "partitioned-2pass",
             },
             "roofline": {

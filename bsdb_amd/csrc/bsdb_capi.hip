@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <dlfcn.h>
+#include <sched.h>
 #include <fcntl.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
