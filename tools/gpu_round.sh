@@ -1,5 +1,6 @@
 #!/bin/bash
-# One GPU call: the whole -m gpu suite, the bench line, the rocprofv3 kernel-trace summary.
+# One GPU call: the whole -m gpu suite, the bench line, the rocprofv3 kernel-trace summary
+# of the headline alone (--no-full-build: its pass-1 launches are the bench's roofline launches).
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 OUT=gpurun_out/${TAG:-round}; mkdir -p $OUT
@@ -11,6 +12,6 @@ tail -n 1 $OUT/smoke.log
 timeout -k 10 400 python -u bench.py --steps 10 --warmup 3 > $OUT/bench.json 2> $OUT/bench.err || { tail -n 20 $OUT/bench.err; exit 2; }
 tail -n 1 $OUT/bench.json | cut -c1-400
 [ -n "$NOPROF" ] && exit 0
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/prof -o bench --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu > $OUT/prof_bench.json 2> $OUT/prof_bench.err || { tail -n 20 $OUT/prof_bench.err; exit 3; }
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/prof -o bench --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu --no-full-build > $OUT/prof_bench.json 2> $OUT/prof_bench.err || { tail -n 20 $OUT/prof_bench.err; exit 3; }
 find $OUT/prof -name "*kernel_stats.csv" -exec cp {} $OUT/kernel_stats.csv \;
 head -n 12 $OUT/kernel_stats.csv | cut -c1-160
