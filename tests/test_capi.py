@@ -48,6 +48,9 @@ def test_host_only_calls(lib):
     assert lib.bsdb_num_buckets(13_193_787_549) == 8_795_859
     assert lib.bsdb_num_buckets(0) == 1
     assert lib.bsdb_abi_version() == 3
+    hdr = open(os.path.join(ROOT, "include", "bsdb_mi355x.h")).read()
+    assert f"#define BSDB_ABI_VERSION {lib.bsdb_abi_version()}" in hdr
+
     lib.bsdb_strerror.restype = C.c_char_p
     assert lib.bsdb_strerror(-17) == b"duplicate key signature"
     lib.bsdb_open.argtypes = [C.c_int, C.POINTER(C.c_void_p)]
@@ -68,3 +71,10 @@ def test_var_host_argument_checks():
                 np.zeros(0, np.uint64)):             # no n+1 entries
         with pytest.raises(ValueError):
             Context._var_host_args(blob, bad)
+
+
+def test_graft_entry_build_checks_the_header_abi():
+    # __graft_entry__.build() compares the library's ABI with the header's
+    # (a hard-coded number there once went stale and failed the build check)
+    src = open(os.path.join(ROOT, "__graft_entry__.py")).read()
+    assert "bsdb_abi_version() ==" in src and "BSDB_ABI_VERSION" in src
