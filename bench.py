@@ -332,13 +332,21 @@ def main():
         # communicator cannot be set up on every rank, the same all-reduce
         # runs through torch.distributed (also RCCL), and the line says so.
         ok_local = 1
-        try:
-            obj = [Context.comm_unique_id() if rank == 0 else None]
-            dist.broadcast_object_list(obj, src=0)
-            ctx.comm_init(world, rank, obj[0])
-        except Exception as e:  # recorded in the line, not hidden
-            print(f"[bench r{rank}] bsdb_comm_init failed: {e!r}", file=sys.stderr, flush=True)
+        obj = [None]
+        if rank == 0:
+            try:
+                obj[0] = Context.comm_unique_id()
+            except Exception as e:  # (RCCL not loadable by the library)
+                print(f"[bench r0] bsdb_comm_unique_id failed: {e!r}", file=sys.stderr, flush=True)
+        dist.broadcast_object_list(obj, src=0)  # every rank joins, id or None
+        if obj[0] is None:
             ok_local = 0
+        else:
+            try:
+                ctx.comm_init(world, rank, obj[0])
+            except Exception as e:  # recorded in the line, not hidden
+                print(f"[bench r{rank}] bsdb_comm_init failed: {e!r}", file=sys.stderr, flush=True)
+                ok_local = 0
         flag = torch.tensor([ok_local], dtype=torch.int32, device="cuda")
         dist.all_reduce(flag, op=dist.ReduceOp.MIN)
         if int(flag.item()) == 0:
