@@ -153,18 +153,26 @@ int mph_build_index(bsdb_ctx *c, uint64_t n, uint32_t width, const uint64_t *h_a
         for (void *q : {rank, addr, index, v8, vl, index_a}) (void)hipFree(q);
         return close_all(rc);
     };
-    if (hipMalloc(&rank, nn * 8) != hipSuccess) return free_all(BSDB_ENOMEM);
+    if (hipMalloc(&rank, nn * 8) != hipSuccess || hipMalloc(&addr, nn * 8) != hipSuccess)
+        return free_all(BSDB_ENOMEM);
+    // the record addresses go up while the MPHF builds (the solve leaves PCIe idle)
+    int addr_rc = BSDB_OK;
+    std::thread addr_up([&, dev = c->device] { addr_rc = h2d_pageable(dev, addr, h_addr, n * 8); });
     bsdb_mph *p = nullptr;
     int rc = mph_build_locked(c, n, width, &p, (int64_t *)rank, hash_dev);
+    addr_up.join();
     if (rc) return free_all(rc);
-    if (hipMalloc(&addr, nn * 8) != hipSuccess || hipMalloc(&index, nn * 8) != hipSuccess ||
+    if (addr_rc) {
+        mph_release(p);
+        return free_all(addr_rc);
+    }
+    if (hipMalloc(&index, nn * 8) != hipSuccess ||
         (approx && (hipMalloc(&v8, nn * 8) != hipSuccess || hipMalloc(&vl, nn) != hipSuccess ||
                     hipMalloc(&index_a, nn * 8) != hipSuccess))) {
         mph_release(p);
         return free_all(BSDB_ENOMEM);
     }
-    bool ok = hipMemcpyAsync(addr, h_addr, n * 8, hipMemcpyHostToDevice, c->stream) == hipSuccess &&
-              hipMemsetAsync(index, 0, nn * 8, c->stream) == hipSuccess;
+    bool ok = hipMemsetAsync(index, 0, nn * 8, c->stream) == hipSuccess;
     if (ok && approx)
         ok = hipMemcpyAsync(v8, h_value8, n * 8, hipMemcpyHostToDevice, c->stream) == hipSuccess &&
              hipMemcpyAsync(vl, h_vlen, n, hipMemcpyHostToDevice, c->stream) == hipSuccess &&
@@ -271,13 +279,16 @@ int write_chunks(FILE *f, const void *d_src, uint64_t bytes, hipStream_t s) {
     return BSDB_OK;
 }
 
-// The same for up to two files at once (index.db and index_a.db), each on a
-// thread of its own with its own stream and two pinned 128 MiB staging
-// buffers: chunk i+1 comes over PCIe while chunk i is written.  The device
-// data must be complete (the caller has synchronised its stream).
+// The same, fast: each file is cut into 32 MiB writes (the reference writes
+// at most 128 MiB at a time) that up to 8 threads issue at their offsets
+// (pwrite), each thread staging its pieces through two pooled pinned buffers
+// of its own (the DMA of its next piece runs while it writes the current one).
+// One thread's fwrite stream ran at ~3 GB/s of page-cache copies; the threads
+// share the copies.  The device data must be complete (the caller has
+// synchronised its stream).
 int write_files(int device, FILE *const *files, const void *const *d_srcs, int nfiles, uint64_t bytes) {
     constexpr uint64_t CHUNK = 128ULL << 20;
-    if (bytes <= 2 * CHUNK) {  // small: the plain path (no pinned allocation)
+    if (bytes <= 2 * CHUNK) {  // small: the plain path (no pinned staging)
         hipStream_t s0 = nullptr;
         for (int i = 0; i < nfiles; ++i) {
             const int rc = write_chunks(files[i], d_srcs[i], bytes, s0);
@@ -285,48 +296,69 @@ int write_files(int device, FILE *const *files, const void *const *d_srcs, int n
         }
         return BSDB_OK;
     }
-    std::vector<int> rcs(nfiles, BSDB_OK);
-    auto one = [&](int i) {
-        int &rc = rcs[i];
-        hipStream_t st = nullptr;
-        void *buf[2] = {nullptr, nullptr};
-        if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess ||
-            hipHostMalloc(&buf[0], CHUNK, hipHostMallocDefault) != hipSuccess ||
-            hipHostMalloc(&buf[1], CHUNK, hipHostMallocDefault) != hipSuccess) {
-            rc = BSDB_ENOMEM;
-        } else {
-            const uint8_t *src = (const uint8_t *)d_srcs[i];
-            const uint64_t nch = (bytes + CHUNK - 1) / CHUNK;
-            auto issue = [&](uint64_t c) {
-                const uint64_t o = c * CHUNK, k = std::min(CHUNK, bytes - o);
-                return hipMemcpyAsync(buf[c & 1], src + o, k, hipMemcpyDeviceToHost, st) == hipSuccess;
+    cpu_set_t cs_set;
+    int ncpu = 1;
+    if (sched_getaffinity(0, sizeof(cs_set), &cs_set) == 0) ncpu = CPU_COUNT(&cs_set);
+    const uint64_t npieces = (bytes + XFER_PIECE - 1) / XFER_PIECE;
+    const uint64_t T = std::max<uint64_t>(1, std::min<uint64_t>({(uint64_t)8, (uint64_t)ncpu, npieces}));
+    for (int fi = 0; fi < nfiles; ++fi) {
+        if (fflush(files[fi]) != 0) return BSDB_EFILE;
+        const int fd = fileno(files[fi]);
+        const off_t base = ftello(files[fi]);
+        if (fd < 0 || base < 0) return BSDB_EFILE;
+        const uint8_t *src = (const uint8_t *)d_srcs[fi];
+        std::atomic<int> rc{BSDB_OK};
+        auto work = [&](uint64_t t) {
+            hipStream_t st = nullptr;
+            void *pin[2] = {nullptr, nullptr};
+            hipEvent_t done[2] = {nullptr, nullptr};
+            bool ok = hipSetDevice(device) == hipSuccess && hipStreamCreateWithFlags(&st, hipStreamNonBlocking) == hipSuccess;
+            for (int i = 0; i < 2 && ok; ++i)
+                ok = (pin[i] = pinned_pool().take()) != nullptr &&
+                     hipEventCreateWithFlags(&done[i], hipEventDisableTiming) == hipSuccess;
+            auto len_of = [&](uint64_t j) { return std::min<uint64_t>(XFER_PIECE, bytes - j * XFER_PIECE); };
+            auto issue = [&](uint64_t j, int i) {
+                return hipMemcpyAsync(pin[i], src + j * XFER_PIECE, len_of(j), hipMemcpyDeviceToHost, st) == hipSuccess &&
+                       hipEventRecord(done[i], st) == hipSuccess;
             };
-            bool ok = issue(0) && hipStreamSynchronize(st) == hipSuccess;
-            for (uint64_t c = 0; ok && c < nch; ++c) {
-                if (c + 1 < nch) ok = issue(c + 1);  // overlaps the write of chunk c
-                const uint64_t k = std::min(CHUNK, bytes - c * CHUNK);
-                if (ok && fwrite(buf[c & 1], 1, k, files[i]) != k) {
-                    rc = BSDB_EFILE;
-                    ok = false;
+            if (ok && t < npieces) ok = issue(t, 0);
+            int k = 0;
+            for (uint64_t j = t; ok && j < npieces; j += T, ++k) {
+                const int i = k & 1;
+                if (j + T < npieces) ok = issue(j + T, i ^ 1);
+                ok = ok && hipEventSynchronize(done[i]) == hipSuccess;
+                if (!ok) break;
+                const uint64_t len = len_of(j);
+                uint64_t w = 0;
+                while (w < len) {
+                    const ssize_t r = pwrite(fd, (const uint8_t *)pin[i] + w, len - w, base + (off_t)(j * XFER_PIECE + w));
+                    if (r <= 0) {
+                        rc.store(BSDB_EFILE);
+                        ok = false;
+                        break;
+                    }
+                    w += (uint64_t)r;
                 }
-                if (hipStreamSynchronize(st) != hipSuccess && ok) ok = false;
             }
-            if (!ok && rc == BSDB_OK) rc = BSDB_EIO;
-        }
-        if (st) {
-            (void)hipStreamSynchronize(st);
-            (void)hipStreamDestroy(st);
-        }
-        for (void *b : buf)
-            if (b) (void)hipHostFree(b);
-    };
-    std::vector<std::thread> th;
-    for (int i = 1; i < nfiles; ++i) th.emplace_back(one, i);
-    one(0);
-    for (auto &t : th) t.join();
+            if (st) ok = hipStreamSynchronize(st) == hipSuccess && ok;
+            if (!ok) {
+                int expect = BSDB_OK;
+                rc.compare_exchange_strong(expect, BSDB_EIO);
+            }
+            for (int i = 0; i < 2; ++i) {
+                pinned_pool().give(pin[i]);
+                if (done[i]) (void)hipEventDestroy(done[i]);
+            }
+            if (st) (void)hipStreamDestroy(st);
+        };
+        std::vector<std::thread> th;
+        for (uint64_t t = 1; t < T; ++t) th.emplace_back(work, t);
+        work(0);
+        for (auto &x : th) x.join();
+        if (rc.load()) return rc.load();
+        if (fseeko(files[fi], base + (off_t)bytes, SEEK_SET) != 0) return BSDB_EFILE;  // the FILE's position after the data
+    }
     (void)hipSetDevice(device);
-    for (int rc : rcs)
-        if (rc) return rc;
     return BSDB_OK;
 }
 

@@ -20,68 +20,6 @@
 
 namespace {
 
-// Device -> pageable host copy at host-memory speed.  A plain hipMemcpy into
-// pageable memory is staged by one runtime thread (and pays the destination's
-// first-touch page faults there): ~3 GB/s measured for C4's 17.6 GB slices,
-// so every other pass waited ~2 s for the copy of the pass before last.  Here
-// T threads each take a contiguous share: the DMA of piece k+1 into one of its
-// two pinned buffers runs while the thread copies piece k out of the other.
-constexpr size_t D2H_PIECE = 32ull << 20;
-
-int d2h_pageable(int dev, void *dst, const void *src, size_t bytes) {
-    if (bytes == 0) return BSDB_OK;
-    cpu_set_t cs_set;
-    int ncpu = 1;
-    if (sched_getaffinity(0, sizeof(cs_set), &cs_set) == 0) ncpu = CPU_COUNT(&cs_set);
-    const size_t T = std::max<size_t>(1, std::min<size_t>({(size_t)8, (size_t)ncpu, bytes / (2 * D2H_PIECE) + 1}));
-    std::atomic<int> rc{BSDB_OK};
-    auto work = [&](size_t lo, size_t hi) {
-        hipStream_t cs = nullptr;
-        void *pin[2] = {nullptr, nullptr};
-        hipEvent_t done[2] = {nullptr, nullptr};
-        auto fail = [&]() { rc.store(BSDB_EIO); };
-        if (hipSetDevice(dev) != hipSuccess || hipStreamCreateWithFlags(&cs, hipStreamNonBlocking) != hipSuccess) {
-            fail();
-            return;
-        }
-        bool ok = true;
-        for (int i = 0; i < 2 && ok; ++i)
-            ok = hipHostMalloc(&pin[i], D2H_PIECE, hipHostMallocDefault) == hipSuccess &&
-                 hipEventCreateWithFlags(&done[i], hipEventDisableTiming) == hipSuccess;
-        auto issue = [&](size_t off, int i) {
-            const size_t len = std::min(D2H_PIECE, hi - off);
-            return hipMemcpyAsync(pin[i], (const uint8_t *)src + off, len, hipMemcpyDeviceToHost, cs) == hipSuccess &&
-                   hipEventRecord(done[i], cs) == hipSuccess;
-        };
-        if (ok && lo < hi) ok = issue(lo, 0);
-        int k = 0;
-        for (size_t off = lo; ok && off < hi; off += D2H_PIECE, ++k) {
-            const int i = k & 1;
-            if (off + D2H_PIECE < hi) ok = issue(off + D2H_PIECE, i ^ 1);  // the next piece's DMA first
-            if (!ok || hipEventSynchronize(done[i]) != hipSuccess) {
-                ok = false;
-                break;
-            }
-            memcpy((uint8_t *)dst + off, pin[i], std::min(D2H_PIECE, hi - off));
-        }
-        if (!ok) fail();
-        (void)hipStreamSynchronize(cs);
-        for (int i = 0; i < 2; ++i) {
-            if (pin[i]) (void)hipHostFree(pin[i]);
-            if (done[i]) (void)hipEventDestroy(done[i]);
-        }
-        (void)hipStreamDestroy(cs);
-    };
-    std::vector<std::thread> th;
-    const size_t share = (bytes / T + 4095) & ~(size_t)4095;  // page-aligned shares of the destination
-    for (size_t t = 0; t < T; ++t) {
-        const size_t lo = std::min(bytes, t * share), hi = std::min(bytes, lo + share);
-        if (lo < hi) th.emplace_back(work, lo, hi);
-    }
-    for (auto &x : th) x.join();
-    return rc.load();
-}
-
 // device bytes per key of one pass: sorted signature + position payload, plus
 // the pass's index slots (twice when they go to host memory: one buffer is
 // copied out while the next pass fills the other)
