@@ -185,18 +185,10 @@ int grow(void **p, size_t *have, size_t need) {
     return BSDB_OK;
 }
 
-// Copies between device memory and PAGEABLE host memory at host-memory speed.
-// A plain hipMemcpy with pageable memory is staged by one runtime thread (which
-// also takes the first-touch page faults of a fresh destination): ~3 GB/s was
-// measured for C4's 17.6 GB index slices.  Here up to 8 threads each take a
-// contiguous, page-aligned share and stream it through two pinned 32 MiB
-// buffers of their own: the DMA of one piece runs while the thread copies the
-// other (D2H: the next piece lands while the previous one is copied out; H2D:
-// the next piece is copied in while the previous one is DMAed).  Synchronous.
+// Pinned 32 MiB pieces, pooled for the life of the process: the index-file
+// writer stages its pieces through them (write_files, capi_mph.hip).
 constexpr size_t XFER_PIECE = 32ull << 20;
 
-// Pinned pieces are pooled for the life of the process (pinning 64 MiB per
-// thread per call cost more than copying a 256 MiB feed batch).
 struct PinnedPool {
     std::mutex mu;
     std::vector<void *> free_list;
@@ -223,71 +215,24 @@ PinnedPool &pinned_pool() {
     return *pool;
 }
 
-template <bool D2H>
-int pageable_copy(int dev, void *dst, const void *src, size_t bytes) {
+// A synchronous copy on a stream of the calling thread (the pass slices'
+// copier threads, the address upload beside the MPHF build).  The runtime's
+// own pageable path: a parallel pinned-bounce copy was measured 2 % slower
+// for C4's 17.6 GB slices and 37 % slower for host-key uploads.
+int copy_on_own_stream(int dev, void *dst, const void *src, size_t bytes, hipMemcpyKind kind) {
     if (bytes == 0) return BSDB_OK;
-    if (bytes < 2 * XFER_PIECE) {  // small: the runtime's own path
-        if (hipSetDevice(dev) != hipSuccess) return BSDB_EIO;
-        return hipMemcpy(dst, src, bytes, D2H ? hipMemcpyDeviceToHost : hipMemcpyHostToDevice) == hipSuccess
-                   ? BSDB_OK : BSDB_EIO;
-    }
-    cpu_set_t cs_set;
-    int ncpu = 1;
-    if (sched_getaffinity(0, sizeof(cs_set), &cs_set) == 0) ncpu = CPU_COUNT(&cs_set);
-    const size_t T = std::max<size_t>(1, std::min<size_t>({(size_t)8, (size_t)ncpu, bytes / (2 * XFER_PIECE)}));
-    std::atomic<int> rc{BSDB_OK};
-    auto work = [&](size_t lo, size_t hi) {
-        hipStream_t cs = nullptr;
-        void *pin[2] = {nullptr, nullptr};
-        hipEvent_t done[2] = {nullptr, nullptr};
-        bool ok = hipSetDevice(dev) == hipSuccess && hipStreamCreateWithFlags(&cs, hipStreamNonBlocking) == hipSuccess;
-        for (int i = 0; i < 2 && ok; ++i)
-            ok = (pin[i] = pinned_pool().take()) != nullptr &&
-                 hipEventCreateWithFlags(&done[i], hipEventDisableTiming) == hipSuccess;
-        auto len_at = [&](size_t off) { return std::min(XFER_PIECE, hi - off); };
-        if (D2H) {
-            auto issue = [&](size_t off, int i) {
-                return hipMemcpyAsync(pin[i], (const uint8_t *)src + off, len_at(off), hipMemcpyDeviceToHost, cs) ==
-                           hipSuccess && hipEventRecord(done[i], cs) == hipSuccess;
-            };
-            if (ok && lo < hi) ok = issue(lo, 0);
-            int k = 0;
-            for (size_t off = lo; ok && off < hi; off += XFER_PIECE, ++k) {
-                const int i = k & 1;
-                if (off + XFER_PIECE < hi) ok = issue(off + XFER_PIECE, i ^ 1);  // the next piece's DMA first
-                ok = ok && hipEventSynchronize(done[i]) == hipSuccess;
-                if (ok) memcpy((uint8_t *)dst + off, pin[i], len_at(off));
-            }
-        } else {
-            int k = 0;
-            for (size_t off = lo; ok && off < hi; off += XFER_PIECE, ++k) {
-                const int i = k & 1;
-                if (k >= 2) ok = hipEventSynchronize(done[i]) == hipSuccess;  // buffer i's last DMA done
-                if (!ok) break;
-                memcpy(pin[i], (const uint8_t *)src + off, len_at(off));
-                ok = hipMemcpyAsync((uint8_t *)dst + off, pin[i], len_at(off), hipMemcpyHostToDevice, cs) == hipSuccess &&
-                     hipEventRecord(done[i], cs) == hipSuccess;
-            }
-        }
-        if (cs) ok = hipStreamSynchronize(cs) == hipSuccess && ok;
-        if (!ok) rc.store(BSDB_EIO);
-        for (int i = 0; i < 2; ++i) {
-            pinned_pool().give(pin[i]);  // (its DMAs finished: the stream was synchronised)
-            if (done[i]) (void)hipEventDestroy(done[i]);
-        }
-        if (cs) (void)hipStreamDestroy(cs);
-    };
-    std::vector<std::thread> th;
-    const size_t share = (bytes / T + 4095) & ~(size_t)4095;  // page-aligned shares
-    for (size_t t = 0; t < T; ++t) {
-        const size_t lo = std::min(bytes, t * share), hi = std::min(bytes, lo + share);
-        if (lo < hi) th.emplace_back(work, lo, hi);
-    }
-    for (auto &x : th) x.join();
-    return rc.load();
+    hipStream_t s = nullptr;
+    bool ok = hipSetDevice(dev) == hipSuccess && hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess &&
+              hipMemcpyAsync(dst, src, bytes, kind, s) == hipSuccess && hipStreamSynchronize(s) == hipSuccess;
+    if (s) (void)hipStreamDestroy(s);
+    return ok ? BSDB_OK : BSDB_EIO;
 }
-int d2h_pageable(int dev, void *dst, const void *src, size_t bytes) { return pageable_copy<true>(dev, dst, src, bytes); }
-int h2d_pageable(int dev, void *dst, const void *src, size_t bytes) { return pageable_copy<false>(dev, dst, src, bytes); }
+int d2h_pageable(int dev, void *dst, const void *src, size_t bytes) {
+    return copy_on_own_stream(dev, dst, src, bytes, hipMemcpyDeviceToHost);
+}
+int h2d_pageable(int dev, void *dst, const void *src, size_t bytes) {
+    return copy_on_own_stream(dev, dst, src, bytes, hipMemcpyHostToDevice);
+}
 
 // NULL is the HIP null stream (torch's default stream reports handle 0), not
 // the context's private stream, which only the host-buffer entry points use.
@@ -1535,8 +1480,8 @@ static uint64_t fixed_batch(uint32_t key_len, uint64_t bytes) {
 static int upload_fixed(bsdb_ctx *c, FeedSlot &f, const uint8_t *h_keys, uint32_t key_len, uint64_t k0, uint64_t k1) {
     int rc = grow(&f.buf[0], &f.cap[0], (size_t)(k1 - k0) * key_len + 16);
     if (rc) return rc;
-    // (feed_batches waited for the slot's last compute: a host-synchronous copy is safe)
-    return h2d_pageable(c->device, f.buf[0], h_keys + k0 * key_len, (size_t)(k1 - k0) * key_len);
+    HIP_OK(hipMemcpyAsync(f.buf[0], h_keys + k0 * key_len, (k1 - k0) * key_len, hipMemcpyHostToDevice, c->copy_stream));
+    return BSDB_OK;
 }
 
 // Batches of variable-length keys: [k0, k1) with at most VAR_BATCH_KEYS keys
