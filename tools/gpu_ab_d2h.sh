@@ -1,3 +1,10 @@
+#!/bin/bash
+# A/B recorded in DESIGN §3.1 (profiles/r3/d2h/ab_bounce_vs_runtime.jsonl): the
+# C4 exact build with the pass slices copied by the in-tree library against a
+# variant build bsdb_amd/libbsdb_rtd2h.so (the same sources with d2h_pageable
+# replaced by one runtime hipMemcpyAsync; built from a scratch copy of
+# bsdb_amd/csrc, not kept).  At the time of the A/B the in-tree library used
+# the parallel pinned-bounce copy, now replaced by the runtime copy.
 set -o pipefail
 mkdir -p gpurun_out/abd2h
 for i in 1 2; do
