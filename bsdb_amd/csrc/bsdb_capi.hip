@@ -1641,4 +1641,5 @@ int bsdb_hash_var(bsdb_ctx *c, const uint8_t *h_blob, const uint64_t *h_off, uin
 #include "capi_mph.hip"
 #include "capi_multi.hip"
 #include "capi_passes.hip"
+#include "capi_builder.hip"
 #include "capi_kv.hip"

@@ -11,9 +11,10 @@
 // record (SCK:62-66, BKV:98-103) and re-scans the files once per index pass.
 // Here each partition file is mapped and parsed by a host thread into packed
 // arrays -- key blob (+ offsets unless every key has one length), record
-// address, the first <= 8 value bytes and their count (index_a.db) -- in
-// partition order, ready for the one-call build (F2: ranks from the solve,
-// index slots scattered on the device, one write of each file).
+// address, the first <= 8 value bytes and their count (index_a.db).
+// bsdb_kv_scan returns them all (partition order); bsdb_kv_build_index hands
+// each partition to the streaming builder as soon as it is parsed (bounded
+// host memory; index slots from the solve, no rescan).
 //
 // Formats (the two uncompressed kv.db layouts):
 //   0 compact  SimpleCompactKVWriter: records [kLen u8][vLen u16 BE][key][value]
@@ -234,24 +235,79 @@ int bsdb_kv_records_free(bsdb_kv_records *r) {
     return BSDB_OK;
 }
 
-// W:91-155 from the data files: scan, then the one-call build (hash, GOV
-// build with ranks and checksum bits, index scatter, index.db / index_a.db)
+// W:91-155 from the data files, in bounded host memory: the partitions are
+// scanned by host threads (one partition per thread at a time) and each one's
+// keys go into a builder (capi_builder.hip: keys into HBM, addresses and value
+// bytes kept in host memory) as soon as it is parsed, in whatever order the
+// threads finish (the files do not depend on it); then the bucket-range-pass
+// build writes index.db / index_a.db.  Host memory: the records' addresses
+// (+ 9 B per record in approximate mode) and the partitions in flight, not
+// every key.  Device capacity is reserved from the first partition's key
+// bytes per file byte, extrapolated over every file (growth covers the rest).
 int bsdb_kv_build_index(bsdb_ctx *c, const char *kv_base, int partitions, int format, uint32_t block_size,
                         int threads, uint32_t width, int approximate, const char *index_path, const char *index_a_path,
                         bsdb_mph **out) {
-    if (!c || !out || !index_path || width > 64) return BSDB_EINVAL;
+    if (!c || !out || !index_path || width > 64 || !kv_base || partitions < 1 || (format != 0 && format != 1) ||
+        (format == 1 && (block_size == 0 || block_size % KV_PAGE)) || (approximate && !index_a_path))
+        return BSDB_EINVAL;
     *out = nullptr;
-    bsdb_kv_records *r = nullptr;
-    int rc = bsdb_kv_scan(kv_base, partitions, format, block_size, threads, &r);
+    auto scan_one = [&](int p, KvPart &part) {
+        Mapped m;
+        const std::string path = std::string(kv_base) + "." + std::to_string(p);  // PKV:79-81
+        int rc = map_file(path, m);
+        if (!rc) rc = format == 0 ? scan_compact(m, (uint64_t)p, part) : scan_blocked(m, (uint64_t)p, block_size, part);
+        return rc;
+    };
+    uint64_t file_bytes = 0, first_bytes = 0;
+    for (int p = 0; p < partitions; ++p) {
+        struct stat st;
+        const std::string path = std::string(kv_base) + "." + std::to_string(p);
+        if (stat(path.c_str(), &st) != 0) return BSDB_EFILE;
+        file_bytes += (uint64_t)st.st_size;
+        if (p == 0) first_bytes = (uint64_t)st.st_size;
+    }
+    KvPart first;
+    int rc = scan_one(0, first);
     if (rc) return rc;
-    std::unique_ptr<bsdb_kv_records, int (*)(bsdb_kv_records *)> guard(r, bsdb_kv_records_free);
-    const uint64_t *v8 = approximate ? r->value8.data() : nullptr;
-    const uint8_t *vl = approximate ? r->vlen.data() : nullptr;
-    if (r->fixed_len)
-        return bsdb_mph_build_index_fixed(c, r->blob.data(), r->fixed_len, r->n, width, r->addr.data(), v8, vl,
-                                          approximate, index_path, index_a_path, out);
-    return bsdb_mph_build_index_var(c, r->blob.data(), r->off.data(), r->n, width, r->addr.data(), v8, vl, approximate,
-                                    index_path, index_a_path, out);
+    const double per_byte_keys = first_bytes ? (double)first.addr.size() / (double)first_bytes : 0.0;
+    const double per_byte_blob = first_bytes ? (double)first.blob.size() / (double)first_bytes : 0.0;
+    bsdb_builder *b = nullptr;
+    if ((rc = builder_open(c, 0, (uint64_t)(per_byte_keys * (double)file_bytes * 1.02) + 1024,
+                           (uint64_t)(per_byte_blob * (double)file_bytes * 1.02) + 65536, approximate, 0, 0, &b)))
+        return rc;
+    std::unique_ptr<bsdb_builder, int (*)(bsdb_builder *)> guard(b, bsdb_builder_free);
+    std::mutex add_mu;
+    auto add_part = [&](KvPart &part) {
+        const uint64_t k = part.addr.size();
+        std::vector<uint64_t> off(k + 1);
+        off[0] = 0;
+        std::copy(part.len_end.begin(), part.len_end.end(), off.begin() + 1);
+        std::lock_guard<std::mutex> g(add_mu);
+        return builder_add(b, k, part.addr.data(), part.value8.data(), part.vlen.data(),
+                           [&] { return builder_add_var_locked(b, part.blob.data(), off.data(), k); });
+    };
+    if ((rc = add_part(first))) return rc;
+    first = KvPart();
+    const int T = std::max(1, std::min(threads > 0 ? threads : (int)std::thread::hardware_concurrency(), partitions - 1));
+    std::atomic<int> next{1};
+    std::atomic<int> err{BSDB_OK};
+    auto worker = [&] {
+        for (int p; !err.load() && (p = next.fetch_add(1)) < partitions;) {
+            KvPart part;
+            int r = scan_one(p, part);
+            if (!r) r = add_part(part);
+            if (r) {
+                int expect = BSDB_OK;
+                err.compare_exchange_strong(expect, r);
+            }
+        }
+    };
+    std::vector<std::thread> th;
+    for (int t = 1; t < T; ++t) th.emplace_back(worker);
+    worker();
+    for (auto &t : th) t.join();
+    if ((rc = err.load())) return rc;
+    return bsdb_builder_finish(b, width, 0, index_path, index_a_path, out, nullptr);
 }
 
 }  // extern "C"

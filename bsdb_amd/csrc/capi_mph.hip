@@ -126,6 +126,19 @@ int mph_build(bsdb_ctx *c, uint64_t n, uint32_t width, bsdb_mph **out, HashDev &
 
 int write_files(int device, FILE *const *files, const void *const *d_srcs, int nfiles, uint64_t bytes);
 
+}  // namespace
+
+// capi_builder.hip: the same files by bucket-range passes (the F2 entry
+// points fall back to it when their one-shot build does not fit the device)
+static int host_passes_build(bsdb_ctx *c, const uint8_t *h_keys, uint32_t key_len, const uint8_t *h_blob,
+                             const uint64_t *h_off, uint64_t n, uint32_t width, const uint64_t *h_addr,
+                             uint64_t addr_base, uint64_t addr_stride, const uint64_t *h_value8, const uint8_t *h_vlen,
+                             int approximate, uint32_t passes, const char *index_path, const char *index_a_path,
+                             bsdb_mph **out, uint32_t *passes_used);
+static bool one_shot_fits(bsdb_ctx *c, uint64_t n, bool approx);
+
+namespace {
+
 // F2: build + index.db / index_a.db from the solve's ranks, no rescan.  The
 // slots are the same as bsdb_index_* passes over the same records give.
 template <class HashDev>
@@ -429,6 +442,9 @@ int bsdb_mph_build_index_fixed(bsdb_ctx *c, const uint8_t *h_keys, uint32_t key_
         (n && (!h_keys || !h_addr || (approximate && (!h_value8 || !h_vlen)))))
         return BSDB_EINVAL;
     *out = nullptr;
+    if (!one_shot_fits(c, n, approximate != 0))
+        return host_passes_build(c, h_keys, key_len, nullptr, nullptr, n, width, h_addr, 0, 0, h_value8, h_vlen,
+                                 approximate, 0, index_path, index_a_path, out, nullptr);
     return mph_build_index(c, n, width, h_addr, h_value8, h_vlen, approximate != 0, index_path, index_a_path, out,
                            [&](uint64_t *d_sig) { return host_hash_fixed_dev(c, h_keys, key_len, n, 0, d_sig); });
 }
@@ -440,6 +456,9 @@ int bsdb_mph_build_index_var(bsdb_ctx *c, const uint8_t *h_blob, const uint64_t 
         (n && (!h_blob || !h_off || !h_addr || (approximate && (!h_value8 || !h_vlen)))))
         return BSDB_EINVAL;
     *out = nullptr;
+    if (!one_shot_fits(c, n, approximate != 0))
+        return host_passes_build(c, nullptr, 0, h_blob, h_off, n, width, h_addr, 0, 0, h_value8, h_vlen, approximate, 0,
+                                 index_path, index_a_path, out, nullptr);
     return mph_build_index(c, n, width, h_addr, h_value8, h_vlen, approximate != 0, index_path, index_a_path, out,
                            [&](uint64_t *d_sig) { return host_hash_var_dev(c, h_blob, h_off, n, 0, d_sig); });
 }
@@ -615,10 +634,15 @@ int bsdb_index_open(bsdb_mph *p, int approximate, uint64_t pass_cache_bytes, con
     if (index_a_path) ix->fa = fopen(index_a_path, "wb");
     bool ok = ix->f && (!index_a_path || ix->fa);
     if (ok && ix->pass_size) {
-        std::lock_guard<std::mutex> g(p->c->mu);
-        ok = hipSetDevice(p->c->device) == hipSuccess && hipMalloc(&ix->d_index, ix->pass_size * 8) == hipSuccess &&
-             (!ix->approx || hipMalloc(&ix->d_index_a, ix->pass_size * 8) == hipSuccess);
-        if (!ok) {
+        bool alloc_ok;
+        {
+            std::lock_guard<std::mutex> g(p->c->mu);
+            alloc_ok = hipSetDevice(p->c->device) == hipSuccess &&
+                       hipMalloc(&ix->d_index, ix->pass_size * 8) == hipSuccess &&
+                       (!ix->approx || hipMalloc(&ix->d_index_a, ix->pass_size * 8) == hipSuccess);
+        }
+        // (bsdb_index_close takes the context lock itself: called after the scope)
+        if (!alloc_ok) {
             bsdb_index_close(ix);
             return BSDB_ENOMEM;
         }

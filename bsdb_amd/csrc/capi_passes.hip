@@ -20,16 +20,35 @@
 
 namespace {
 
+// Where a pass's index slots go.  d_index: the device array of all n slots;
+// h_index: a host array of all n slots; job: run on a copier thread of its own
+// after the pass's solve, with the pass's contiguous slots [e_lo, e_lo + nl)
+// in the device buffer d_slice (slot buffer sl = pass & 1, reused two passes
+// later), e.g. written to the index files at byte 8 e_lo (the builder,
+// capi_builder.hip).  prepare (optional, main thread, before the solve): per
+// slot buffer state the job needs for nl slots.  positions: the slots hold
+// each key's input position (byte-reversed, as the solve stores addresses)
+// for the job to turn into addresses.
+struct PassSink {
+    uint64_t *d_index = nullptr;
+    uint64_t *h_index = nullptr;
+    std::function<int(int sl, uint64_t nl)> prepare;
+    std::function<int(int sl, const uint64_t *d_slice, uint64_t nl, uint64_t e_lo)> job;
+    uint64_t job_bytes_per_key = 0;  // device bytes per key of a pass the job holds (both slot buffers)
+    bool positions = false;
+    bool slices() const { return h_index || job; }
+};
+
 // device bytes per key of one pass: sorted signature + position payload, plus
-// the pass's index slots (twice when they go to host memory: one buffer is
+// the pass's index slots (twice when they go out of the device: one buffer is
 // copied out while the next pass fills the other)
-uint64_t pass_bytes_per_key(bool dev_index, bool host_index) {
-    return 16 + 8 + (dev_index ? 0 : host_index ? 16 : 0);
+uint64_t pass_bytes_per_key(const PassSink &sink) {
+    return 16 + 8 + (sink.slices() ? 16 + sink.job_bytes_per_key : 0);
 }
 
 int passes_build(bsdb_ctx *c, const GovSrc &src, uint64_t n, uint32_t width, uint32_t passes, const uint64_t *d_addr,
                  uint64_t addr_base, uint64_t addr_stride, uint64_t *d_E, uint64_t *d_values, uint64_t *d_sigbits,
-                 uint64_t *d_index, uint64_t *h_index, uint32_t *passes_used, hipStream_t s) {
+                 const PassSink &sink, uint32_t *passes_used, hipStream_t s) {
     const uint64_t m = n / BUCKET_SIZE + 1;
     // Every bucket's count over the whole set, once, by the histogram stage
     // (binned pass 1 + pass 2: C4 ~43 ms) instead of a re-hash with per-key
@@ -61,15 +80,15 @@ int passes_build(bsdb_ctx *c, const GovSrc &src, uint64_t n, uint32_t width, uin
         size_t free_b = 0, total_b = 0;
         HIP_OK(hipMemGetInfo(&free_b, &total_b));
         const double room = 0.85 * (double)free_b - 12e9;
-        const double need = 1.05 * (double)n * (double)pass_bytes_per_key(d_index != nullptr, h_index != nullptr);
+        const double need = 1.05 * (double)n * (double)pass_bytes_per_key(sink);
         passes = room <= 0 ? 64u : (uint32_t)std::min(64.0, std::max(1.0, std::ceil(need / room)));
     }
     passes = (uint32_t)std::min<uint64_t>(passes, m);
     if (passes_used) *passes_used = passes;
     HIP_OK(hipMemsetAsync(d_values, 0, bsdb_values_words(n) * 8, s));
     if (width) HIP_OK(hipMemsetAsync(d_sigbits, 0, ((n * width + 63) / 64 + 1) * 8, s));
-    // host index: two device slice buffers; the copy of pass p's slots runs on
-    // a thread of its own (own stream) while pass p+1 solves into the other
+    // two device slice buffers; the copy-out of pass p's slots runs on a
+    // thread of its own (own stream) while pass p+1 solves into the other
     void *slice[2] = {nullptr, nullptr};
     size_t slice_bytes[2] = {0, 0};
     std::thread copier[2];
@@ -93,30 +112,39 @@ int passes_build(bsdb_ctx *c, const GovSrc &src, uint64_t n, uint32_t width, uin
         if (b_lo >= b_hi) continue;
         const int sl = (int)(p & 1);
         GovIndexOut ixo;
-        ixo.addr = d_addr;
-        ixo.addr_base = addr_base;
-        ixo.addr_stride = addr_stride;
-        if (d_index) {
-            ixo.index = d_index;  // global slots
-        } else if (h_index) {
+        ixo.addr = sink.positions ? nullptr : d_addr;
+        ixo.addr_base = sink.positions ? 0 : addr_base;
+        ixo.addr_stride = sink.positions ? 1 : addr_stride;
+        if (sink.d_index) {
+            ixo.index = sink.d_index;  // global slots
+        } else if (sink.slices()) {
             ixo.idx_lo = e_lo;
             ixo.slots = [&](uint64_t nl) -> uint64_t * {
                 if (join(sl)) return nullptr;  // the copy out of this buffer (pass p-2) is done
                 if (grow(&slice[sl], &slice_bytes[sl], std::max<uint64_t>(nl, 1) * 8)) return nullptr;
+                if (sink.prepare && sink.prepare(sl, nl)) return nullptr;
                 return (uint64_t *)slice[sl];
             };
         }  // (neither: the structure only)
         uint64_t nl = 0;
         int rc = gov_build_impl(c, gsrc, n, b_lo, b_hi, e_lo, width, d_E, d_values, d_sigbits, nullptr, ixo, s, false, &nl);
         if (rc) return finish(rc);
-        if (h_index && nl) {  // gov_build_impl returned after the device finished
-            uint64_t *dst = h_index + e_lo;
-            const void *src_slots = slice[sl];
+        if (sink.slices() && nl) {  // gov_build_impl returned after the device finished
+            const uint64_t *src_slots = (const uint64_t *)slice[sl];
             const int dev = c->device;
+            const uint64_t lo = e_lo;
             copy_rc[sl] = BSDB_OK;
-            copier[sl] = std::thread([&, dst, src_slots, nl, dev, sl] {
-                copy_rc[sl] = d2h_pageable(dev, dst, src_slots, nl * 8);
-            });
+            if (sink.job) {
+                copier[sl] = std::thread([&, src_slots, nl, lo, dev, sl] {
+                    (void)hipSetDevice(dev);
+                    copy_rc[sl] = sink.job(sl, src_slots, nl, lo);
+                });
+            } else {
+                uint64_t *dst = sink.h_index + e_lo;
+                copier[sl] = std::thread([&, dst, src_slots, nl, dev, sl] {
+                    copy_rc[sl] = d2h_pageable(dev, dst, src_slots, nl * 8);
+                });
+            }
         }
         e_lo += nl;
     }
@@ -136,8 +164,11 @@ int passes_entry(bsdb_ctx *c, const GovSrc &src, uint64_t n, uint32_t width, uin
     HIP_OK(hipSetDevice(c->device));
     hipStream_t s = pick(c, stream);
     Ordered ord(c, s);
-    return passes_build(c, src, n, width, passes, d_addr, addr_base, addr_stride, d_E, d_values, d_sigbits, d_index,
-                        h_index, passes_used, s);
+    PassSink sink;
+    sink.d_index = d_index;
+    sink.h_index = h_index;
+    return passes_build(c, src, n, width, passes, d_addr, addr_base, addr_stride, d_E, d_values, d_sigbits, sink,
+                        passes_used, s);
 }
 
 }  // namespace

@@ -93,6 +93,16 @@ SIGNATURES = [
     ("bsdb_mph_lookup_fixed", _i, [_vp, _vp, _u32, _u64, _i, _vp]),
     ("bsdb_mph_lookup_var", _i, [_vp, _vp, _vp, _u64, _i, _vp]),
     ("bsdb_mph_free", _i, [_vp]),
+    ("bsdb_mph_build_index_passes_fixed", _i, [_vp, _vp, _u32, _u64, _u32, _vp, _u64, _u64, _vp, _vp, _i, _u32,
+                                               C.c_char_p, C.c_char_p, C.POINTER(_vp), C.POINTER(_u32)]),
+    ("bsdb_mph_build_index_passes_var", _i, [_vp, _vp, _vp, _u64, _u32, _vp, _u64, _u64, _vp, _vp, _i, _u32,
+                                             C.c_char_p, C.c_char_p, C.POINTER(_vp), C.POINTER(_u32)]),
+    ("bsdb_builder_open", _i, [_vp, _u32, _u64, _u64, _i, _u64, _u64, C.POINTER(_vp)]),
+    ("bsdb_builder_add_fixed", _i, [_vp, _vp, _u32, _u64, _vp, _vp, _vp]),
+    ("bsdb_builder_add_var", _i, [_vp, _vp, _vp, _u64, _vp, _vp, _vp]),
+    ("bsdb_builder_count", _i, [_vp, C.POINTER(_u64)]),
+    ("bsdb_builder_finish", _i, [_vp, _u32, _u32, C.c_char_p, C.c_char_p, C.POINTER(_vp), C.POINTER(_u32)]),
+    ("bsdb_builder_free", _i, [_vp]),
     ("bsdb_index_open", _i, [_vp, _i, _u64, C.c_char_p, C.c_char_p, C.POINTER(_vp), C.POINTER(_u64)]),
     ("bsdb_index_begin_pass", _i, [_vp, _u64]),
     ("bsdb_index_put_var", _i, [_vp, _vp, _vp, _u64, _vp, _vp, _vp]),
@@ -425,6 +435,45 @@ class Context:
             C.byref(h)))
         return Mph(h, self)
 
+    def mph_build_index_passes_host(self, keys_np, key_len: int, width: int, index_path: str,
+                                    index_a_path: Optional[str] = None, addr_np=None, addr_base: int = 0,
+                                    addr_stride: int = 0, approximate: bool = False, value8_np=None, vlen_np=None,
+                                    passes: int = 0, offsets_np=None):
+        """F2 in bounded device memory from host records
+        (bsdb_mph_build_index_passes_{fixed,var}): keys uploaded once, built by
+        bucket-range passes, each pass's slots written at their file offset.
+        key_len 0 with offsets_np: variable-length keys.  addr_np None:
+        addresses addr_base + addr_stride * i.  Returns (Mph, passes_used)."""
+        import numpy as np
+        if offsets_np is not None:
+            blob, off, n = self._var_host_args(keys_np, offsets_np)
+        else:
+            blob = np.ascontiguousarray(keys_np, np.uint8)
+            n = blob.size // key_len
+        if addr_np is not None:
+            a, v8, vl = self._records_args(n, addr_np, value8_np, vlen_np, approximate)
+        else:
+            a = None
+            _, v8, vl = self._records_args(n, np.zeros(n, np.uint64), value8_np, vlen_np, approximate)
+        h = C.c_void_p()
+        used = C.c_uint32()
+        ip, ap = index_path.encode(), index_a_path.encode() if index_a_path else None
+        if offsets_np is not None:
+            _check("bsdb_mph_build_index_passes_var", lib().bsdb_mph_build_index_passes_var(
+                self._h, blob.ctypes.data, off.ctypes.data, n, width, _np_ptr(a), addr_base, addr_stride, _np_ptr(v8),
+                _np_ptr(vl), 1 if approximate else 0, passes, ip, ap, C.byref(h), C.byref(used)))
+        else:
+            _check("bsdb_mph_build_index_passes_fixed", lib().bsdb_mph_build_index_passes_fixed(
+                self._h, blob.ctypes.data, key_len, n, width, _np_ptr(a), addr_base, addr_stride, _np_ptr(v8),
+                _np_ptr(vl), 1 if approximate else 0, passes, ip, ap, C.byref(h), C.byref(used)))
+        return Mph(h, self), used.value
+
+    def builder(self, key_len: int = 0, key_capacity: int = 0, blob_capacity: int = 0, approximate: bool = False,
+                addr_base: int = 0, addr_stride: int = 0) -> "Builder":
+        """A streaming builder (bsdb_builder_*): keys added in batches into
+        HBM, then one bucket-range-pass build into the index files."""
+        return Builder(self, key_len, key_capacity, blob_capacity, approximate, addr_base, addr_stride)
+
     def kv_build_index(self, kv_base: str, partitions: int, width: int, index_path: str,
                        index_a_path: Optional[str] = None, approximate: bool = False, fmt: int = 0,
                        block_size: int = 4096, threads: int = 0) -> "Mph":
@@ -644,6 +693,71 @@ class Mph:
         must call ``put(keys..., addr, value8, vlen)`` for every record (the
         kv.db scan).  Returns the number of passes."""
         return IndexWriter(self, index_path, index_a_path, approximate, pass_cache_bytes).run(feed)
+
+
+class Builder:
+    """``bsdb_builder``: BSDBWriter.put's key stream into one device's HBM,
+    then the whole build by bucket-range passes (``finish``)."""
+
+    def __init__(self, ctx: Context, key_len: int, key_capacity: int, blob_capacity: int, approximate: bool,
+                 addr_base: int, addr_stride: int):
+        self.ctx = ctx
+        self.approx = approximate
+        self._h = C.c_void_p()
+        _check("bsdb_builder_open", lib().bsdb_builder_open(ctx._h, key_len, key_capacity, blob_capacity,
+                                                            1 if approximate else 0, addr_base, addr_stride,
+                                                            C.byref(self._h)))
+
+    def close(self):
+        if self._h:
+            _check("bsdb_builder_free", lib().bsdb_builder_free(self._h))
+            self._h = C.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def count(self) -> int:
+        n = C.c_uint64()
+        _check("bsdb_builder_count", lib().bsdb_builder_count(self._h, C.byref(n)))
+        return n.value
+
+    def add_fixed(self, keys_np, key_len: int, addr_np=None, value8_np=None, vlen_np=None):
+        import numpy as np
+        keys_np = np.ascontiguousarray(keys_np, np.uint8)
+        n = keys_np.size // key_len
+        a = np.ascontiguousarray(addr_np, np.uint64) if addr_np is not None else None
+        v8 = np.ascontiguousarray(value8_np, np.uint64) if value8_np is not None else None
+        vl = np.ascontiguousarray(vlen_np, np.uint8) if vlen_np is not None else None
+        _check("bsdb_builder_add_fixed", lib().bsdb_builder_add_fixed(
+            self._h, keys_np.ctypes.data, key_len, n, _np_ptr(a), _np_ptr(v8), _np_ptr(vl)))
+
+    def add_var(self, blob_np, off_np, addr_np=None, value8_np=None, vlen_np=None):
+        import numpy as np
+        blob_np, off_np, n = Context._var_host_args(blob_np, off_np)
+        a = np.ascontiguousarray(addr_np, np.uint64) if addr_np is not None else None
+        v8 = np.ascontiguousarray(value8_np, np.uint64) if value8_np is not None else None
+        vl = np.ascontiguousarray(vlen_np, np.uint8) if vlen_np is not None else None
+        _check("bsdb_builder_add_var", lib().bsdb_builder_add_var(
+            self._h, blob_np.ctypes.data, off_np.ctypes.data, n, _np_ptr(a), _np_ptr(v8), _np_ptr(vl)))
+
+    def finish(self, width: int, index_path: Optional[str] = None, index_a_path: Optional[str] = None,
+               passes: int = 0):
+        """Builds everything added; returns (Mph, passes_used)."""
+        h = C.c_void_p()
+        used = C.c_uint32()
+        _check("bsdb_builder_finish", lib().bsdb_builder_finish(
+            self._h, width, passes, index_path.encode() if index_path else None,
+            index_a_path.encode() if index_a_path else None, C.byref(h), C.byref(used)))
+        return Mph(h, self.ctx), used.value
 
 
 class IndexWriter:

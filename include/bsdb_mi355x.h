@@ -35,6 +35,7 @@
  *   bsdb_mph    a GOV MPHF resident on one device (E, 2-bit values, checksum bits)
  *   bsdb_index  the index.db / index_a.db writer of BSDBWriter.buildIndex
  *   bsdb_multi  one context per device of this process + an RCCL communicator
+ *   bsdb_builder keys streamed into one device's HBM, built by bucket-range passes
  */
 #ifndef BSDB_MI355X_H
 #define BSDB_MI355X_H
@@ -46,7 +47,7 @@
 extern "C" {
 #endif
 
-#define BSDB_ABI_VERSION 3
+#define BSDB_ABI_VERSION 4
 
 /* Return codes (negative errno-style). */
 #define BSDB_OK          0
@@ -412,6 +413,53 @@ int bsdb_mph_build_index_fixed(bsdb_ctx *ctx, const uint8_t *h_keys, uint32_t ke
 int bsdb_mph_build_index_var(bsdb_ctx *ctx, const uint8_t *h_blob, const uint64_t *h_off, uint64_t n, uint32_t width,
                              const uint64_t *h_addr, const uint64_t *h_value8, const uint8_t *h_vlen, int approximate,
                              const char *index_path, const char *index_a_path, bsdb_mph **out);
+/* F2 + F3 in bounded device memory: the same files and MPHF as
+ * bsdb_mph_build_index_* from records in host memory, built by sequential
+ * bucket-range passes over the keys kept in HBM (the reference's 256-segment
+ * spill and segment-by-segment solve, CBHS:379-395,852-978, W:91-155): the
+ * keys go to the device once, every pass re-hashes them and solves its range,
+ * and each pass's index slots are written at their offset while the next pass
+ * solves.  Reaches README-size sets on one device (C4: 13.19e9 x 13 B).
+ * Addresses: h_addr[n], or (h_addr NULL) addr_base + addr_stride * i
+ * (fixed-size records of one data file).  Addresses/values that do not fit
+ * HBM beside the keys are gathered from the caller's arrays in host memory.
+ * passes = 0 picks the fewest passes that fit; *passes_used (optional).
+ * bsdb_mph_build_index_* take this path themselves when their one-shot build
+ * does not fit the free HBM. */
+int bsdb_mph_build_index_passes_fixed(bsdb_ctx *ctx, const uint8_t *h_keys, uint32_t key_len, uint64_t n,
+                                      uint32_t width, const uint64_t *h_addr, uint64_t addr_base, uint64_t addr_stride,
+                                      const uint64_t *h_value8, const uint8_t *h_vlen, int approximate, uint32_t passes,
+                                      const char *index_path, const char *index_a_path, bsdb_mph **out,
+                                      uint32_t *passes_used);
+int bsdb_mph_build_index_passes_var(bsdb_ctx *ctx, const uint8_t *h_blob, const uint64_t *h_off, uint64_t n,
+                                    uint32_t width, const uint64_t *h_addr, uint64_t addr_base, uint64_t addr_stride,
+                                    const uint64_t *h_value8, const uint8_t *h_vlen, int approximate, uint32_t passes,
+                                    const char *index_path, const char *index_a_path, bsdb_mph **out,
+                                    uint32_t *passes_used);
+
+/* The same build fed incrementally, as BSDBWriter.put feeds the hash store
+ * (W:75-89 -> CBHS:360-395): a builder owns the keys added so far in HBM (and,
+ * unless addr_stride != 0 makes the address addr_base + addr_stride * (add
+ * order), each record's address -- plus value8/vlen in approximate mode -- in
+ * host memory).  key_len 0 = variable-length keys (add_fixed is accepted too);
+ * key_capacity / blob_capacity reserve device memory up front (0 = grow on
+ * demand).  Adds are synchronous (the caller may reuse its buffers) and may
+ * come in any order: the files do not depend on it.  finish builds everything
+ * added (index_path NULL: the MPHF only), releases the keys from HBM and
+ * returns the MPHF; free releases the builder (after finish or instead of it).
+ * A failed add leaves the builder failed (later calls return that code). */
+typedef struct bsdb_builder bsdb_builder;
+int bsdb_builder_open(bsdb_ctx *ctx, uint32_t key_len, uint64_t key_capacity, uint64_t blob_capacity, int approximate,
+                      uint64_t addr_base, uint64_t addr_stride, bsdb_builder **out);
+int bsdb_builder_add_fixed(bsdb_builder *b, const uint8_t *h_keys, uint32_t key_len, uint64_t count,
+                           const uint64_t *h_addr, const uint64_t *h_value8, const uint8_t *h_vlen);
+int bsdb_builder_add_var(bsdb_builder *b, const uint8_t *h_blob, const uint64_t *h_off, uint64_t count,
+                         const uint64_t *h_addr, const uint64_t *h_value8, const uint8_t *h_vlen);
+int bsdb_builder_count(const bsdb_builder *b, uint64_t *n);
+int bsdb_builder_finish(bsdb_builder *b, uint32_t width, uint32_t passes, const char *index_path,
+                        const char *index_a_path, bsdb_mph **out, uint32_t *passes_used);
+int bsdb_builder_free(bsdb_builder *b);
+
 int bsdb_index_open(bsdb_mph *mph, int approximate, uint64_t pass_cache_bytes, const char *index_path,
                     const char *index_a_path, bsdb_index **out, uint64_t *passes);
 int bsdb_index_begin_pass(bsdb_index *ix, uint64_t pass);

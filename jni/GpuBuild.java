@@ -7,6 +7,8 @@
 // Not compiled here: this image and the GPU box have no JDK (INTEGRATION.md).
 package tech.bsdb.gpu;
 
+import tech.bsdb.io.NativeUtils;
+
 public final class GpuBuild {
     static { NativeUtils.loadLibraryFromJar(System.mapLibraryName("bsdbgpujni")); }
 
@@ -44,6 +46,29 @@ public final class GpuBuild {
     public static native long mphBuildIndexVar(long ctx, long blob, long offs, long n, int checksumBits, long addr,
                                                long value8, long vlen, boolean approximate, String indexPath,
                                                String indexAPath);
+    public static native long mphBuildIndexFixed(long ctx, long keys, int keyLen, long n, int checksumBits, long addr,
+                                                 long value8, long vlen, boolean approximate, String indexPath,
+                                                 String indexAPath);
+    // F2 in bounded device memory: README-size sets on one GPU by bucket-range passes; addr 0 = the
+    // records' addresses are addrBase + addrStride * i; passesOut[0] receives the passes used
+    public static native long mphBuildIndexPassesFixed(long ctx, long keys, int keyLen, long n, int checksumBits,
+                                                       long addr, long addrBase, long addrStride, long value8,
+                                                       long vlen, boolean approximate, int passes, String indexPath,
+                                                       String indexAPath, long[] passesOut);
+    public static native long mphBuildIndexPassesVar(long ctx, long blob, long offs, long n, int checksumBits,
+                                                     long addr, long addrBase, long addrStride, long value8,
+                                                     long vlen, boolean approximate, int passes, String indexPath,
+                                                     String indexAPath, long[] passesOut);
+    // put() batches straight into HBM (CBHS.add, W:75-89), then buildHash + buildIndex in one finish
+    public static native long builderOpen(long ctx, int keyLen, long keyCapacity, long blobCapacity,
+                                          boolean approximate, long addrBase, long addrStride);
+    public static native void builderAddFixed(long b, long keys, int keyLen, long count, long addr, long value8,
+                                              long vlen);
+    public static native void builderAddVar(long b, long blob, long offs, long count, long addr, long value8,
+                                            long vlen);
+    public static native long builderCount(long b);
+    public static native long builderFinish(long b, int checksumBits, int passes, String indexPath, String indexAPath);
+    public static native void builderFree(long b);
     public static native long[] mphInfo(long mph);        // {n, numBuckets, width, valuesWords, sigWords}
     public static native void mphExport(long mph, long outE, long outValues, long outSigBits);
     public static native long mphImport(long ctx, long n, int width, long E, long values, long sigBits);

@@ -24,6 +24,10 @@ static void fail(JNIEnv *env, int rc) {
 }
 #define CHECK(call) do { int rc_ = (call); if (rc_) fail(env, rc_); } while (0)
 #define JF(name) JNICALL Java_tech_bsdb_gpu_GpuBuild_##name
+/* Strings may be null where the C ABI allows it (index_a_path in exact mode,
+ * index paths of the MPHF-only forms): every jstring goes through these. */
+static const char *utf(JNIEnv *env, jstring s) { return s ? (*env)->GetStringUTFChars(env, s, NULL) : NULL; }
+static void unutf(JNIEnv *env, jstring s, const char *p) { if (s) (*env)->ReleaseStringUTFChars(env, s, p); }
 
 JNIEXPORT jlong JF(open)(JNIEnv *env, jclass c, jint dev) {
     bsdb_ctx *ctx = NULL; CHECK(bsdb_open(dev, &ctx)); return (jlong)(intptr_t)ctx;
@@ -75,9 +79,6 @@ JNIEXPORT void JF(multiHistogramFixed)(JNIEnv *env, jclass c, jlong mc, jlong ke
 JNIEXPORT void JF(multiHistogramVar)(JNIEnv *env, jclass c, jlong mc, jlong blob, jlong offs, jlong n, jlong seed, jlong E) {
     CHECK(bsdb_multi_histogram_var(P(mc), P(blob), P(offs), (uint64_t)n, (uint64_t)seed, P(E)));
 }
-/* index paths may be null (the MPHF only) */
-static const char *utf(JNIEnv *env, jstring s) { return s ? (*env)->GetStringUTFChars(env, s, NULL) : NULL; }
-static void unutf(JNIEnv *env, jstring s, const char *p) { if (s) (*env)->ReleaseStringUTFChars(env, s, p); }
 JNIEXPORT void JF(multiMphBuildIndexVar)(JNIEnv *env, jclass c, jlong mc, jlong blob, jlong offs, jlong n, jint w,
                                          jlong addr, jlong v8, jlong vl, jboolean approx, jstring ip, jstring ap,
                                          jlong E, jlong values, jlong sig) {
@@ -107,14 +108,79 @@ JNIEXPORT jlong JF(mphBuildVar)(JNIEnv *env, jclass c, jlong ctx, jlong blob, jl
 }
 JNIEXPORT jlong JF(mphBuildIndexVar)(JNIEnv *env, jclass c, jlong ctx, jlong blob, jlong offs, jlong n, jint w,
                                      jlong addr, jlong v8, jlong vl, jboolean approx, jstring ip, jstring ap) {
-    const char *i = (*env)->GetStringUTFChars(env, ip, NULL), *a = (*env)->GetStringUTFChars(env, ap, NULL);
+    const char *i = utf(env, ip), *a = utf(env, ap);
     bsdb_mph *m = NULL;
     int rc = bsdb_mph_build_index_var(P(ctx), P(blob), P(offs), (uint64_t)n, (uint32_t)w, P(addr), P(v8), P(vl),
                                       approx, i, a, &m);
-    (*env)->ReleaseStringUTFChars(env, ip, i); (*env)->ReleaseStringUTFChars(env, ap, a);
+    unutf(env, ip, i); unutf(env, ap, a);
     if (rc) { fail(env, rc); return 0; }
     return (jlong)(intptr_t)m;
 }
+JNIEXPORT jlong JF(mphBuildIndexFixed)(JNIEnv *env, jclass c, jlong ctx, jlong keys, jint L, jlong n, jint w,
+                                       jlong addr, jlong v8, jlong vl, jboolean approx, jstring ip, jstring ap) {
+    const char *i = utf(env, ip), *a = utf(env, ap);
+    bsdb_mph *m = NULL;
+    int rc = bsdb_mph_build_index_fixed(P(ctx), P(keys), (uint32_t)L, (uint64_t)n, (uint32_t)w, P(addr), P(v8), P(vl),
+                                        approx, i, a, &m);
+    unutf(env, ip, i); unutf(env, ap, a);
+    if (rc) { fail(env, rc); return 0; }
+    return (jlong)(intptr_t)m;
+}
+/* F2 in bounded device memory (README-size sets on one GPU); passesOut[0] = passes used */
+JNIEXPORT jlong JF(mphBuildIndexPassesFixed)(JNIEnv *env, jclass c, jlong ctx, jlong keys, jint L, jlong n, jint w,
+                                             jlong addr, jlong addrBase, jlong addrStride, jlong v8, jlong vl,
+                                             jboolean approx, jint passes, jstring ip, jstring ap, jlongArray passesOut) {
+    const char *i = utf(env, ip), *a = utf(env, ap);
+    bsdb_mph *m = NULL; uint32_t used = 0;
+    int rc = bsdb_mph_build_index_passes_fixed(P(ctx), P(keys), (uint32_t)L, (uint64_t)n, (uint32_t)w, P(addr),
+                                               (uint64_t)addrBase, (uint64_t)addrStride, P(v8), P(vl), approx,
+                                               (uint32_t)passes, i, a, &m, &used);
+    unutf(env, ip, i); unutf(env, ap, a);
+    if (rc) { fail(env, rc); return 0; }
+    if (passesOut) { jlong u = (jlong)used; (*env)->SetLongArrayRegion(env, passesOut, 0, 1, &u); }
+    return (jlong)(intptr_t)m;
+}
+JNIEXPORT jlong JF(mphBuildIndexPassesVar)(JNIEnv *env, jclass c, jlong ctx, jlong blob, jlong offs, jlong n, jint w,
+                                           jlong addr, jlong addrBase, jlong addrStride, jlong v8, jlong vl,
+                                           jboolean approx, jint passes, jstring ip, jstring ap, jlongArray passesOut) {
+    const char *i = utf(env, ip), *a = utf(env, ap);
+    bsdb_mph *m = NULL; uint32_t used = 0;
+    int rc = bsdb_mph_build_index_passes_var(P(ctx), P(blob), P(offs), (uint64_t)n, (uint32_t)w, P(addr),
+                                             (uint64_t)addrBase, (uint64_t)addrStride, P(v8), P(vl), approx,
+                                             (uint32_t)passes, i, a, &m, &used);
+    unutf(env, ip, i); unutf(env, ap, a);
+    if (rc) { fail(env, rc); return 0; }
+    if (passesOut) { jlong u = (jlong)used; (*env)->SetLongArrayRegion(env, passesOut, 0, 1, &u); }
+    return (jlong)(intptr_t)m;
+}
+/* the streaming builder: put() batches straight into HBM, then one build */
+JNIEXPORT jlong JF(builderOpen)(JNIEnv *env, jclass c, jlong ctx, jint L, jlong keyCap, jlong blobCap, jboolean approx,
+                                jlong addrBase, jlong addrStride) {
+    bsdb_builder *b = NULL;
+    CHECK(bsdb_builder_open(P(ctx), (uint32_t)L, (uint64_t)keyCap, (uint64_t)blobCap, approx, (uint64_t)addrBase,
+                            (uint64_t)addrStride, &b));
+    return (jlong)(intptr_t)b;
+}
+JNIEXPORT void JF(builderAddFixed)(JNIEnv *env, jclass c, jlong b, jlong keys, jint L, jlong cnt, jlong addr, jlong v8,
+                                   jlong vl) {
+    CHECK(bsdb_builder_add_fixed(P(b), P(keys), (uint32_t)L, (uint64_t)cnt, P(addr), P(v8), P(vl)));
+}
+JNIEXPORT void JF(builderAddVar)(JNIEnv *env, jclass c, jlong b, jlong blob, jlong offs, jlong cnt, jlong addr, jlong v8,
+                                 jlong vl) {
+    CHECK(bsdb_builder_add_var(P(b), P(blob), P(offs), (uint64_t)cnt, P(addr), P(v8), P(vl)));
+}
+JNIEXPORT jlong JF(builderCount)(JNIEnv *env, jclass c, jlong b) {
+    uint64_t n = 0; CHECK(bsdb_builder_count(P(b), &n)); return (jlong)n;
+}
+JNIEXPORT jlong JF(builderFinish)(JNIEnv *env, jclass c, jlong b, jint w, jint passes, jstring ip, jstring ap) {
+    const char *i = utf(env, ip), *a = utf(env, ap);
+    bsdb_mph *m = NULL;
+    int rc = bsdb_builder_finish(P(b), (uint32_t)w, (uint32_t)passes, i, a, &m, NULL);
+    unutf(env, ip, i); unutf(env, ap, a);
+    if (rc) { fail(env, rc); return 0; }
+    return (jlong)(intptr_t)m;
+}
+JNIEXPORT void JF(builderFree)(JNIEnv *env, jclass c, jlong b) { CHECK(bsdb_builder_free(P(b))); }
 JNIEXPORT jlongArray JF(mphInfo)(JNIEnv *env, jclass c, jlong mph) {
     uint64_t n, m, vw, sw; uint32_t w;
     int rc = bsdb_mph_info(P(mph), &n, &m, &w, &vw, &sw);
@@ -132,15 +198,15 @@ JNIEXPORT jlong JF(mphImport)(JNIEnv *env, jclass c, jlong ctx, jlong n, jint w,
     return (jlong)(intptr_t)m;
 }
 JNIEXPORT void JF(mphDump)(JNIEnv *env, jclass c, jlong mph, jstring path) {
-    const char *p = (*env)->GetStringUTFChars(env, path, NULL);
-    int rc = bsdb_mph_dump(P(mph), p);
-    (*env)->ReleaseStringUTFChars(env, path, p);               /* released on every path, unlike native.c:54 */
+    const char *p = utf(env, path);
+    int rc = bsdb_mph_dump(P(mph), p);                          /* (null path: BSDB_EINVAL) */
+    unutf(env, path, p);                                        /* released on every path, unlike native.c:54 */
     if (rc) fail(env, rc);
 }
 JNIEXPORT jlong JF(mphLoad)(JNIEnv *env, jclass c, jlong ctx, jstring path) {
-    const char *p = (*env)->GetStringUTFChars(env, path, NULL);
+    const char *p = utf(env, path);
     bsdb_mph *m = NULL; int rc = bsdb_mph_load(P(ctx), p, &m);
-    (*env)->ReleaseStringUTFChars(env, path, p);
+    unutf(env, path, p);
     if (rc) { fail(env, rc); return 0; }
     return (jlong)(intptr_t)m;
 }
@@ -154,10 +220,10 @@ JNIEXPORT void JF(mphFree)(JNIEnv *env, jclass c, jlong mph) { CHECK(bsdb_mph_fr
 
 JNIEXPORT jlong JF(indexOpen)(JNIEnv *env, jclass c, jlong mph, jboolean approx, jlong ps, jstring ip, jstring ap,
                               jlongArray passesOut) {
-    const char *i = (*env)->GetStringUTFChars(env, ip, NULL), *a = (*env)->GetStringUTFChars(env, ap, NULL);
+    const char *i = utf(env, ip), *a = utf(env, ap);
     bsdb_index *ix = NULL; uint64_t passes = 0;
     int rc = bsdb_index_open(P(mph), approx, (uint64_t)ps, i, a, &ix, &passes);
-    (*env)->ReleaseStringUTFChars(env, ip, i); (*env)->ReleaseStringUTFChars(env, ap, a);
+    unutf(env, ip, i); unutf(env, ap, a);
     if (rc) { fail(env, rc); return 0; }
     jlong p = (jlong)passes; (*env)->SetLongArrayRegion(env, passesOut, 0, 1, &p);
     return (jlong)(intptr_t)ix;

@@ -103,9 +103,51 @@ def test_shim_calls_exported_header_functions_with_their_arity():
             assert n == fns[fn], f"{name}: {fn} called with {n} arguments, the header has {fns[fn]}"
             called.add(fn)
     # the host-buffer build path a JVM needs is all bound
-    for fn in ("bsdb_open", "bsdb_close", "bsdb_mph_build_index_var", "bsdb_mph_export", "bsdb_index_open",
-               "bsdb_index_put_fixed", "bsdb_index_close", "bsdb_multi_mph_build_index_fixed", "bsdb_mph_free"):
+    for fn in ("bsdb_open", "bsdb_close", "bsdb_mph_build_index_var", "bsdb_mph_build_index_fixed",
+               "bsdb_mph_build_index_passes_fixed", "bsdb_mph_build_index_passes_var", "bsdb_builder_open",
+               "bsdb_builder_add_fixed", "bsdb_builder_add_var", "bsdb_builder_finish", "bsdb_builder_free",
+               "bsdb_mph_export", "bsdb_index_open", "bsdb_index_put_fixed", "bsdb_index_close",
+               "bsdb_multi_mph_build_index_fixed", "bsdb_mph_free", "bsdb_kv_build_index"):
         assert fn in called, fn
+
+
+def test_strings_go_through_the_null_safe_helpers():
+    """a null jstring (index_a_path in exact mode) must not reach
+    GetStringUTFChars: only the utf()/unutf() helpers call the JNI string
+    functions."""
+    src = _strip_comments(open(SHIM).read())
+    calls = [m.start() for m in re.finditer(r"(Get|Release)StringUTFChars", src)]
+    helpers = [m.start() for m in re.finditer(r"static\s+(const char \*|void)\s*(utf|unutf)\s*\(", src)]
+    assert len(calls) == 2 and len(helpers) == 2
+    for pos in calls:  # each call sits inside one of the two helper definitions (one line each)
+        assert any(h < pos < src.index("\n", h) for h in helpers), src[max(0, pos - 80): pos + 40]
+
+
+# classes of the JDK (java.lang is implicit) and of the reference the Java class may use
+_JAVA_LANG = {"String", "System", "Object", "Override", "Exception", "RuntimeException", "Integer", "Long", "Boolean",
+              "Math", "Thread", "Class", "Deprecated", "SuppressWarnings", "IllegalArgumentException"}
+
+
+def test_java_class_resolves_every_simple_name():
+    """GpuBuild.java used NativeUtils (tech.bsdb.io,
+    src/main/java/tech/bsdb/io/NativeUtils.java) without importing it.  Every
+    capitalised simple name in the class must be java.lang, imported, or the
+    class itself (javac is not in this image: this is the check that stands in
+    for it)."""
+    src = _strip_comments(open(JAVA).read())
+    src_nostr = re.sub(r'"[^"\n]*"', '""', src)
+    pkg = re.search(r"^package\s+([\w.]+);", src_nostr, re.M).group(1)
+    imported = {m.group(1).split(".")[-1] for m in re.finditer(r"^import\s+([\w.]+);", src_nostr, re.M)}
+    own = set(re.findall(r"\b(?:class|interface|enum)\s+(\w+)", src_nostr))
+    body = re.sub(r"^(package|import)\s+[^;]+;", "", src_nostr, flags=re.M)
+    used = set(re.findall(r"\b([A-Z]\w*)\b(?=\s*[.(\[<\w])", body)) | set(re.findall(r"\bnew\s+([A-Z]\w*)", body))
+    used -= {"JNI"}
+    missing = {u for u in used if u not in _JAVA_LANG and u not in imported and u not in own}
+    assert not missing, f"{pkg}: unresolved simple names {sorted(missing)}"
+    assert "NativeUtils" in imported
+    ref = "/root/reference/src/main/java/tech/bsdb/io/NativeUtils.java"
+    if os.path.exists(ref):  # (this container only) the import names the reference's own class
+        assert "package tech.bsdb.io;" in open(ref).read()
 
 
 @pytest.mark.skipif(shutil.which("gcc") is None, reason="no gcc")
