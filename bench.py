@@ -179,6 +179,127 @@ def c4_exact_passes(ctx, keys, n: int, width: int):
                     "(8 B x n, byte-reversed addr = 0x1000 + 48 i) in host memory"}
 
 
+def _roomiest_dir(need_bytes: float):
+    """The candidate directory with the most free space, or None when none has
+    room for `need_bytes` (the figure then writes to /dev/null and says so)."""
+    import shutil
+    best, free = None, -1
+    for d in ("/tmp", "/dev/shm", os.path.join(ROOT, "build")):
+        try:
+            os.makedirs(d, exist_ok=True)
+            f = shutil.disk_usage(d).free
+        except OSError:
+            continue
+        if f > free:
+            best, free = d, f
+    return (best, free) if free > need_bytes * 1.1 else (None, free)
+
+
+def e2e_c4_host_passes(ctx, n: int, width: int, chunk: int = 1 << 28):
+    """BASELINE C4 from HOST memory on one GPU (bsdb_builder_*, what the JVM
+    calls): the 13.19e9 keys arrive in host batches of `chunk` keys (each
+    batch is produced before the clock runs for it: generated on the device
+    and copied to a pinned host buffer), every add() copies its batch into
+    HBM, then finish() runs the bucket-range passes and writes index.db at
+    each pass's offset while the next pass solves.  Timed: the adds + the
+    finish (host keys -> index.db on disk + the MPHF in HBM); record
+    addresses 0x1000 + 48 i (fixed 48-byte records of one file)."""
+    import shutil
+    import tempfile
+    import time as _t
+    import torch
+    d, free = _roomiest_dir(8 * n)
+    tmp = tempfile.mkdtemp(prefix="bsdb_c4_", dir=d) if d else None
+    ip = os.path.join(tmp, "index.db") if tmp else "/dev/null"
+    try:
+        dev = torch.empty(13 * chunk + 16, dtype=torch.uint8, device="cuda")
+        host = torch.empty(13 * chunk, dtype=torch.uint8, pin_memory=True)
+        b = ctx.builder(13, key_capacity=n, addr_base=0x1000, addr_stride=48)
+        t_add = 0.0
+        for k0 in range(0, n, chunk):
+            k = min(chunk, n - k0)
+            ctx.gen_keys13(k0, k, out=dev)
+            host[: 13 * k].copy_(dev[: 13 * k])
+            torch.cuda.synchronize()
+            t0 = _t.perf_counter()
+            b.add_fixed(host[: 13 * k].numpy(), 13)
+            t_add += _t.perf_counter() - t0
+        del dev
+        torch.cuda.empty_cache()
+        t0 = _t.perf_counter()
+        mph, used = b.finish(width, ip, None)
+        t_fin = _t.perf_counter() - t0
+        size = os.path.getsize(ip) if tmp else None
+        E, _, _ = mph.export()
+        ok = int(E[-1]) & ((1 << 56) - 1) == n
+        mph.close()
+        b.close()
+        del host
+    finally:
+        if tmp:
+            shutil.rmtree(tmp, ignore_errors=True)
+    dt = t_add + t_fin
+    return {"n_keys": n, "checksum_bits": width, "passes": used, "keys_per_s": n / dt, "ms": dt * 1e3,
+            "add_ms": t_add * 1e3, "finish_ms": t_fin * 1e3, "h2d_GBps": 13 * n / t_add / 1e9,
+            "index_db": ip if tmp is None else f"{d} ({size} bytes; {free / 1e9:.0f} GB free before)",
+            "check": {"E[m]==n": ok, "index.db bytes == 8n": (size == 8 * n) if tmp else None},
+            "path": "host keys (batches of 2^28) -> bsdb_builder_add_fixed (H2D into HBM) -> bsdb_builder_finish "
+                    "(bucket-range passes; each pass's index.db slots pwritten at their offset while the next "
+                    "pass solves) -> index.db" + ("" if tmp else " written to /dev/null: no file system on this "
+                                                  "box had room for 8n bytes")}
+
+
+def e2e_c2_kv_to_disk(ctx, n: int, width: int, partitions: int = 8):
+    """BASELINE C2 from the DATA FILES: n records of 13-byte keys and 32-byte
+    values in SimpleCompactKVWriter's layout (48-byte records, kv.db.<p>,
+    written before the clock) -> bsdb_kv_build_index (host threads parse the
+    partitions and stream them into the builder; bucket-range-pass build;
+    index.db) + hash.dump.  The reference's buildIndex reads the same files
+    (W:134, PartitionedKVWriter.java:50-70)."""
+    import shutil
+    import tempfile
+    import time as _t
+    import numpy as np
+    import torch
+    d, _ = _roomiest_dir(48 * n + 8 * n)
+    if d is None:
+        return {"skipped": f"no directory with {56 * n / 1e9:.1f} GB free"}
+    tmp = tempfile.mkdtemp(prefix="bsdb_kv_", dir=d)
+    try:
+        base = os.path.join(tmp, "kv.db")
+        per = -(-n // partitions)
+        for p in range(partitions):
+            lo, hi = p * per, min(n, (p + 1) * per)
+            with open(f"{base}.{p}", "wb") as f:
+                for c0 in range(lo, hi, 1 << 24):
+                    k = min(1 << 24, hi - c0)
+                    rec = torch.empty((k, 48), dtype=torch.uint8, device="cuda")
+                    rec[:, 0] = 13
+                    rec[:, 1] = 0
+                    rec[:, 2] = 32
+                    rec[:, 3:16] = ctx.gen_keys13(c0, k).view(k, 13)
+                    rec[:, 16:] = torch.randint(0, 256, (k, 32), dtype=torch.uint8, device="cuda")
+                    rec.cpu().numpy().tofile(f)
+                    del rec
+        torch.cuda.empty_cache()
+        ip = os.path.join(tmp, "index.db")
+        t0 = _t.perf_counter()
+        mph = ctx.kv_build_index(base, partitions, width, ip, os.path.join(tmp, "index_a.db"))
+        mph.dump(os.path.join(tmp, "hash.dump"))
+        dt = _t.perf_counter() - t0
+        size = os.path.getsize(ip)
+        E, _, _ = mph.export()
+        ok = int(E[-1]) & ((1 << 56) - 1) == n
+        mph.close()
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+    return {"n_keys": n, "checksum_bits": width, "partitions": partitions, "keys_per_s": n / dt, "ms": dt * 1e3,
+            "kv_db_bytes": 48 * n, "check": {"E[m]==n": ok, "index.db bytes == 8n": size == 8 * n},
+            "path": f"kv.db.<p> files ({48 * n / 1e9:.1f} GB, compact layout, in {d}) -> bsdb_kv_build_index "
+                    "(parallel partition scan streamed into the builder, bucket-range-pass build) -> index.db + "
+                    "index_a.db (empty) + hash.dump"}
+
+
 def single_pass_ab(ctx, keys, n: int, m: int, ref_counts, reps: int = 3):
     """The single-pass histogram (mode 3) on the same resident
     keys: its counts against the headline's, and its time (HIP events).  Opt-in
@@ -331,14 +452,22 @@ def main():
         # process group once, outside the timed region.  If the library's own
         # communicator cannot be set up on every rank, the same all-reduce
         # runs through torch.distributed (also RCCL), and the line says so.
+        # every rank first agrees that it can load RCCL at all: the
+        # communicator init below is collective and has no timeout, so a
+        # rank that could not join it would leave the others waiting
+        avail = torch.tensor([1 if Context.comm_available() else 0], dtype=torch.int32, device="cuda")
+        dist.all_reduce(avail, op=dist.ReduceOp.MIN)
         ok_local = 1
         obj = [None]
-        if rank == 0:
+        if int(avail.item()) == 0:
+            pass
+        elif rank == 0:
             try:
                 obj[0] = Context.comm_unique_id()
             except Exception as e:  # (RCCL not loadable by the library)
                 print(f"[bench r0] bsdb_comm_unique_id failed: {e!r}", file=sys.stderr, flush=True)
-        dist.broadcast_object_list(obj, src=0)  # every rank joins, id or None
+        if int(avail.item()) != 0:
+            dist.broadcast_object_list(obj, src=0)  # every rank joins, id or None
         if obj[0] is None:
             ok_local = 0
         else:
@@ -459,6 +588,13 @@ def main():
         log("C4 exact full build done")
         del keys
         torch.cuda.empty_cache()
+        ctx.release_workspace()
+        try:
+            full["e2e_c4_host_passes"] = e2e_c4_host_passes(ctx, n, 4)
+        except Exception as e:  # recorded, not faked
+            full["e2e_c4_host_passes"] = {"error": repr(e)[:300]}
+        torch.cuda.empty_cache()
+        log("C4 host passes done")
         try:
             full["gpu_c5_varlen_histogram"], full["gpu_c5_full_build_passes"] = c5_varlen_histogram(
                 ctx, 4_000_000_000, 5)
@@ -471,6 +607,10 @@ def main():
             full["e2e_c2_host_to_disk"] = e2e_host_to_disk(ctx, 100_000_000, 4)
         except OSError as e:  # (no room for 0.8 GB in /tmp: the figure is skipped, not faked)
             full["e2e_c2_host_to_disk"] = {"skipped": str(e)}
+        try:
+            full["e2e_c2_kv_to_disk"] = e2e_c2_kv_to_disk(ctx, 100_000_000, 4)
+        except Exception as e:  # recorded, not faked
+            full["e2e_c2_kv_to_disk"] = {"error": repr(e)[:300]}
         if args.e4_devices > 0:
             try:
                 full["e4_c3_multi_device"] = e4_multi_device(ctx, 1_000_000_000, 4, args.e4_devices)

@@ -786,6 +786,37 @@ int bsdb_open(int device, bsdb_ctx **out) {
 
 static void mph_detach_all(bsdb_ctx *c);
 
+// Frees the grown workspace buffers (they grow again on the next call that
+// needs them): the histogram id stream, the GOV build's sorted signatures,
+// payloads, scratch, ledger and slabs, the host feed's device buffers.
+static void release_workspace(bsdb_ctx *c) {
+    for (void **p : {&c->ids, &c->d_out, &c->g_sorted, &c->g_pay, &c->g_scratch, &c->g_led, &c->g_mid, &c->g_slabs,
+                     &c->g_big, &c->pack}) {
+        (void)hipFree(*p);
+        *p = nullptr;
+    }
+    c->ids_bytes = c->d_out_bytes = c->g_sorted_bytes = c->g_pay_bytes = c->g_scratch_bytes = c->g_led_bytes =
+        c->g_mid_bytes = c->g_slabs_bytes = c->g_big_bytes = c->pack_bytes = 0;
+    for (auto &f : c->feed) {
+        if (f.used) (void)hipEventSynchronize(f.done);
+        for (int i = 0; i < 8; ++i) {
+            (void)hipFree(f.buf[i]);
+            f.buf[i] = nullptr;
+            f.cap[i] = 0;
+        }
+        f.used = false;
+    }
+}
+
+int bsdb_release_workspace(bsdb_ctx *c) {
+    if (!c) return BSDB_EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    HIP_OK(hipSetDevice(c->device));
+    HIP_OK(hipDeviceSynchronize());
+    release_workspace(c);
+    return BSDB_OK;
+}
+
 int bsdb_close(bsdb_ctx *c) {
     if (!c) return BSDB_EINVAL;
     (void)hipSetDevice(c->device);

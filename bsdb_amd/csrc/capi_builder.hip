@@ -313,10 +313,15 @@ int builder_add(bsdb_builder *b, uint64_t count, const uint64_t *h_addr, const u
     return BSDB_OK;
 }
 
+// creates (truncates) an index file at its final size; a path that is not a
+// regular file (e.g. /dev/null for a measurement without a file system) is
+// opened for writing as it is
 int open_out(const char *path, uint64_t bytes, int *fd) {
     *fd = open(path, O_WRONLY | O_CREAT | O_TRUNC, 0644);
     if (*fd < 0) return BSDB_EFILE;
-    if (bytes && ftruncate(*fd, (off_t)bytes) != 0) return BSDB_EFILE;
+    struct stat st;
+    if (fstat(*fd, &st) != 0) return BSDB_EFILE;
+    if (S_ISREG(st.st_mode) && bytes && ftruncate(*fd, (off_t)bytes) != 0) return BSDB_EFILE;
     return BSDB_OK;
 }
 

@@ -109,6 +109,8 @@ static int finalize_impl(bsdb_ctx *c, const Rccl *r, uint32_t *d_counts, uint64_
 
 extern "C" {
 
+int bsdb_comm_available(void) { return rccl() ? 1 : 0; }
+
 int bsdb_comm_unique_id(uint8_t *id) {
     if (!id) return BSDB_EINVAL;
     const Rccl *r = rccl();

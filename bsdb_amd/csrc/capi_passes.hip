@@ -74,6 +74,15 @@ int passes_build(bsdb_ctx *c, const GovSrc &src, uint64_t n, uint32_t width, uin
         if (hrc) return hrc;
         gsrc.counts_all = (const uint32_t *)q;
     }
+    // the per-key buffers of an earlier build on this context are sized for
+    // it: released, so the pass count below sees their memory as free (they
+    // grow back to this build's pass size)
+    HIP_OK(hipStreamSynchronize(s));
+    for (void **q : {&c->g_sorted, &c->g_pay}) {
+        (void)hipFree(*q);
+        *q = nullptr;
+    }
+    c->g_sorted_bytes = c->g_pay_bytes = 0;
     if (passes == 0) {
         // the fewest passes whose working set fits 85 % of the free HBM (the
         // solver scratch and the per-bucket arrays come on top: ~10 GB)

@@ -55,8 +55,10 @@ constexpr uint32_t FU_HDR_BYTES = FU_OWNERS * 4;  // a region's header: (chunk o
 constexpr uint32_t FU_CHUNKS_MAX = FU_OWNERS * (FU_CAPB / 8);
 constexpr uint32_t FU_REGION_BYTES = FU_HDR_BYTES + FU_CHUNKS_MAX * 16;  // 41 984 (= 328 lines)
 constexpr size_t FU_SLOT_BYTES = (size_t)FU_OWNERS * FU_REGION_BYTES;   // 10.7 MB
-// sync words (u64): pub[FU_SLOTS][FU_SHARDS] lines, then fin, then abort
-constexpr size_t FU_SYNC_U64 = ((size_t)FU_SLOTS * FU_SHARDS + 2) * FU_LINE_U64;
+// sync words (u64): pub[FU_SLOTS][FU_SHARDS] lines, then fin, abort and the
+// end decision (0 open, FU_COMMIT, FU_ABORT: set once, by one CAS)
+constexpr size_t FU_SYNC_U64 = ((size_t)FU_SLOTS * FU_SHARDS + 3) * FU_LINE_U64;
+constexpr uint64_t FU_COMMIT = 1, FU_ABORT = 2;
 
 struct FusedArgs {
     const uint8_t *keys;   // 13-byte keys, the super-tiles [0, nsuper * 256)
@@ -77,6 +79,15 @@ __device__ __forceinline__ uint64_t fu_load_relaxed(const uint64_t *p) {
 }
 __device__ __forceinline__ void fu_add_relaxed(uint64_t *p, uint64_t v) {
     (void)__hip_atomic_fetch_add((fu_gu64 *)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t fu_fetch_add_relaxed(uint64_t *p, uint64_t v) {
+    return __hip_atomic_fetch_add((fu_gu64 *)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// sets *p from 0 to v unless another value got there first
+__device__ __forceinline__ void fu_decide(uint64_t *p, uint64_t v) {
+    uint64_t expect = 0;
+    (void)__hip_atomic_compare_exchange_strong((fu_gu64 *)p, &expect, v, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // VAR 0 is production.  Profiling only (results invalid unless noted): bit 0
@@ -223,6 +234,7 @@ __global__ __launch_bounds__(FU_NT, 1) void k_hist13_fused(FusedArgs a) {
     uint64_t *const pub = a.sync;
     uint64_t *const fin = a.sync + (size_t)FU_SLOTS * FU_SHARDS * FU_LINE_U64;
     uint64_t *const abort_w = fin + FU_LINE_U64;
+    uint64_t *const decide = abort_w + FU_LINE_U64;
     auto region_rsrc = [&](uint64_t y) {
         const uint32_t slot = (uint32_t)(y % SLOTS);
         return __builtin_amdgcn_make_buffer_rsrc(a.ring + (size_t)slot * FU_SLOT_BYTES, 0, (uint32_t)FU_SLOT_BYTES,
@@ -398,28 +410,28 @@ __global__ __launch_bounds__(FU_NT, 1) void k_hist13_fused(FusedArgs a) {
         for (int i = 0; i < FU_NW; ++i) dsum += red[i];
         // any_ovf of wave 0 covers every round (each wave waited on every round)
         const bool bad = dsum != 0 || any_dead || any_ovf || fu_load_relaxed(abort_w) != 0;
-        fu_add_relaxed(fin, 1ull + ((uint64_t)bad << 32));
-        uint64_t v = fu_load_relaxed(fin);
+        // commit or abort is ONE decision for the whole grid: the
+        // last workgroup to arrive sets it from every arrival's bad bit; a
+        // workgroup that times out waiting sets abort instead; whichever CAS
+        // lands first holds, and every workgroup acts on that value
+        const uint64_t now = fu_fetch_add_relaxed(fin, 1ull + ((uint64_t)bad << 32)) + 1ull + ((uint64_t)bad << 32);
+        if ((uint32_t)now == (uint32_t)gridDim.x) fu_decide(decide, (now >> 32) ? FU_ABORT : FU_COMMIT);
+        uint64_t d = fu_load_relaxed(decide);
         uint32_t spins = 0;
-        while ((uint32_t)v != (uint32_t)gridDim.x) {
+        while (d == 0) {
             __builtin_amdgcn_s_sleep(2);
             if (++spins > FU_SPIN_MAX || fu_load_relaxed(abort_w) != 0) {
                 fu_add_relaxed(abort_w, 1);
-                v = 1ull << 32;
-                break;
+                fu_decide(decide, FU_ABORT);
             }
-            v = fu_load_relaxed(fin);
+            d = fu_load_relaxed(decide);
         }
-        fin_word = v;
+        fin_word = d;
+        if (d == FU_ABORT) atomicOr(a.overflow, 1u);  // nothing added anywhere: the fallback recounts
         if (fu_load_relaxed(abort_w) != 0 && p == 0) atomicAdd(a.overflow + 3, 1u);  // timeouts
     }
     __syncthreads();
-    const uint64_t fw = fin_word;
-    if ((fw >> 32) != 0) {
-        // overflow (or abort) somewhere: nothing added; the fallback recounts
-        if (p == 0 && tid == 0) atomicOr(a.overflow, 1u);
-        return;
-    }
+    if (fin_word != FU_COMMIT) return;
     for (uint32_t i = tid; i < nent; i += NT) {
         const uint32_t v = (table[i >> 1] >> ((i & 1) << 4)) & 0xFFFFu;
         if (v) atomicAdd(a.counts + lo + i, v);

@@ -50,6 +50,7 @@ SIGNATURES = [
     ("bsdb_dev_mph_build_index_passes_var", _i, [_vp, _vp, _u64, _vp, _u64, _u32, _u32, _vp, _u64, _u64, _vp, _vp,
                                                  _vp, _vp, _vp, C.POINTER(_u32), _vp]),
     ("bsdb_dev_partition_owners", _i, [_vp, _vp, _vp, _u64, _u64, _i, _vp, _vp, _vp, _vp]),
+    ("bsdb_release_workspace", _i, [_vp]),
     ("bsdb_set_verify", _i, [_vp, _i]),
     ("bsdb_set_histogram_mode", _i, [_vp, _i]),
     ("bsdb_set_frontend", _i, [_vp, _i]),
@@ -65,6 +66,7 @@ SIGNATURES = [
     ("bsdb_hash_var", _i, [_vp, _vp, _vp, _u64, _u64, _vp]),
     ("bsdb_dev_gen_keys13", _i, [_vp, _u64, _u64, _vp, _vp]),
     ("bsdb_dev_gen_keys_var", _i, [_vp, _u64, _u64, _vp, _vp, _u64, _vp]),
+    ("bsdb_comm_available", _i, []),
     ("bsdb_comm_unique_id", _i, [_vp]),
     ("bsdb_comm_init", _i, [_vp, _i, _i, _vp]),
     ("bsdb_dev_histogram_finalize", _i, [_vp, _vp, _u64, _u64, _vp, _vp]),
@@ -366,10 +368,17 @@ class Context:
             _ptr(pout) if pout is not None else None, counts.ctypes.data, _stream(stream)))
         return out, pout, [int(x) for x in counts]
 
+    def release_workspace(self):
+        _check("bsdb_release_workspace", lib().bsdb_release_workspace(self._h))
+
     def set_verify(self, on: bool):
         _check("bsdb_set_verify", lib().bsdb_set_verify(self._h, 1 if on else 0))
 
     # ---- B4: the histogram collective (RCCL) inside the library
+    @staticmethod
+    def comm_available() -> bool:
+        return bool(lib().bsdb_comm_available())
+
     @staticmethod
     def comm_unique_id() -> bytes:
         buf = C.create_string_buffer(COMM_ID_BYTES)

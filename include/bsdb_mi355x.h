@@ -198,6 +198,10 @@ int bsdb_dev_mph_build_index_passes_var(bsdb_ctx *ctx, const uint8_t *d_blob, ui
 int bsdb_dev_partition_owners(bsdb_ctx *ctx, const uint64_t *d_sig, const uint64_t *d_payload, uint64_t n,
                               uint64_t num_buckets, int nranks, uint64_t *d_out, uint64_t *d_payload_out,
                               uint64_t *h_counts, void *stream);
+/* Frees the context's grown workspace (histogram id stream, GOV build
+ * buffers, host staging): a long-lived context hands its HBM back between
+ * builds (the next call grows what it needs again).  Synchronises the device. */
+int bsdb_release_workspace(bsdb_ctx *ctx);
 /* Debug/test option: after every GOV build, look every key up again on the
  * device and check the ranks form a permutation of [0, n) (BSDB_EVERIFY if not). */
 int bsdb_set_verify(bsdb_ctx *ctx, int enable);
@@ -284,6 +288,9 @@ int bsdb_dev_gen_keys_var(bsdb_ctx *ctx, uint64_t first, uint64_t n, uint64_t *d
  * holds the global counts afterwards.
  * ------------------------------------------------------------------------- */
 #define BSDB_COMM_ID_BYTES 128
+/* 1 when this process can load RCCL (every rank should agree on it before
+ * bsdb_comm_init, which is collective and waits for every rank), else 0. */
+int bsdb_comm_available(void);
 int bsdb_comm_unique_id(uint8_t *id /* [BSDB_COMM_ID_BYTES] */);
 int bsdb_comm_init(bsdb_ctx *ctx, int nranks, int rank, const uint8_t *id);
 int bsdb_dev_histogram_finalize(bsdb_ctx *ctx, uint32_t *d_counts, uint64_t num_buckets, uint64_t n_total,

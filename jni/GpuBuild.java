@@ -18,6 +18,7 @@ public final class GpuBuild {
     public static native long numBuckets(long n);                                   // GOV:281,350
     public static native long valuesWords(long n);                                  // GOV:357
     public static native void setVerify(long ctx, boolean on);
+    public static native void releaseWorkspace(long ctx);                           // HBM back between builds
     // A3/A4/A6 from host memory (what put() batches feed)
     public static native void histogramFixed(long ctx, long keys, int keyLen, long n, long seed, long m, long counts);
     public static native void histogramVar(long ctx, long blob, long offs, long n, long seed, long m, long counts);

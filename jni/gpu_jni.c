@@ -35,6 +35,7 @@ JNIEXPORT jlong JF(open)(JNIEnv *env, jclass c, jint dev) {
 JNIEXPORT void JF(close)(JNIEnv *env, jclass c, jlong ctx) { CHECK(bsdb_close(P(ctx))); }   /* freed, unlike native.c:50-59 */
 JNIEXPORT jlong JF(numBuckets)(JNIEnv *env, jclass c, jlong n) { return (jlong)bsdb_num_buckets((uint64_t)n); }
 JNIEXPORT jlong JF(valuesWords)(JNIEnv *env, jclass c, jlong n) { return (jlong)bsdb_values_words((uint64_t)n); }
+JNIEXPORT void JF(releaseWorkspace)(JNIEnv *env, jclass c, jlong ctx) { CHECK(bsdb_release_workspace(P(ctx))); }
 JNIEXPORT void JF(setVerify)(JNIEnv *env, jclass c, jlong ctx, jboolean on) { CHECK(bsdb_set_verify(P(ctx), on)); }
 
 JNIEXPORT void JF(histogramFixed)(JNIEnv *env, jclass c, jlong ctx, jlong keys, jint L, jlong n, jlong seed, jlong m, jlong counts) {

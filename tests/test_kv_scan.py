@@ -101,3 +101,41 @@ def test_bad_inputs(tmp_path):
         kv_scan(str(tmp_path / "missing.db"), 1, 0)
     with pytest.raises(BsdbError):
         kv_scan(base, 1, 1, 1000)  # block size not a multiple of 4096
+
+
+def test_blocked_layout_matches_the_reference_writers_bytes(tmp_path):
+    """the blocked layout pinned by a byte-level fixture built from
+    BlockedKVWriter.java:45-74 (tests/golden/make_blocked_fixture.py): a large
+    record written before the block still pending, blocks after a longer one
+    carrying its stale bytes past their 0 end mark.  The scan returns the
+    reference's partitionForEach stream (file order, addresses :124-136; the
+    large record's value is read where the reference hands null), and the
+    test writer's file of the same records scans to the same stream."""
+    g = dict(np.load(os.path.join(os.path.dirname(__file__), "golden", "blocked_kv_v1.npz"), allow_pickle=False))
+    bs = int(g["block_size"][0])
+    base = str(tmp_path / "kv.db")
+    g["file0"].tofile(base + ".0")
+    open(base + ".1", "wb").close()                  # an empty partition
+    s = kv_scan(base, 2, 1, bs, threads=2)
+    np.testing.assert_array_equal(s["addr"], g["addr"])
+    np.testing.assert_array_equal(s["offsets"], g["key_off"])
+    np.testing.assert_array_equal(s["blob"], g["keys"])
+    np.testing.assert_array_equal(s["value8"], g["value8"])
+    np.testing.assert_array_equal(s["vlen"], g["vlen"])
+    # kvfiles (the tests' writer) on the same records, written in the fixture's
+    # put order (r0, r1, r2, r3 = scan order 1, 0, 2, 3): same scan stream
+    put = [1, 0, 2, 3]
+    ko, vo = g["key_off"].astype(np.int64), g["value_off"].astype(np.int64)
+    kb = np.concatenate([g["keys"][ko[i]:ko[i + 1]] for i in put])
+    vb = np.concatenate([g["values"][vo[i]:vo[i + 1]] for i in put])
+    kl = np.cumsum([0] + [ko[i + 1] - ko[i] for i in put]).astype(np.uint64)
+    vl = np.cumsum([0] + [vo[i + 1] - vo[i] for i in put]).astype(np.uint64)
+    base2 = str(tmp_path / "mine.db")
+    kvfiles.write_blocked(base2, 1, kb, kl, vb, vl, bs)
+    s2 = kv_scan(base2, 1, 1, bs)
+    np.testing.assert_array_equal(s2["addr"], g["addr"])
+    np.testing.assert_array_equal(s2["blob"], g["keys"])
+    f2 = np.fromfile(base2 + ".0", np.uint8)
+    assert f2.size == g["file0"].size
+    # every byte up to each block's end mark agrees (the tails past it are unspecified)
+    np.testing.assert_array_equal(f2[:5013], g["file0"][:5013])
