@@ -92,6 +92,8 @@ struct bsdb_ctx {
     size_t g_led_bytes = 0;
     void *g_mid = nullptr;  // mid-size ranges: per-workgroup counts (u16) and bases (u32)
     size_t g_mid_bytes = 0;
+    void *g_midscr = nullptr;  // k_gov_solve_mid: dense scratch per workgroup
+    size_t g_midscr_bytes = 0;
     // the oversized buckets' solver runs on its own stream beside k_gov_solve
     hipStream_t big_stream = nullptr;
     hipEvent_t big_ev[2] = {nullptr, nullptr};  // [0] inputs ready on s, [1] big solve done
@@ -160,10 +162,32 @@ namespace {
 
 constexpr uint64_t DEFAULT_CHUNK_KEYS = 1ULL << 32;  // measured: 2^32 286 G keys/s, 2^33 284, one launch (13.2e9) 266
 
-#define HIP_OK(x)                                      \
-    do {                                               \
-        if ((x) != hipSuccess) return BSDB_EIO;        \
+// BSDB_DEBUG=1: every failing HIP call behind an EIO is reported on stderr
+// with its source line (the return code alone does not say which call failed)
+int hip_fail(hipError_t e, const char *what, int line) {
+    static const bool dbg = getenv("BSDB_DEBUG") != nullptr;
+    if (dbg) fprintf(stderr, "[bsdb] line %d: %s -> %d (%s)\n", line, what, (int)e, hipGetErrorString(e));
+    return BSDB_EIO;
+}
+#define HIP_OK(x)                                                   \
+    do {                                                            \
+        const hipError_t e_ = (x);                                  \
+        if (e_ != hipSuccess) return hip_fail(e_, #x, __LINE__);    \
     } while (0)
+
+// Device allocation whose failure is an answer, not an error state: HIP
+// records a failed hipMalloc as the thread's last error, which the next
+// launch check (hipGetLastError) would then report as a failed kernel launch
+// (BSDB_EIO long after the ENOMEM was handled).  Cleared here.
+template <class T>
+hipError_t dmalloc(T **p, size_t bytes) {
+    const hipError_t e = hipMalloc(reinterpret_cast<void **>(p), bytes);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        *p = nullptr;
+    }
+    return e;
+}
 
 // Workspace growth.  hipFree waits for the whole device (every stream), so a
 // regrowth in the middle of overlapped work (the bucket-range passes, whose
@@ -176,11 +200,11 @@ int grow(void **p, size_t *have, size_t need) {
     *p = nullptr;
     *have = 0;
     const size_t roomy = need >= (1u << 20) ? need + need / 64 : need;
-    if (roomy != need && hipMalloc(p, roomy) == hipSuccess) {
+    if (roomy != need && dmalloc(p, roomy) == hipSuccess) {
         *have = roomy;
         return BSDB_OK;
     }
-    if (hipMalloc(p, need) != hipSuccess) return BSDB_ENOMEM;
+    if (dmalloc(p, need) != hipSuccess) return BSDB_ENOMEM;
     *have = need;
     return BSDB_OK;
 }
@@ -202,7 +226,9 @@ struct PinnedPool {
             }
         }
         void *p = nullptr;
-        return hipHostMalloc(&p, XFER_PIECE, hipHostMallocDefault) == hipSuccess ? p : nullptr;
+        if (hipHostMalloc(&p, XFER_PIECE, hipHostMallocDefault) == hipSuccess) return p;
+        (void)hipGetLastError();  // (as dmalloc: not a launch failure)
+        return nullptr;
     }
     void give(void *p) {
         if (!p) return;
@@ -222,10 +248,12 @@ PinnedPool &pinned_pool() {
 int copy_on_own_stream(int dev, void *dst, const void *src, size_t bytes, hipMemcpyKind kind) {
     if (bytes == 0) return BSDB_OK;
     hipStream_t s = nullptr;
-    bool ok = hipSetDevice(dev) == hipSuccess && hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess &&
-              hipMemcpyAsync(dst, src, bytes, kind, s) == hipSuccess && hipStreamSynchronize(s) == hipSuccess;
+    hipError_t e = hipSetDevice(dev);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipMemcpyAsync(dst, src, bytes, kind, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
     if (s) (void)hipStreamDestroy(s);
-    return ok ? BSDB_OK : BSDB_EIO;
+    return e == hipSuccess ? BSDB_OK : hip_fail(e, kind == hipMemcpyHostToDevice ? "H2D copy (own stream)" : "D2H copy (own stream)", __LINE__);
 }
 int d2h_pageable(int dev, void *dst, const void *src, size_t bytes) {
     return copy_on_own_stream(dev, dst, src, bytes, hipMemcpyDeviceToHost);
@@ -238,7 +266,10 @@ int h2d_pageable(int dev, void *dst, const void *src, size_t bytes) {
 // the context's private stream, which only the host-buffer entry points use.
 hipStream_t pick(bsdb_ctx *, void *stream) { return (hipStream_t)stream; }
 
-int launch_status() { return hipGetLastError() == hipSuccess ? BSDB_OK : BSDB_EIO; }
+int launch_status() {
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? BSDB_OK : hip_fail(e, "kernel launch", 0);
+}
 
 // ---- pass-1 dispatch over (source layout, epilogue) ------------------------
 // One-tile-per-workgroup launches: tiles * 512 work-items must stay below 2^32
@@ -343,6 +374,7 @@ D13Sel d13_select(const bsdb_ctx *c, bool var = false, uint32_t key_len = 13, bo
     switch (c->d13_variant) {
         case 1: return {k_pass1_d13e<1>, D13E_NT, D13E_TILE, D13E_MAXP, true, D13E_BIN_IDS};
         case 4: return {k_pass1_d13e<4>, D13E_NT, D13E_TILE, D13E_MAXP, true, D13E_BIN_IDS};
+        case 12: return {k_pass1_d13e<12>, D13E_NT, D13E_TILE, D13E_MAXP, true, D13E_BIN_IDS};
         case 2:
             if (c->d13_threads == 256) return {k_pass1_d13<256>, 256, 256 * P1_KEYS_PER_THREAD, 512, false, 0};
             return {k_pass1_d13<512>, 512, 512 * P1_KEYS_PER_THREAD, 1024, false, 0};
@@ -775,7 +807,7 @@ int bsdb_open(int device, bsdb_ctx **out) {
     }
     // [0] / [4]: overflow flags of id buffers 0 / 1, [2] / [6]: their fallback
     // counts, [3]: single-pass timeouts
-    if (hipMalloc(&c->overflow, sizeof(uint32_t) * 8) != hipSuccess ||
+    if (dmalloc(&c->overflow, sizeof(uint32_t) * 8) != hipSuccess ||
         hipMemset(c->overflow, 0, sizeof(uint32_t) * 8) != hipSuccess) {
         bsdb_close(c);
         return BSDB_ENOMEM;
@@ -791,12 +823,12 @@ static void mph_detach_all(bsdb_ctx *c);
 // payloads, scratch, ledger and slabs, the host feed's device buffers.
 static void release_workspace(bsdb_ctx *c) {
     for (void **p : {&c->ids, &c->d_out, &c->g_sorted, &c->g_pay, &c->g_scratch, &c->g_led, &c->g_mid, &c->g_slabs,
-                     &c->g_big, &c->pack}) {
+                     &c->g_big, &c->pack, &c->g_midscr}) {
         (void)hipFree(*p);
         *p = nullptr;
     }
     c->ids_bytes = c->d_out_bytes = c->g_sorted_bytes = c->g_pay_bytes = c->g_scratch_bytes = c->g_led_bytes =
-        c->g_mid_bytes = c->g_slabs_bytes = c->g_big_bytes = c->pack_bytes = 0;
+        c->g_mid_bytes = c->g_slabs_bytes = c->g_big_bytes = c->pack_bytes = c->g_midscr_bytes = 0;
     for (auto &f : c->feed) {
         if (f.used) (void)hipEventSynchronize(f.done);
         for (int i = 0; i < 8; ++i) {
@@ -854,6 +886,7 @@ int bsdb_close(bsdb_ctx *c) {
     (void)hipFree(c->g_led);
     (void)hipFree(c->g_mid);
     (void)hipFree(c->g_slabs);
+    (void)hipFree(c->g_midscr);
     (void)hipFree(c->pack);
     comm_destroy(c);
     if (c->last_ev) (void)hipEventDestroy(c->last_ev);
@@ -1238,14 +1271,22 @@ static int gov_build_impl(bsdb_ctx *c, const GovSrc &src, uint64_t n_global, uin
     if (st[0] & GOV_DUP) return BSDB_EDUP;
     if (st[0] & GOV_TOO_BIG) return BSDB_E2BIG;
     const uint32_t nbig = std::min(st[3], big_cap);
-    const uint32_t big_grid = std::min<uint32_t>(nbig, 8);
+    // oversized buckets: those up to GM_CMAX keys (all of a random set) in
+    // LDS, one workgroup per CU (k_gov_solve_mid); larger ones (st[1]) in
+    // global slabs (k_gov_solve_big, 8 workgroups)
+    const uint32_t nhuge = std::min(st[1], nbig);
+    const uint32_t sort_grid = std::min<uint32_t>(nbig, (uint32_t)c->num_cus);
+    const uint32_t mid_grid = std::min<uint32_t>(nbig - nhuge, (uint32_t)c->num_cus);
+    const uint32_t big_grid = std::min<uint32_t>(nhuge, 8);
     if (nbig) {
-        // oversized buckets: per-workgroup slabs for the sort, then the solver
-        const size_t sort_bytes = (size_t)big_grid * GB_CMAX * (16 + 8);  // signatures + payloads
+        // per-workgroup slabs for the sort, then the global-slab solver's state
+        const size_t sort_bytes = (size_t)sort_grid * GB_CMAX * (16 + 8);  // signatures + payloads
         if ((rc = grow(&c->g_slabs, &c->g_slabs_bytes, std::max(sort_bytes, (size_t)big_grid * big_slab_bytes()))))
             return rc;
-        k_bucket_sort_big<<<big_grid, GB_THREADS, 0, s>>>(sorted, Eb, e_lo, (const uint32_t *)c->g_big, nbig,
-                                                          (ulonglong2 *)c->g_slabs, status, pay);
+        if (mid_grid && (rc = grow(&c->g_midscr, &c->g_midscr_bytes, (size_t)mid_grid * solve_scratch_words<SolveMid>() * 8)))
+            return rc;
+        k_bucket_sort_big<<<sort_grid, GB_THREADS, 0, s>>>(sorted, Eb, e_lo, (const uint32_t *)c->g_big, nbig,
+                                                           (ulonglong2 *)c->g_slabs, status, pay);
     }
     // BSDB_GOV_PROFILE=1: per-phase cycle totals of the solver printed to stderr
     const bool gprof = getenv("BSDB_GOV_PROFILE") != nullptr;
@@ -1253,7 +1294,7 @@ static int gov_build_impl(bsdb_ctx *c, const GovSrc &src, uint64_t n_global, uin
     uint64_t *d_prof = nullptr;
     if (gprof) {
         void *p = nullptr;
-        HIP_OK(hipMalloc(&p, (size_t)solve_grid * GP_N * 8));
+        HIP_OK(dmalloc(&p, (size_t)solve_grid * GP_N * 8));
         prof_buf.reset(p);
         d_prof = (uint64_t *)p;
         HIP_OK(hipMemsetAsync(d_prof, 0, (size_t)solve_grid * GP_N * 8, s));
@@ -1293,8 +1334,12 @@ static int gov_build_impl(bsdb_ctx *c, const GovSrc &src, uint64_t n_global, uin
         }
         HIP_OK(hipEventRecord(c->big_ev[0], s));
         HIP_OK(hipStreamWaitEvent(c->big_stream, c->big_ev[0], 0));
-        k_gov_solve_big<<<big_grid, GS_THREADS, 0, c->big_stream>>>(sa, (const uint32_t *)c->g_big, nbig,
-                                                                    (uint8_t *)c->g_slabs, big_slab_bytes());
+        if (mid_grid)
+            k_gov_solve_mid<<<mid_grid, GS_THREADS, 0, c->big_stream>>>(sa, (const uint32_t *)c->g_big, nbig,
+                                                                        (uint64_t *)c->g_midscr);
+        if (big_grid)
+            k_gov_solve_big<<<big_grid, GS_THREADS, 0, c->big_stream>>>(sa, (const uint32_t *)c->g_big, nbig,
+                                                                        (uint8_t *)c->g_slabs, big_slab_bytes());
         HIP_OK(hipEventRecord(c->big_ev[1], c->big_stream));
     }
     if (one_per_cu) HIP_OK(hipFuncSetAttribute((const void *)k_gov_solve, hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024));
@@ -1312,7 +1357,7 @@ static int gov_build_impl(bsdb_ctx *c, const GovSrc &src, uint64_t n_global, uin
     const MphView v{d_E, d_values, nullptr, n_global, mult, width};
     if (c->verify && n_local) {
         void *p = nullptr;
-        HIP_OK(hipMalloc(&p, ((n_local + 63) / 64) * 8));
+        HIP_OK(dmalloc(&p, ((n_local + 63) / 64) * 8));
         std::unique_ptr<void, DevFree> bm(p);
         HIP_OK(hipMemsetAsync(p, 0, ((n_local + 63) / 64) * 8, s));
         k_verify_ranks<<<grid, 256, 0, s>>>(v, sorted, n_local, e_lo, (unsigned long long *)p, status);

@@ -129,9 +129,9 @@ int dev_reserve(bsdb_ctx *c, void **p, size_t *cap, size_t used, size_t need) {
     if (need <= *cap) return BSDB_OK;
     void *q = nullptr;
     size_t nc = std::max(need, *cap + *cap / 2);
-    if (hipMalloc(&q, nc) != hipSuccess) {
+    if (dmalloc(&q, nc) != hipSuccess) {
         nc = need;
-        if (hipMalloc(&q, nc) != hipSuccess) return BSDB_ENOMEM;
+        if (dmalloc(&q, nc) != hipSuccess) return BSDB_ENOMEM;
     }
     if (used) HIP_OK(hipMemcpyAsync(q, *p, used, hipMemcpyDeviceToDevice, c->stream));
     HIP_OK(hipStreamSynchronize(c->stream));
@@ -379,9 +379,9 @@ int builder_finish_locked(bsdb_builder *b, uint32_t width, uint32_t passes, cons
         if (!host_gather) {
             const int dev = c->device;
             int up_rc = BSDB_OK;
-            if (!b->stride && (hipMalloc(&d_addr, n * 8) != hipSuccess || (up_rc = h2d_pageable(dev, d_addr, b->addr.p, n * 8))))
+            if (!b->stride && (dmalloc(&d_addr, n * 8) != hipSuccess || (up_rc = h2d_pageable(dev, d_addr, b->addr.p, n * 8))))
                 return done(up_rc ? up_rc : BSDB_ENOMEM);
-            if (b->approx && (hipMalloc(&d_v8, n * 8) != hipSuccess || hipMalloc(&d_vl, n) != hipSuccess ||
+            if (b->approx && (dmalloc(&d_v8, n * 8) != hipSuccess || dmalloc(&d_vl, n) != hipSuccess ||
                               (up_rc = h2d_pageable(dev, d_v8, b->value8.p, n * 8)) ||
                               (up_rc = h2d_pageable(dev, d_vl, b->vlen.p, n))))
                 return done(up_rc ? up_rc : BSDB_ENOMEM);

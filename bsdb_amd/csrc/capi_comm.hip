@@ -191,7 +191,7 @@ int multi_grow(bsdb_multi *mc, uint64_t m) {
         if (mc->E[i]) (void)hipFree(mc->E[i]);
         mc->counts[i] = nullptr;
         mc->E[i] = nullptr;
-        if (hipMalloc(&mc->counts[i], m * 4) != hipSuccess || hipMalloc(&mc->E[i], (m + 1) * 8) != hipSuccess)
+        if (dmalloc(&mc->counts[i], m * 4) != hipSuccess || dmalloc(&mc->E[i], (m + 1) * 8) != hipSuccess)
             return BSDB_ENOMEM;
     }
     mc->m_alloc = m;

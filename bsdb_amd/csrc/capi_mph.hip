@@ -81,8 +81,8 @@ int mph_alloc(bsdb_ctx *c, uint64_t n, uint32_t width, bsdb_mph **out) {
     p->width = width;
     p->values_words = bsdb_values_words(n);
     p->sig_words = mph_sig_words(n, width);
-    if (hipMalloc(&p->E, (p->m + 1) * 8) != hipSuccess || hipMalloc(&p->values, p->values_words * 8) != hipSuccess ||
-        (width && hipMalloc(&p->sigbits, p->sig_words * 8) != hipSuccess)) {
+    if (dmalloc(&p->E, (p->m + 1) * 8) != hipSuccess || dmalloc(&p->values, p->values_words * 8) != hipSuccess ||
+        (width && dmalloc(&p->sigbits, p->sig_words * 8) != hipSuccess)) {
         mph_release(p);
         return BSDB_ENOMEM;
     }
@@ -99,7 +99,7 @@ int mph_build_locked(bsdb_ctx *c, uint64_t n, uint32_t width, bsdb_mph **out, in
     int rc = mph_alloc(c, n, width, &p);
     if (rc) return rc;
     void *sig = nullptr;
-    if (hipMalloc(&sig, std::max<uint64_t>(n, 1) * 16) != hipSuccess) {
+    if (dmalloc(&sig, std::max<uint64_t>(n, 1) * 16) != hipSuccess) {
         mph_release(p);
         return BSDB_ENOMEM;
     }
@@ -166,7 +166,7 @@ int mph_build_index(bsdb_ctx *c, uint64_t n, uint32_t width, const uint64_t *h_a
         for (void *q : {rank, addr, index, v8, vl, index_a}) (void)hipFree(q);
         return close_all(rc);
     };
-    if (hipMalloc(&rank, nn * 8) != hipSuccess || hipMalloc(&addr, nn * 8) != hipSuccess)
+    if (dmalloc(&rank, nn * 8) != hipSuccess || dmalloc(&addr, nn * 8) != hipSuccess)
         return free_all(BSDB_ENOMEM);
     // the record addresses go up while the MPHF builds (the solve leaves PCIe idle)
     int addr_rc = BSDB_OK;
@@ -179,24 +179,25 @@ int mph_build_index(bsdb_ctx *c, uint64_t n, uint32_t width, const uint64_t *h_a
         mph_release(p);
         return free_all(addr_rc);
     }
-    if (hipMalloc(&index, nn * 8) != hipSuccess ||
-        (approx && (hipMalloc(&v8, nn * 8) != hipSuccess || hipMalloc(&vl, nn) != hipSuccess ||
-                    hipMalloc(&index_a, nn * 8) != hipSuccess))) {
+    if (dmalloc(&index, nn * 8) != hipSuccess ||
+        (approx && (dmalloc(&v8, nn * 8) != hipSuccess || dmalloc(&vl, nn) != hipSuccess ||
+                    dmalloc(&index_a, nn * 8) != hipSuccess))) {
         mph_release(p);
         return free_all(BSDB_ENOMEM);
     }
-    bool ok = hipMemsetAsync(index, 0, nn * 8, c->stream) == hipSuccess;
+    auto chk = [](hipError_t e, const char *what, int line) { return e == hipSuccess || (hip_fail(e, what, line), false); };
+    bool ok = chk(hipMemsetAsync(index, 0, nn * 8, c->stream), "memset index", __LINE__);
     if (ok && approx)
-        ok = hipMemcpyAsync(v8, h_value8, n * 8, hipMemcpyHostToDevice, c->stream) == hipSuccess &&
-             hipMemcpyAsync(vl, h_vlen, n, hipMemcpyHostToDevice, c->stream) == hipSuccess &&
-             hipMemsetAsync(index_a, 0, nn * 8, c->stream) == hipSuccess;
+        ok = chk(hipMemcpyAsync(v8, h_value8, n * 8, hipMemcpyHostToDevice, c->stream), "H2D value8", __LINE__) &&
+             chk(hipMemcpyAsync(vl, h_vlen, n, hipMemcpyHostToDevice, c->stream), "H2D vlen", __LINE__) &&
+             chk(hipMemsetAsync(index_a, 0, nn * 8, c->stream), "memset index_a", __LINE__);
     if (ok && n) {
         k_index_scatter<<<grid_for(c, n), 256, 0, c->stream>>>((const int64_t *)rank, (const uint64_t *)addr, n, 0, n,
                                                                 (uint64_t *)index, (const uint64_t *)v8,
                                                                 (const uint8_t *)vl, (uint8_t *)index_a);
-        ok = hipGetLastError() == hipSuccess;
+        ok = chk(hipGetLastError(), "k_index_scatter", __LINE__);
     }
-    ok = ok && hipStreamSynchronize(c->stream) == hipSuccess;
+    ok = ok && chk(hipStreamSynchronize(c->stream), "sync", __LINE__);
     if (ok) {
         FILE *fs[2] = {f, fa};
         const void *ds[2] = {index, index_a};
@@ -356,7 +357,7 @@ int write_files(int device, FILE *const *files, const void *const *d_srcs, int n
             if (st) ok = hipStreamSynchronize(st) == hipSuccess && ok;
             if (!ok) {
                 int expect = BSDB_OK;
-                rc.compare_exchange_strong(expect, BSDB_EIO);
+                if (rc.compare_exchange_strong(expect, BSDB_EIO)) (void)hip_fail(hipGetLastError(), "write_files piece", __LINE__);
             }
             for (int i = 0; i < 2; ++i) {
                 pinned_pool().give(pin[i]);
@@ -638,8 +639,8 @@ int bsdb_index_open(bsdb_mph *p, int approximate, uint64_t pass_cache_bytes, con
         {
             std::lock_guard<std::mutex> g(p->c->mu);
             alloc_ok = hipSetDevice(p->c->device) == hipSuccess &&
-                       hipMalloc(&ix->d_index, ix->pass_size * 8) == hipSuccess &&
-                       (!ix->approx || hipMalloc(&ix->d_index_a, ix->pass_size * 8) == hipSuccess);
+                       dmalloc(&ix->d_index, ix->pass_size * 8) == hipSuccess &&
+                       (!ix->approx || dmalloc(&ix->d_index_a, ix->pass_size * 8) == hipSuccess);
         }
         // (bsdb_index_close takes the context lock itself: called after the scope)
         if (!alloc_ok) {

@@ -48,7 +48,7 @@ struct DevBufs {
         // a fresh host thread's current device is 0: allocate on OUR device
         void *q = nullptr;
         if (hipSetDevice(device) != hipSuccess) return BSDB_EIO;
-        if (hipMalloc(&q, std::max<uint64_t>(count, 1) * sizeof(T)) != hipSuccess) return BSDB_ENOMEM;
+        if (dmalloc(&q, std::max<uint64_t>(count, 1) * sizeof(T)) != hipSuccess) return BSDB_ENOMEM;
         ptrs.push_back(q);
         *p = (T *)q;
         return BSDB_OK;

@@ -59,7 +59,7 @@ int passes_build(bsdb_ctx *c, const GovSrc &src, uint64_t n, uint32_t width, uin
     const bool fixed_ok = src.off || (!bad_key_len(src.key_len) && aligned16(src.keys));
     if (n >= (1ULL << 16) && fixed_ok) {
         void *q = nullptr;
-        HIP_OK(hipMalloc(&q, m * 4));
+        HIP_OK(dmalloc(&q, m * 4));
         counts_all.reset(q);
         HIP_OK(hipMemsetAsync(q, 0, m * 4, s));
         const uint64_t saved_chunk = c->chunk_keys;

@@ -46,6 +46,11 @@ constexpr int GS_WMAX = (GS_CMAX + 1 + 63) / 64;  // words per bit-sliced row
 // above the mean for random keys) are solved by the same code with its state
 // in a per-workgroup slab of global memory, up to GB_CMAX keys.
 constexpr int GB_CMAX = 16384;  // a power of two (the bitonic sort's padding)
+// Oversized buckets up to GM_CMAX keys (every one of a random key set: the
+// largest of C4's 8.8 M buckets holds ~1 720) are solved with their state in
+// LDS by k_gov_solve_mid, one workgroup per CU; only larger (adversarial)
+// buckets take the global-slab kernel, whose every state access goes to L2.
+constexpr int GM_CMAX = 2048;
 constexpr int GB_THREADS = 256;  // sort of an oversized bucket
 // FVS: most heavy hinges of a block (a larger set falls back to Gauss-Jordan
 // over the whole block).  SolveArgs::fvs_max may lower it (tests force the
@@ -375,6 +380,8 @@ __global__ __launch_bounds__(256) void k_big_list(const uint64_t *Eb, uint64_t n
             atomicOr(status, (uint32_t)GOV_TOO_BIG);
             continue;
         }
+        const uint64_t nv = vertex_offset(Eb[b + 1] & OFFSET_MASK) - vertex_offset(Eb[b] & OFFSET_MASK);
+        if (cnt > (uint64_t)GM_CMAX || nv > (uint64_t)(GM_CMAX + GM_CMAX / 8)) atomicAdd(status + 1, 1u);  // global-slab kernel
         const uint32_t i = atomicAdd(status + 3, 1u);
         if (i < cap) list[i] = (uint32_t)b;
     }
@@ -532,6 +539,9 @@ struct SolveLdsT {
 };
 using SolveLds = SolveLdsT<GS_CMAX>;
 using SolveBig = SolveLdsT<GB_CMAX>;
+using SolveMid = SolveLdsT<GM_CMAX>;
+static_assert(SolveMid::NVMAX == GM_CMAX + GM_CMAX / 8, "k_big_list's mid test");
+static_assert(sizeof(SolveMid) + 64 <= 160 * 1024, "k_gov_solve_mid: one workgroup per CU");
 static_assert(SolveLds::NVMAX == GS_NVMAX && SolveLds::WMAX == GS_WMAX, "LDS layout");
 static_assert(sizeof(SolveLds) + 64 <= 160 * 1024 / GS_PER_CU, "GS_PER_CU solver workgroups per CU");
 // per-workgroup global scratch of the dense phase (bit-sliced rows, forms)
@@ -2089,14 +2099,32 @@ __global__ __launch_bounds__(GS_THREADS, GS_THREADS * GS_PER_CU / 256) void k_go
     }
 }
 
-// The oversized buckets of k_big_list: one per workgroup at a time, solver
-// state in a global slab (slabs[blockIdx.x]), dense scratch after it.
+// whether oversized bucket b fits k_gov_solve_mid's LDS state
+__device__ __forceinline__ bool mid_bucket(const SolveArgs &a, uint64_t b) {
+    const uint64_t lo = a.E[b] & OFFSET_MASK, hi = a.E[b + 1] & OFFSET_MASK;
+    return hi - lo <= (uint64_t)GM_CMAX && vertex_offset(hi) - vertex_offset(lo) <= (uint64_t)SolveMid::NVMAX;
+}
+
+// The oversized buckets of k_big_list that fit GM_CMAX: state in LDS (one
+// workgroup per CU), dense scratch per workgroup in global memory.
+__global__ __launch_bounds__(GS_THREADS) void k_gov_solve_mid(SolveArgs a, const uint32_t *list, uint32_t nbig,
+                                                              uint64_t *scratch) {
+    __shared__ SolveMid L;
+    uint64_t *scr = scratch + (size_t)blockIdx.x * solve_scratch_words<SolveMid>();
+    PhaseClock pc{nullptr, 0};
+    for (uint32_t li = blockIdx.x; li < nbig; li += gridDim.x)
+        if (mid_bucket(a, a.b0 + list[li])) solve_bucket(L, a, a.b0 + list[li], scr, pc);
+}
+
+// The rest of them: one per workgroup at a time, solver state in a global
+// slab (slabs[blockIdx.x]), dense scratch after it.
 __global__ __launch_bounds__(GS_THREADS) void k_gov_solve_big(SolveArgs a, const uint32_t *list, uint32_t nbig,
                                                               uint8_t *slabs, size_t slab_bytes) {
     SolveBig &L = *reinterpret_cast<SolveBig *>(slabs + (size_t)blockIdx.x * slab_bytes);
     uint64_t *scr = reinterpret_cast<uint64_t *>(slabs + (size_t)blockIdx.x * slab_bytes + ((sizeof(SolveBig) + 255) & ~(size_t)255));
     PhaseClock pc{nullptr, 0};
-    for (uint32_t li = blockIdx.x; li < nbig; li += gridDim.x) solve_bucket(L, a, a.b0 + list[li], scr, pc);
+    for (uint32_t li = blockIdx.x; li < nbig; li += gridDim.x)
+        if (!mid_bucket(a, a.b0 + list[li])) solve_bucket(L, a, a.b0 + list[li], scr, pc);
 }
 
 // bytes of one k_gov_solve_big workgroup slab (state + dense scratch)

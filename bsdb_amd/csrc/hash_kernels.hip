@@ -595,7 +595,10 @@ constexpr uint16_t ID_PAD = 0xFFFF;                       // not a local id (ids
 
 // VARIANT 0 is production.  Profiling only (results invalid): 1 = hash and
 // bins, no cursor atomics and no write-out; 4 = per-wave phase cycles
-// (s_memtime) written over counts[8*wave ..] (tools/stamp_probe_e.py).
+// (s_memtime) written over counts[8*wave ..] (tools/stamp_probe_e.py);
+// 12 = everything but the hash: the same loads, bins, cursor atomics and
+// write-out with a 2-instruction stand-in bucket (uniform over [0, m) for
+// random key bytes) -- what pass 1's memory traffic alone costs.
 // L: the key length, 13 or an aligned 8 / 12 / 16 (the same design; the
 // 16-byte window of a key then starts at the key itself).
 template <int VARIANT, bool SEED0 = false, int L = 13>
@@ -655,7 +658,9 @@ __global__ __launch_bounds__(D13E_NT, 1) void k_pass1_d13e(P1Args a, uint64_t nt
         uint32_t b[D13_Q], r[D13_Q];
 #pragma unroll
         for (int j = 0; j < D13_Q; ++j) {
-            if constexpr (L == 13)
+            if constexpr (VARIANT == 12)
+                b[j] = __umulhi(S[q][j].x ^ S[q][j].z, mult >> 1);
+            else if constexpr (L == 13)
                 b[j] = spooky13_bucket(S[q][j].x, S[q][j].y, S[q][j].z, S[q][j].w, sh, seed, mult);
             else
                 b[j] = spooky_fix_bucket<L>(S[q][j].x, S[q][j].y, S[q][j].z, S[q][j].w, seed, mult);

@@ -212,10 +212,11 @@ def skewed_keys(n_total, big, rng_seed=3):
     return np.concatenate([k[b == 0][:big], k[b != 0][: n_total - big]]).reshape(-1)
 
 
-@pytest.mark.parametrize("n_total,big", [(3001, 2100), (4500, 4000)])
+@pytest.mark.parametrize("n_total,big", [(3001, 1700), (3001, 2040), (3001, 2100), (4500, 4000)])
 def test_oversized_bucket_matches_oracle(ctx, n_total, big):
-    """A bucket over the LDS solver's 2048 keys goes to the global-memory
-    solver (no BSDB_E2BIG), bit-identical to the oracle."""
+    """A bucket over the main solver's 1 664 keys: up to 2 048 keys it is
+    solved in LDS by k_gov_solve_mid (one workgroup per CU), above that by
+    the global-memory solver (no BSDB_E2BIG); bit-identical to the oracle."""
     keys = skewed_keys(n_total, big)
     sig = O.hash_fixed(keys, 13)
     rc, E, vals, sb = O.gov_build(sig, 4)

@@ -3,7 +3,7 @@
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 OUT=gpurun_out/${TAG:-r4a}; mkdir -p $OUT
-{
+[ -z "$NOPROBE" ] && {
   echo "== free"; free -g
   echo "== df"; df -h /tmp /dev/shm "$HOME" "$GRAFT_REPO_ROOT" 2>&1
   echo "== mounts"; grep -E " / | /tmp | /dev/shm " /proc/mounts
@@ -12,8 +12,8 @@ OUT=gpurun_out/${TAG:-r4a}; mkdir -p $OUT
   echo "== dd 8 GiB to /tmp (fdatasync)"; dd if=/dev/zero of=/tmp/bsdb_dd_probe bs=64M count=128 conv=fdatasync 2>&1 | tail -1
   rm -f /tmp/bsdb_dd_probe
 } > $OUT/box_probe.txt 2>&1
-cat $OUT/box_probe.txt
-timeout -k 10 900 python -u -m pytest tests/test_builder_gpu.py -x -v --timeout 600 --timeout-method thread > $OUT/pytest_builder.log 2>&1 || { tail -n 40 $OUT/pytest_builder.log; exit 1; }
+[ -z "$NOPROBE" ] && cat $OUT/box_probe.txt
+timeout -k 10 900 python -u -m pytest ${TESTS:-tests/test_builder_gpu.py} ${KEXPR:+-k "$KEXPR"} -x -v --timeout 600 --timeout-method thread > $OUT/pytest_builder.log 2>&1 || { tail -n 40 $OUT/pytest_builder.log; exit 1; }
 tail -n 3 $OUT/pytest_builder.log
 [ -n "$NOTRACE" ] && exit 0
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/rp -o c4 --output-format csv -- python3 tools/c4_trace.py --host-index > $OUT/c4.log 2>&1 || { tail -20 $OUT/c4.log; exit 3; }

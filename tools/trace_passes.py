@@ -14,7 +14,8 @@ import sys
 def main():
     path = sys.argv[1]
     rows = []
-    with open(path) as f:
+    import gzip
+    with (gzip.open(path, "rt") if path.endswith(".gz") else open(path)) as f:
         for r in csv.DictReader(f):
             rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
     rows.sort()
@@ -23,7 +24,7 @@ def main():
     passes = []
     cur = None
     for s, e, name in rows:
-        short = name.split("(")[0].split("<")[0].replace("void ", "").strip()
+        short = name.split("(")[0].split("<")[0].replace("void ", "").strip().split("::")[-1]
         if short == "k_sel" and "<1" in name:
             cur = {"sel_start": ms(s), "kernels": {}}
             passes.append(cur)
@@ -37,7 +38,8 @@ def main():
     out = []
     for i, p in enumerate(passes):
         kk = p["kernels"]
-        main_k, big_k = kk.get("k_gov_solve"), kk.get("k_gov_solve_big")
+        main_k = kk.get("k_gov_solve")
+        big_k = kk.get("k_gov_solve_big") or kk.get("k_gov_solve_mid")
         row = {"pass": i, "sel_start_ms": round(p["sel_start"], 2)}
         if main_k:
             row["solve_ms"] = [round(main_k["start"], 2), round(main_k["end"], 2)]
