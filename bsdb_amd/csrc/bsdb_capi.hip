@@ -256,7 +256,29 @@ int copy_on_own_stream(int dev, void *dst, const void *src, size_t bytes, hipMem
     return e == hipSuccess ? BSDB_OK : hip_fail(e, kind == hipMemcpyHostToDevice ? "H2D copy (own stream)" : "D2H copy (own stream)", __LINE__);
 }
 int d2h_pageable(int dev, void *dst, const void *src, size_t bytes) {
-    return copy_on_own_stream(dev, dst, src, bytes, hipMemcpyDeviceToHost);
+    // BSDB_D2H_THREADS=T (A/B knob, default 1): the copy cut into T ranges,
+    // each on a thread and stream of its own (the runtime's pageable path
+    // stages and page-faults per copy)
+    static const int T = [] {
+        const char *v = getenv("BSDB_D2H_THREADS");
+        return v ? std::max(1, std::min(atoi(v), 32)) : 1;
+    }();
+    if (T == 1 || bytes < (64ull << 20)) return copy_on_own_stream(dev, dst, src, bytes, hipMemcpyDeviceToHost);
+    const size_t piece = ((bytes + T - 1) / T + 4095) & ~(size_t)4095;
+    std::vector<std::thread> th;
+    std::vector<int> rc(T, BSDB_OK);
+    for (int t = 0; t < T; ++t) {
+        const size_t o = (size_t)t * piece;
+        if (o >= bytes) break;
+        const size_t k = std::min(piece, bytes - o);
+        th.emplace_back([&, t, o, k] {
+            rc[t] = copy_on_own_stream(dev, (uint8_t *)dst + o, (const uint8_t *)src + o, k, hipMemcpyDeviceToHost);
+        });
+    }
+    for (auto &x : th) x.join();
+    for (int r : rc)
+        if (r) return r;
+    return BSDB_OK;
 }
 int h2d_pageable(int dev, void *dst, const void *src, size_t bytes) {
     return copy_on_own_stream(dev, dst, src, bytes, hipMemcpyHostToDevice);
@@ -1301,6 +1323,7 @@ static int gov_build_impl(bsdb_ctx *c, const GovSrc &src, uint64_t n_global, uin
     }
     uint32_t fvs_max = FVS_NH_MAX;
     if (const char *v = getenv("BSDB_GOV_FVS_MAX")) fvs_max = (uint32_t)std::max(2, std::min(atoi(v), (int)FVS_NH_MAX));
+    if (getenv("BSDB_GOV_GJ_COLUMN")) fvs_max |= 0x80000000u;  // A/B: the heavy system by columns
     if (width && full) HIP_OK(hipMemsetAsync(d_sigbits, 0, ((n_global * width + 63) / 64 + 1) * 8, s));
     // the seed ledger: claim, won, done (u32 per bucket), fail (4 u64 per
     // bucket), zeroed; active (u32 per workgroup), all ones

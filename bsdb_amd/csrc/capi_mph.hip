@@ -126,6 +126,14 @@ int mph_build(bsdb_ctx *c, uint64_t n, uint32_t width, bsdb_mph **out, HashDev &
 
 int write_files(int device, FILE *const *files, const void *const *d_srcs, int nfiles, uint64_t bytes);
 
+// An index file, created/truncated (W:124-127), open for reading too so the
+// writer can map it (w+b); a path that cannot be opened so (a write-only
+// device) falls back to wb.
+FILE *fopen_index(const char *path) {
+    FILE *f = fopen(path, "w+b");
+    return f ? f : fopen(path, "wb");
+}
+
 }  // namespace
 
 // capi_builder.hip: the same files by bucket-range passes (the F2 entry
@@ -147,8 +155,8 @@ int mph_build_index(bsdb_ctx *c, uint64_t n, uint32_t width, const uint64_t *h_a
                     bsdb_mph **out, HashDev &&hash_dev) {
     if (n / BUCKET_SIZE + 1 > 0x7FFFFFFFULL) return BSDB_EINVAL;
     // W:124-127: both files created first (index_a.db empty in exact mode)
-    FILE *f = fopen(index_path, "wb");
-    FILE *fa = index_a_path ? fopen(index_a_path, "wb") : nullptr;
+    FILE *f = fopen_index(index_path);
+    FILE *fa = index_a_path ? fopen_index(index_a_path) : nullptr;
     auto close_all = [&](int rc) {
         bool ok = true;
         if (f) ok = fclose(f) == 0 && ok;
@@ -322,6 +330,25 @@ int write_files(int device, FILE *const *files, const void *const *d_srcs, int n
         if (fd < 0 || base < 0) return BSDB_EFILE;
         const uint8_t *src = (const uint8_t *)d_srcs[fi];
         std::atomic<int> rc{BSDB_OK};
+        // a regular file is extended to its new end and the range mapped:
+        // parallel pwrite()s to one file serialise on its inode lock, stores
+        // into a shared mapping do not (capi_builder.hip's OutFile)
+        uint8_t *map = nullptr;
+        size_t map_len = 0, map_skip = 0;
+        {
+            struct stat st;
+            if (!getenv("BSDB_NO_MMAP_WRITE") && fstat(fd, &st) == 0 && S_ISREG(st.st_mode)) {
+                const off_t end = base + (off_t)bytes;
+                if (st.st_size >= end || ftruncate(fd, end) == 0) {
+                    const off_t pg = (off_t)sysconf(_SC_PAGESIZE);
+                    const off_t mbase = base / pg * pg;
+                    map_skip = (size_t)(base - mbase);
+                    map_len = map_skip + (size_t)bytes;
+                    void *m = mmap(nullptr, map_len, PROT_READ | PROT_WRITE, MAP_SHARED, fd, mbase);
+                    if (m != MAP_FAILED) map = (uint8_t *)m;
+                }
+            }
+        }
         auto work = [&](uint64_t t) {
             hipStream_t st = nullptr;
             void *pin[2] = {nullptr, nullptr};
@@ -343,6 +370,10 @@ int write_files(int device, FILE *const *files, const void *const *d_srcs, int n
                 ok = ok && hipEventSynchronize(done[i]) == hipSuccess;
                 if (!ok) break;
                 const uint64_t len = len_of(j);
+                if (map) {
+                    memcpy(map + map_skip + j * XFER_PIECE, pin[i], len);
+                    continue;
+                }
                 uint64_t w = 0;
                 while (w < len) {
                     const ssize_t r = pwrite(fd, (const uint8_t *)pin[i] + w, len - w, base + (off_t)(j * XFER_PIECE + w));
@@ -369,6 +400,7 @@ int write_files(int device, FILE *const *files, const void *const *d_srcs, int n
         for (uint64_t t = 1; t < T; ++t) th.emplace_back(work, t);
         work(0);
         for (auto &x : th) x.join();
+        if (map && munmap(map, map_len) != 0 && !rc.load()) rc.store(BSDB_EFILE);
         if (rc.load()) return rc.load();
         if (fseeko(files[fi], base + (off_t)bytes, SEEK_SET) != 0) return BSDB_EFILE;  // the FILE's position after the data
     }
@@ -631,8 +663,8 @@ int bsdb_index_open(bsdb_mph *p, int approximate, uint64_t pass_cache_bytes, con
     ix->pass_size = std::min(p->n, pass_cache_bytes / 8);
     ix->passes = ix->pass_size ? (p->n + ix->pass_size - 1) / ix->pass_size : 0;
     // W:124-127: both files are created (truncated), index_a.db even in exact mode
-    ix->f = fopen(index_path, "wb");
-    if (index_a_path) ix->fa = fopen(index_a_path, "wb");
+    ix->f = fopen_index(index_path);
+    if (index_a_path) ix->fa = fopen_index(index_a_path);
     bool ok = ix->f && (!index_a_path || ix->fa);
     if (ok && ix->pass_size) {
         bool alloc_ok;
