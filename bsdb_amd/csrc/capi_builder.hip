@@ -284,31 +284,45 @@ int builder_add_fixed_locked(bsdb_builder *b, const uint8_t *h_keys, uint32_t ke
     return BSDB_OK;
 }
 
-int builder_add_var_locked(bsdb_builder *b, const uint8_t *h_blob, const uint64_t *h_off, uint64_t count) {
-    bsdb_ctx *c = b->c;
-    const uint64_t o0 = h_off[0];
-    for (uint64_t i = 0; i < count; ++i)
+// The lengths of a batch of variable-length keys: checked non-decreasing,
+// and whether they all equal one length (*len, or 0xFFFFFFFF when they
+// differ).  No builder state: callers may run it outside the lock.
+int var_batch_lengths(const uint64_t *h_off, uint64_t count, uint32_t *len) {
+    uint32_t l0 = count ? (uint32_t)std::min<uint64_t>(h_off[1] - h_off[0], 0xFFFFFFFEu) : 0;
+    bool same = true;
+    for (uint64_t i = 0; i < count; ++i) {
         if (h_off[i + 1] < h_off[i]) return BSDB_EINVAL;
-    const uint64_t bytes = h_off[count] - o0;
+        same = same && h_off[i + 1] - h_off[i] == l0;
+    }
+    *len = same ? l0 : 0xFFFFFFFFu;
+    return BSDB_OK;
+}
+
+// offsets of a batch rebased onto the resident blob on the device:
+// off[i] = h_off[i+1] - o0 + base, uploaded as they are and shifted here
+__global__ __launch_bounds__(256) void k_rebase_offsets(uint64_t *off, uint64_t count, uint64_t shift) {
+    const uint64_t step = (uint64_t)gridDim.x * 256;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < count; i += step) off[i] += shift;
+}
+
+// one add of variable-length keys whose lengths var_batch_lengths has
+// checked (uni: their common length or 0xFFFFFFFF)
+int builder_add_var_locked(bsdb_builder *b, const uint8_t *h_blob, const uint64_t *h_off, uint64_t count,
+                           uint32_t uni) {
+    bsdb_ctx *c = b->c;
+    if (count == 0) return BSDB_OK;
+    const uint64_t o0 = h_off[0], bytes = h_off[count] - o0;
     int rc = dev_reserve(c, (void **)&b->d_keys, &b->keys_cap, b->key_bytes, b->key_bytes + bytes + 16);
     if (rc) return rc;
     if ((rc = dev_reserve(c, (void **)&b->d_off, &b->off_cap, (b->n + 1) * 8, (b->n + count + 1) * 8))) return rc;
     if (bytes) HIP_OK(hipMemcpyAsync(b->d_keys + b->key_bytes, h_blob + o0, bytes, hipMemcpyHostToDevice, c->stream));
-    // offsets rebased onto the resident blob, in host chunks
-    constexpr uint64_t CH = 1ULL << 22;
-    std::vector<uint64_t> reb((size_t)std::min<uint64_t>(count, CH));
-    for (uint64_t k0 = 0; k0 < count; k0 += CH) {
-        const uint64_t k = std::min(CH, count - k0);
-        for (uint64_t i = 0; i < k; ++i) {
-            const uint64_t e = h_off[k0 + i + 1], l = e - h_off[k0 + i];
-            reb[i] = b->key_bytes + (e - o0);
-            if (b->n + k0 + i == 0) b->uni_len = (uint32_t)std::min<uint64_t>(l, 0xFFFFFFFFu);
-            b->uniform = b->uniform && l == b->uni_len;
-        }
-        HIP_OK(hipMemcpyAsync(b->d_off + b->n + 1 + k0, reb.data(), k * 8, hipMemcpyHostToDevice, c->stream));
-        HIP_OK(hipStreamSynchronize(c->stream));
-    }
-    HIP_OK(hipStreamSynchronize(c->stream));
+    uint64_t *dst = b->d_off + b->n + 1;
+    HIP_OK(hipMemcpyAsync(dst, h_off + 1, count * 8, hipMemcpyHostToDevice, c->stream));
+    k_rebase_offsets<<<grid_for(c, count), 256, 0, c->stream>>>(dst, count, b->key_bytes - o0);
+    HIP_OK(hipStreamSynchronize(c->stream));  // the caller may reuse its buffers
+    if ((rc = launch_status())) return rc;
+    if (b->n == 0) b->uni_len = uni;
+    b->uniform = b->uniform && uni != 0xFFFFFFFFu && uni == b->uni_len;
     b->key_bytes += bytes;
     return BSDB_OK;
 }
@@ -368,6 +382,7 @@ int builder_finish_locked(bsdb_builder *b, uint32_t width, uint32_t passes, cons
     bsdb_ctx *c = b->c;
     const uint64_t n = b->n;
     OutFile fo, fao;
+    Populator pop_o, pop_a;
     void *d_addr = nullptr, *d_v8 = nullptr, *d_vl = nullptr;
     void *slot_a[2] = {nullptr, nullptr};
     size_t slot_a_bytes[2] = {0, 0};
@@ -375,6 +390,10 @@ int builder_finish_locked(bsdb_builder *b, uint32_t width, uint32_t passes, cons
     auto done = [&](int rc) {
         (void)hipStreamSynchronize(c->stream);
         for (void *q : {d_addr, d_v8, d_vl, slot_a[0], slot_a[1]}) (void)hipFree(q);
+        pop_o.finish();
+        pop_a.finish();
+        if (getenv("BSDB_BUILDER_PROFILE") && fo.map)
+            fprintf(stderr, "[bsdb builder] index pages prefaulted in %.3f s (index_a %.3f s)\n", pop_o.seconds, pop_a.seconds);
         if (close_out(fo) && !rc) rc = BSDB_EFILE;
         if (close_out(fao) && !rc) rc = BSDB_EFILE;
         if (rc && p) mph_release(p);
@@ -386,6 +405,8 @@ int builder_finish_locked(bsdb_builder *b, uint32_t width, uint32_t passes, cons
     if (index_path && ((rc = open_out(index_path, n * 8, &fo)) ||
                        (index_a_path && (rc = open_out(index_a_path, b->approx ? n * 8 : 0, &fao)))))
         return done(rc);
+    pop_o.start(fo.map, fo.bytes);
+    pop_a.start(fao.map, fao.bytes);
     if ((rc = mph_alloc(c, n, width, &p))) return done(rc);
     if (n == 0) {  // E = {0}, no values beyond the trailing word (GOV:484)
         HIP_OK(hipMemsetAsync(p->E, 0, (p->m + 1) * 8, c->stream));
@@ -555,7 +576,11 @@ static int host_passes_build(bsdb_ctx *c, const uint8_t *h_keys, uint32_t key_le
         if (var) {
             k1 = std::min<uint64_t>(n, k0 + (1ULL << 28));
             while (k1 - k0 > 1 && h_off[k1] - h_off[k0] > BATCH) k1 = k0 + (k1 - k0) / 2;
-            rc = builder_add(b, k1 - k0, nullptr, nullptr, nullptr, [&] { return builder_add_var_locked(b, h_blob, h_off + k0, k1 - k0); });
+            uint32_t uni = 0;
+            rc = var_batch_lengths(h_off + k0, k1 - k0, &uni);
+            if (!rc)
+                rc = builder_add(b, k1 - k0, nullptr, nullptr, nullptr,
+                                 [&] { return builder_add_var_locked(b, h_blob, h_off + k0, k1 - k0, uni); });
         } else {
             k1 = std::min(n, k0 + std::max<uint64_t>(1, BATCH / key_len));
             rc = builder_add(b, k1 - k0, nullptr, nullptr, nullptr,
@@ -609,8 +634,10 @@ int bsdb_builder_add_fixed(bsdb_builder *b, const uint8_t *h_keys, uint32_t key_
 int bsdb_builder_add_var(bsdb_builder *b, const uint8_t *h_blob, const uint64_t *h_off, uint64_t count,
                          const uint64_t *h_addr, const uint64_t *h_value8, const uint8_t *h_vlen) {
     if (!b || b->key_len || (count && (!h_blob || !h_off))) return BSDB_EINVAL;
+    uint32_t uni = 0;
+    if (count && var_batch_lengths(h_off, count, &uni)) return BSDB_EINVAL;
     return builder_add(b, count, h_addr, h_value8, h_vlen,
-                       [&] { return builder_add_var_locked(b, h_blob, h_off, count); });
+                       [&] { return builder_add_var_locked(b, h_blob, h_off, count, uni); });
 }
 
 int bsdb_builder_count(const bsdb_builder *b, uint64_t *n) {

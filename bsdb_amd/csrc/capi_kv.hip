@@ -44,13 +44,20 @@ constexpr uint32_t KV_PAGE = 4096;  // NativeFileIO.PAGE_SIZE
 
 struct KvPart {
     std::vector<uint8_t> blob;
-    std::vector<uint64_t> len_end;  // running key-byte totals (offsets without the leading 0)
+    std::vector<uint64_t> off{0};  // key offsets into blob, n + 1
     std::vector<uint64_t> addr, value8;
     std::vector<uint8_t> vlen;
     int rc = BSDB_OK;
+    void reserve(uint64_t records, uint64_t key_bytes) {
+        blob.reserve(key_bytes);
+        off.reserve(records + 1);
+        addr.reserve(records);
+        value8.reserve(records);
+        vlen.reserve(records);
+    }
     void add(uint64_t a, const uint8_t *key, uint32_t kl, const uint8_t *val, uint32_t vl) {
         blob.insert(blob.end(), key, key + kl);
-        len_end.push_back(blob.size());
+        off.push_back(blob.size());
         addr.push_back(a);
         uint64_t v = 0;
         const uint32_t h = vl < 8 ? vl : 8;
@@ -91,10 +98,10 @@ int map_file(const std::string &path, Mapped &m) {
     return BSDB_OK;
 }
 
-// SCK:55-70
-int scan_compact(const Mapped &m, uint64_t part, KvPart &out) {
+// SCK:55-70.  Records starting at or past `limit` are not read (a sample).
+int scan_compact(const Mapped &m, uint64_t part, KvPart &out, uint64_t limit = UINT64_MAX) {
     uint64_t pos = 0;
-    while (pos < m.size) {
+    while (pos < m.size && pos < limit) {
         const uint32_t kl = m.p[pos];
         if (kl == 0) break;
         if (pos + 3 > m.size) return BSDB_EFILE;
@@ -107,9 +114,9 @@ int scan_compact(const Mapped &m, uint64_t part, KvPart &out) {
 }
 
 // BKV:84-121
-int scan_blocked(const Mapped &m, uint64_t part, uint32_t block, KvPart &out) {
+int scan_blocked(const Mapped &m, uint64_t part, uint32_t block, KvPart &out, uint64_t limit = UINT64_MAX) {
     uint64_t position = 0;
-    while (position < m.size) {
+    while (position < m.size && position < limit) {
         const uint64_t end = std::min<uint64_t>(m.size, position + block);  // readBlockAt: up to one block
         uint64_t next = block;
         uint64_t o = position;
@@ -185,13 +192,11 @@ int bsdb_kv_scan(const char *kv_base, int partitions, int format, uint32_t block
         bool same = true;
         for (auto &p : parts) {
             const uint64_t base = r->blob.size();
-            uint64_t prev = 0;
-            for (uint64_t e : p.len_end) {
-                const uint64_t l = e - prev;
-                prev = e;
+            for (size_t i = 1; i < p.off.size(); ++i) {
+                const uint64_t l = p.off[i] - p.off[i - 1];
                 if (!fixed) fixed = (uint32_t)l;
                 same = same && l == fixed;
-                r->off.push_back(base + e);
+                r->off.push_back(base + p.off[i]);
             }
             r->blob.insert(r->blob.end(), p.blob.begin(), p.blob.end());
             r->addr.insert(r->addr.end(), p.addr.begin(), p.addr.end());
@@ -242,8 +247,9 @@ int bsdb_kv_records_free(bsdb_kv_records *r) {
 // threads finish (the files do not depend on it); then the bucket-range-pass
 // build writes index.db / index_a.db.  Host memory: the records' addresses
 // (+ 9 B per record in approximate mode) and the partitions in flight, not
-// every key.  Device capacity is reserved from the first partition's key
-// bytes per file byte, extrapolated over every file (growth covers the rest).
+// every key.  Device capacity (and each partition's host arrays) is reserved
+// from the records and key bytes per file byte of a 16 MiB sample of
+// partition 0, extrapolated over every file (growth covers the rest).
 int bsdb_kv_build_index(bsdb_ctx *c, const char *kv_base, int partitions, int format, uint32_t block_size,
                         int threads, uint32_t width, int approximate, const char *index_path, const char *index_a_path,
                         bsdb_mph **out) {
@@ -251,51 +257,68 @@ int bsdb_kv_build_index(bsdb_ctx *c, const char *kv_base, int partitions, int fo
         (format == 1 && (block_size == 0 || block_size % KV_PAGE)) || (approximate && !index_a_path))
         return BSDB_EINVAL;
     *out = nullptr;
-    auto scan_one = [&](int p, KvPart &part) {
-        Mapped m;
-        const std::string path = std::string(kv_base) + "." + std::to_string(p);  // PKV:79-81
-        int rc = map_file(path, m);
-        if (!rc) rc = format == 0 ? scan_compact(m, (uint64_t)p, part) : scan_blocked(m, (uint64_t)p, block_size, part);
-        return rc;
-    };
-    uint64_t file_bytes = 0, first_bytes = 0;
+    // BSDB_BUILDER_PROFILE=1: phase times on stderr
+    const bool prof = getenv("BSDB_BUILDER_PROFILE") != nullptr;
+    const auto t_start = std::chrono::steady_clock::now();
+    auto since = [&] { return std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count(); };
+    std::atomic<uint64_t> scan_ns{0}, add_ns{0};
+    uint64_t file_bytes = 0;
     for (int p = 0; p < partitions; ++p) {
         struct stat st;
         const std::string path = std::string(kv_base) + "." + std::to_string(p);
         if (stat(path.c_str(), &st) != 0) return BSDB_EFILE;
         file_bytes += (uint64_t)st.st_size;
-        if (p == 0) first_bytes = (uint64_t)st.st_size;
     }
-    KvPart first;
-    int rc = scan_one(0, first);
-    if (rc) return rc;
-    const double per_byte_keys = first_bytes ? (double)first.addr.size() / (double)first_bytes : 0.0;
-    const double per_byte_blob = first_bytes ? (double)first.blob.size() / (double)first_bytes : 0.0;
+    // records and key bytes per file byte, from the first 16 MiB of partition 0
+    double per_byte_keys = 0.0, per_byte_blob = 0.0;
+    {
+        Mapped m;
+        KvPart sample;
+        const uint64_t limit = 16ull << 20;
+        int rc = map_file(std::string(kv_base) + ".0", m);
+        if (!rc) rc = format == 0 ? scan_compact(m, 0, sample, limit) : scan_blocked(m, 0, block_size, sample, limit);
+        if (rc) return rc;
+        const uint64_t seen = std::min<uint64_t>(m.size, limit);
+        if (seen) {
+            per_byte_keys = (double)sample.addr.size() / (double)seen;
+            per_byte_blob = (double)sample.blob.size() / (double)seen;
+        }
+    }
     bsdb_builder *b = nullptr;
-    if ((rc = builder_open(c, 0, (uint64_t)(per_byte_keys * (double)file_bytes * 1.02) + 1024,
-                           (uint64_t)(per_byte_blob * (double)file_bytes * 1.02) + 65536, approximate, 0, 0, &b)))
-        return rc;
+    int rc = builder_open(c, 0, (uint64_t)(per_byte_keys * (double)file_bytes * 1.02) + 1024,
+                          (uint64_t)(per_byte_blob * (double)file_bytes * 1.02) + 65536, approximate, 0, 0, &b);
+    if (rc) return rc;
     std::unique_ptr<bsdb_builder, int (*)(bsdb_builder *)> guard(b, bsdb_builder_free);
     std::mutex add_mu;
-    auto add_part = [&](KvPart &part) {
-        const uint64_t k = part.addr.size();
-        std::vector<uint64_t> off(k + 1);
-        off[0] = 0;
-        std::copy(part.len_end.begin(), part.len_end.end(), off.begin() + 1);
-        std::lock_guard<std::mutex> g(add_mu);
-        return builder_add(b, k, part.addr.data(), part.value8.data(), part.vlen.data(),
-                           [&] { return builder_add_var_locked(b, part.blob.data(), off.data(), k); });
-    };
-    if ((rc = add_part(first))) return rc;
-    first = KvPart();
-    const int T = std::max(1, std::min(threads > 0 ? threads : (int)std::thread::hardware_concurrency(), partitions - 1));
-    std::atomic<int> next{1};
+    const int T = std::max(1, std::min(threads > 0 ? threads : (int)std::thread::hardware_concurrency(), partitions));
+    std::atomic<int> next{0};
     std::atomic<int> err{BSDB_OK};
     auto worker = [&] {
         for (int p; !err.load() && (p = next.fetch_add(1)) < partitions;) {
             KvPart part;
-            int r = scan_one(p, part);
-            if (!r) r = add_part(part);
+            const auto t0 = std::chrono::steady_clock::now();
+            Mapped m;
+            int r = map_file(std::string(kv_base) + "." + std::to_string(p), m);  // PKV:79-81
+            if (!r) {
+                try {
+                    part.reserve((uint64_t)(per_byte_keys * (double)m.size * 1.05) + 64,
+                                 (uint64_t)(per_byte_blob * (double)m.size * 1.05) + 4096);
+                    r = format == 0 ? scan_compact(m, (uint64_t)p, part) : scan_blocked(m, (uint64_t)p, block_size, part);
+                } catch (const std::bad_alloc &) {
+                    r = BSDB_ENOMEM;
+                }
+            }
+            scan_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
+            const uint64_t k = part.addr.size();
+            uint32_t uni = 0;
+            if (!r) r = var_batch_lengths(part.off.data(), k, &uni);
+            if (!r) {
+                std::lock_guard<std::mutex> g(add_mu);
+                const auto t1 = std::chrono::steady_clock::now();
+                r = builder_add(b, k, part.addr.data(), part.value8.data(), part.vlen.data(),
+                                [&] { return builder_add_var_locked(b, part.blob.data(), part.off.data(), k, uni); });
+                add_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t1).count();
+            }
             if (r) {
                 int expect = BSDB_OK;
                 err.compare_exchange_strong(expect, r);
@@ -307,7 +330,12 @@ int bsdb_kv_build_index(bsdb_ctx *c, const char *kv_base, int partitions, int fo
     worker();
     for (auto &t : th) t.join();
     if ((rc = err.load())) return rc;
-    return bsdb_builder_finish(b, width, 0, index_path, index_a_path, out, nullptr);
+    const double t_scanned = since();
+    rc = bsdb_builder_finish(b, width, 0, index_path, index_a_path, out, nullptr);
+    if (prof)
+        fprintf(stderr, "[bsdb kv] %llu records: scan+add %.3f s (thread scan %.3f s, adds %.3f s under the lock), finish %.3f s\n",
+                (unsigned long long)b->n, t_scanned, scan_ns.load() / 1e9, add_ns.load() / 1e9, since() - t_scanned);
+    return rc;
 }
 
 }  // extern "C"

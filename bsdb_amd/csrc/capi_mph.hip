@@ -396,10 +396,13 @@ int write_files(int device, FILE *const *files, const void *const *d_srcs, int n
             }
             if (st) (void)hipStreamDestroy(st);
         };
+        Populator pop;
+        pop.start(map, map_len);
         std::vector<std::thread> th;
         for (uint64_t t = 1; t < T; ++t) th.emplace_back(work, t);
         work(0);
         for (auto &x : th) x.join();
+        pop.finish();
         if (map && munmap(map, map_len) != 0 && !rc.load()) rc.store(BSDB_EFILE);
         if (rc.load()) return rc.load();
         if (fseeko(files[fi], base + (off_t)bytes, SEEK_SET) != 0) return BSDB_EFILE;  // the FILE's position after the data

@@ -56,6 +56,10 @@ int passes_build(bsdb_ctx *c, const GovSrc &src, uint64_t n, uint32_t width, uin
     // 1 G-key chunks and released before the passes are sized.
     GovSrc gsrc = src;
     std::unique_ptr<void, DevFree> counts_all;
+    // BSDB_BUILDER_PROFILE=1: per-pass times on stderr
+    const bool prof = getenv("BSDB_BUILDER_PROFILE") != nullptr;
+    const auto t_start = std::chrono::steady_clock::now();
+    auto since = [&] { return std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count(); };
     const bool fixed_ok = src.off || (!bad_key_len(src.key_len) && aligned16(src.keys));
     if (n >= (1ULL << 16) && fixed_ok) {
         void *q = nullptr;
@@ -136,8 +140,11 @@ int passes_build(bsdb_ctx *c, const GovSrc &src, uint64_t n, uint32_t width, uin
             };
         }  // (neither: the structure only)
         uint64_t nl = 0;
+        const double t_pass = since();
         int rc = gov_build_impl(c, gsrc, n, b_lo, b_hi, e_lo, width, d_E, d_values, d_sigbits, nullptr, ixo, s, false, &nl);
         if (rc) return finish(rc);
+        if (prof) fprintf(stderr, "[bsdb passes] pass %u: %llu keys, start %.3f s, built in %.3f s\n", p,
+                          (unsigned long long)nl, t_pass, since() - t_pass);
         if (sink.slices() && nl) {  // gov_build_impl returned after the device finished
             const uint64_t *src_slots = (const uint64_t *)slice[sl];
             const int dev = c->device;
@@ -157,7 +164,9 @@ int passes_build(bsdb_ctx *c, const GovSrc &src, uint64_t n, uint32_t width, uin
         }
         e_lo += nl;
     }
+    const double t_join = since();
     const int rc = finish(BSDB_OK);
+    if (prof) fprintf(stderr, "[bsdb passes] last slice out %.3f s after the last pass, total %.3f s\n", since() - t_join, since());
     if (rc) return rc;
     return e_lo == n ? BSDB_OK : BSDB_EIO;
 }

@@ -609,11 +609,7 @@ __device__ void wg_excl_scan3(uint32_t *a, uint32_t n, uint32_t *wsum) {
 // success with L.xval / L.vowner describing the solution.
 template <class Lds>
 __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t cnt, uint32_t nv, uint64_t seed_bits,
-                         uint64_t *scr, PhaseClock &pc, uint32_t fvs_max_flags) {
-    // bit 31 (BSDB_GOV_GJ_COLUMN=1, A/B only): the heavy system by the column
-    // Gauss-Jordan instead of panels (identical results)
-    const bool gj_column = (fvs_max_flags >> 31) != 0;
-    const uint32_t fvs_max = fvs_max_flags & 0x7FFFFFFFu;
+                         uint64_t *scr, PhaseClock &pc, uint32_t fvs_max) {
     const int tid = threadIdx.x;
     pc.start();
     pc.add(GP_N_SEEDS, 1);
@@ -1289,172 +1285,6 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
             __syncthreads();
             return ok;
         };
-        // The same Gauss-Jordan for n <= 384 rows by PANELS of 8 columns:
-        // TWO barriers per panel instead of one per column (the column loop
-        // above spends ~2 700 cycles a column waiting on LDS round trips and
-        // its barrier).  Per panel:
-        //  A. wave 0 holds every row's 8 panel bits (row l + 64 s in lane l,
-        //     slot s) in registers and eliminates the panel's columns in
-        //     order -- pivot = the lowest unused row with a nonzero there,
-        //     eliminated from every other row -- while tracking each row's
-        //     transform t_r: its panel-reduced form is its panel-start row +
-        //     sum_j t_r[j] * (panel-start row of pivot j).  It publishes the
-        //     t_r (8 GF(3) digits per row, two bit planes) and a copy of the
-        //     pivots' panel-start rows.
-        //  B. every row applies its t_r to its words from the panel on.
-        // Same pivot columns, and the reduced row echelon form is unique, so
-        // every output (pivot columns, free columns, colval, the rows the
-        // null-space reduction reads) equals the column loop's.
-        auto gauss_jordan_panel = [&](uint32_t n, auto &&X) -> bool {
-            constexpr uint32_t PW = 8, RS = 6;  // panel width; row slots per lane (n <= 384)
-            const uint32_t W = (n + 1 + 63) / 64;
-            int16_t *piv = L.a0;
-            uint8_t *used = L.b1;
-            uint8_t *T1 = L.b0, *T2 = L.b0 + n;  // (colval's bytes, written after the loop)
-            uint64_t *PB = reinterpret_cast<uint64_t *>((reinterpret_cast<uintptr_t>(L.b0 + 2 * n) + 7) & ~(uintptr_t)7);
-            uint32_t *pj_row = L.hbin;  // the panel's pivot rows (the column loop's bid words)
-            static_assert(Lds::NVMAX >= 2 * 384 + 7 + 8 * 7 * 2 * 8, "T1, T2 and PB fit colval's bytes");
-            for (uint32_t rr = tid; rr < n; rr += GS_THREADS) used[rr] = 0;
-            if (tid == 0) L.nfree = 0;
-            __syncthreads();
-            for (uint32_t c0 = 0; c0 < n; c0 += PW) {
-                const uint32_t kk = min(PW, n - c0), w0 = c0 >> 6, sh = c0 & 63;
-                const uint32_t kmask = (1u << kk) - 1;
-                if (tid < 64) {
-                    const uint32_t lane = tid;
-                    // packed per slot: bits 0-7 the panel's columns, bits 8-15 t_r
-                    uint32_t v1[RS], v2[RS];
-                    bool u[RS];
-#pragma unroll
-                    for (uint32_t s = 0; s < RS; ++s) {
-                        const uint32_t r = lane + 64 * s;
-                        v1[s] = v2[s] = 0;
-                        u[s] = true;
-                        if (r < n) {
-                            v1[s] = (uint32_t)(X(r, w0, 0) >> sh) & kmask;
-                            v2[s] = (uint32_t)(X(r, w0, 1) >> sh) & kmask;
-                            u[s] = used[r] != 0;
-                        }
-                    }
-                    uint32_t npiv = 0;
-                    for (uint32_t j = 0; j < kk; ++j) {
-                        const uint32_t jb = 1u << j;
-                        int P = -1;
-                        uint32_t sP = 0;
-                        uint64_t bal = 0;
-#pragma unroll
-                        for (uint32_t s = 0; s < RS; ++s) {
-                            const uint64_t b = __builtin_amdgcn_ballot_w64(!u[s] && ((v1[s] | v2[s]) & jb));
-                            if (P < 0 && b) {
-                                P = (int)(64 * s + (uint32_t)__builtin_ctzll(b));
-                                sP = s;
-                                bal = b;
-                            }
-                        }
-                        (void)bal;
-                        if (P < 0) {  // a free column: x = 0 (uniform)
-                            if (lane == 0) {
-                                piv[c0 + j] = -1;
-                                ++L.nfree;
-                            }
-                            continue;
-                        }
-                        const int lP = P & 63;
-                        uint32_t s1 = 0, s2 = 0;
-#pragma unroll
-                        for (uint32_t s = 0; s < RS; ++s)
-                            if (s == sP) {
-                                s1 = v1[s];
-                                s2 = v2[s];
-                            }
-                        // the pivot's current panel row, with its own panel-start
-                        // row at transform digit npiv (coefficient 1)
-                        const uint32_t p1 = (uint32_t)__builtin_amdgcn_readlane((int)s1, lP) | (1u << (8 + npiv));
-                        const uint32_t p2 = (uint32_t)__builtin_amdgcn_readlane((int)s2, lP);
-                        const bool two = (p2 & jb) != 0;
-#pragma unroll
-                        for (uint32_t s = 0; s < RS; ++s) {
-                            const bool is_p = s == sP && (int)lane == lP;
-                            if (is_p) u[s] = true;
-                            const uint32_t f1 = v1[s] & jb, f2 = v2[s] & jb;
-                            if (!is_p && (f1 || f2)) {
-                                const bool sw = (f1 != 0) != two;  // subtract cf * (normalised pivot row)
-                                const uint32_t y1 = sw ? p2 : p1, y2 = sw ? p1 : p2;
-                                const uint32_t a1 = v1[s], a2 = v2[s];
-                                v1[s] = (a1 & ~y1 & ~y2) | (~a1 & ~a2 & y1) | (a2 & y2);
-                                v2[s] = (a2 & ~y1 & ~y2) | (~a1 & ~a2 & y2) | (a1 & y1);
-                            }
-                        }
-                        if (lane == 0) {
-                            piv[c0 + j] = (int16_t)P;
-                            pj_row[npiv] = (uint32_t)P;
-                        }
-                        ++npiv;
-                    }
-#pragma unroll
-                    for (uint32_t s = 0; s < RS; ++s) {
-                        const uint32_t r = lane + 64 * s;
-                        if (r < n) {
-                            T1[r] = (uint8_t)(v1[s] >> 8);
-                            T2[r] = (uint8_t)(v2[s] >> 8);
-                            used[r] = u[s] ? 1 : 0;
-                        }
-                    }
-                    __builtin_amdgcn_wave_barrier();
-                    // the pivots' panel-start rows, words w0..W-1
-                    for (uint32_t i = lane; i < npiv * (W - w0) * 2; i += 64) {
-                        const uint32_t jj = i / ((W - w0) * 2), rem = i % ((W - w0) * 2);
-                        PB[i] = X(pj_row[jj], w0 + rem / 2, rem & 1);
-                    }
-                    if (lane == 0) L.npos = npiv;
-                }
-                __syncthreads();
-                const uint32_t npiv = L.npos, WW = W - w0;
-                for (uint32_t rr = tid; rr < n; rr += GS_THREADS) {
-                    const uint32_t t1 = T1[rr], t2 = T2[rr];
-                    if (!(t1 | t2)) continue;
-                    for (uint32_t w = 0; w < WW; ++w) {
-                        uint64_t a1 = X(rr, w0 + w, 0), a2 = X(rr, w0 + w, 1);
-                        for (uint32_t jj = 0; jj < npiv; ++jj) {
-                            const uint32_t c = ((t1 >> jj) & 1) ? 1 : ((t2 >> jj) & 1) ? 2 : 0;
-                            if (!c) continue;
-                            uint64_t y1 = PB[(jj * WW + w) * 2], y2 = PB[(jj * WW + w) * 2 + 1];
-                            if (c == 2) {
-                                const uint64_t t = y1;
-                                y1 = y2;
-                                y2 = t;
-                            }
-                            const uint64_t b1 = (a1 & ~y1 & ~y2) | (~a1 & ~a2 & y1) | (a2 & y2);
-                            const uint64_t b2 = (a2 & ~y1 & ~y2) | (~a1 & ~a2 & y2) | (a1 & y1);
-                            a1 = b1;
-                            a2 = b2;
-                        }
-                        X(rr, w0 + w, 0) = a1;
-                        X(rr, w0 + w, 1) = a2;
-                    }
-                }
-                __syncthreads();
-            }
-            const uint64_t rbit = 1ULL << (n & 63);
-            for (uint32_t cc = tid; cc < n; cc += GS_THREADS) {
-                const int pr = piv[cc];
-                if (pr < 0) {
-                    colval[cc] = 0;
-                    continue;
-                }
-                const uint64_t cbit = 1ULL << (cc & 63);
-                const uint32_t rhs = (X(pr, n >> 6, 0) & rbit) ? 1 : (X(pr, n >> 6, 1) & rbit) ? 2 : 0;
-                const uint32_t cf = (X(pr, cc >> 6, 1) & cbit) ? 2 : 1;
-                colval[cc] = (uint8_t)(cf * rhs % 3);
-            }
-            bool bad = false;
-            for (uint32_t rr = tid; rr < n; rr += GS_THREADS)
-                if (!used[rr] && ((X(rr, n >> 6, 0) | X(rr, n >> 6, 1)) & rbit)) bad = true;
-            const bool ok = !__syncthreads_or(bad);
-            if (!ok && tid == 0) L.flag = 0;
-            __syncthreads();
-            return ok;
-        };
         // Block equation of member i: cf*x_hinge + sum of its other vertices
         // = h (mod 3), h = the hinge's position in the edge, cf = its count.
         // Large blocks: heavy variables chosen so that the others follow in
@@ -1864,9 +1694,7 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
                 }
                 __syncthreads();
                 // (rows in X: words < 12 CMAX, below the forms)
-                static_assert(FVS_NH_MAX <= 384, "the panel Gauss-Jordan's row slots");
-                const bool hok = gj_column ? (hs_lds ? gauss_jordan(nH, HSL) : gauss_jordan(nH, X))
-                                           : (hs_lds ? gauss_jordan_panel(nH, HSL) : gauss_jordan_panel(nH, X));
+                const bool hok = hs_lds ? gauss_jordan(nH, HSL) : gauss_jordan(nH, X);
                 pc.lap(GP_FVS_GJ);
                 if (!hok) {
                     pc.add(GP_N_FAIL_INCONS, 1);

@@ -1,0 +1,34 @@
+#!/usr/bin/env python3
+"""The bench's end-to-end legs alone (BSDB_BUILDER_PROFILE=1 prints their
+phases): C4 from host memory through the streaming builder into index.db,
+and C2 from kv.db files.  python tools/e2e_legs.py [--c4] [--kv]"""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--c4", action="store_true")
+    ap.add_argument("--kv", action="store_true")
+    ap.add_argument("--n", type=int, default=13_193_787_549)
+    args = ap.parse_args()
+    import bench
+    from bsdb_amd import Context
+    ctx = Context(0)
+    out = {}
+    if args.kv:
+        out["e2e_c2_kv_to_disk"] = bench.e2e_c2_kv_to_disk(ctx, 100_000_000, 4)
+        print(json.dumps(out["e2e_c2_kv_to_disk"]), flush=True)
+    if args.c4:
+        out["e2e_c4_host_passes"] = bench.e2e_c4_host_passes(ctx, args.n, 4)
+        print(json.dumps(out["e2e_c4_host_passes"]), flush=True)
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()
