@@ -536,6 +536,7 @@ struct SolveLdsT {
     static constexpr size_t HS_WORDS = (4 * (size_t)NVMAX + 4 * CMAX + 6 * CMAX + 2 * CMAX + 2 * CMAX) / 8;
     static constexpr size_t PEND_ROOM = sizeof(uint64_t) * 2 * WMAX + 2 * CMAX + NVMAX + CMAX;
     static_assert(PEND_ROOM >= 4 * (size_t)CMAX, "pending counts fit the pivot-row region");
+    static_assert(NVMAX >= CMAX + 1 + 64, "the FVS pick's wave counts fit past the reverse CSR offsets");
 };
 using SolveLds = SolveLdsT<GS_CMAX>;
 using SolveBig = SolveLdsT<GB_CMAX>;
@@ -1304,7 +1305,7 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
         auto V = [&](uint32_t i, uint32_t w, uint32_t q) -> uint64_t & { return scr[V0 + (size_t)(2 * w + q) * Lds::CMAX + i]; };
         bool solved = false;
         if (sz >= FVS_MIN) {
-            uint32_t *st = L.xe, *indeg = L.claim;  // 0 open, 1 formed, 2 heavy (dead arrays)
+            uint32_t *st = L.xe, *indeg = L.claim;  // 0 open, 1 formed, 2 heavy, after the selection (dead arrays)
             int16_t *rnd = L.a1, *hid = L.a2;
             auto in_dep = [&](uint32_t k, int i) -> int {  // member index of the owner of vertex i, or -1
                 const uint32_t v = L.e[3 * k + i];
@@ -1312,12 +1313,14 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
                 const int o = L.vowner[v];
                 return (o >= 0 && L.col_of[o] >= 0) ? L.col_of[o] : -1;
             };
+            // lvl (st's words until the selection ends): 1 + the highest
+            // level of the member's dependencies placed so far (heavy: 0)
+            uint32_t *lvl = st;
             // the block's dependency graph, once: idep[3i+t] = member index
             // of the owner of member i's vertex t, or -1 (L.dep is dead here)
             int16_t *idep = L.dep;
             for (uint32_t i = tid; i < sz; i += GS_THREADS) {
-                st[i] = 0;
-                rnd[i] = -1;
+                lvl[i] = 1;
                 const uint32_t k = (uint32_t)L.members[beg + i];
                 for (int t = 0; t < 3; ++t) idep[3 * i + t] = (int16_t)in_dep(k, t);
             }
@@ -1329,6 +1332,12 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
             // so the heavy set is that of level-synchronous rounds.  A formed
             // member's level is 1 + its dependencies' highest (heavy: 0):
             // the forms are evaluated level by level.
+            // pend[i]: i's dependency slots not yet placed, + 0x100 once i is
+            // heavy (so it never reads 1 -> 0); open = 1..0xFF, formed = 0.
+            // A placed member raises its dependents' lvl before it releases
+            // their pending slots (one wave, LDS operations in order), so a
+            // member's lvl is final when its last slot is released: the
+            // closure costs one returned LDS atomic per dependency.
             uint32_t *roff = L.deg;                                        // reverse CSR offsets
             // dependents (3 * CMAX int16) in the workgroup's scratch past the
             // forms (words [28 CMAX, 29.5 CMAX)); pending counts in LDS
@@ -1336,7 +1345,10 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
             uint32_t *pend = L.pend();
             int16_t *queue = L.a3;
             for (uint32_t i = tid; i <= sz; i += GS_THREADS) roff[i] = 0;
-            if (tid == 0) L.qtail = 0;
+            if (tid == 0) {
+                L.qtail = 0;
+                L.rounds = 0;
+            }
             __syncthreads();
             for (uint32_t i = tid; i < sz; i += GS_THREADS) {
                 uint32_t np = 0;
@@ -1361,24 +1373,22 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
             __syncthreads();
             for (uint32_t d = tid; d < sz; d += GS_THREADS) {
                 indeg[d] = roff[d + 1] - roff[d];  // slots of open members on d (all open)
-                if (pend[d] == 0) {
-                    st[d] = 1;
-                    rnd[d] = 1;
-                    queue[atomicAdd(&L.qtail, 1u)] = (int16_t)d;
-                }
+                if (pend[d] == 0) queue[atomicAdd(&L.qtail, 1u)] = (int16_t)d;
             }
             __syncthreads();
             pc.lap(GP_SEL_PREP_CYCLES);
-            if (tid < 64) {
-                const uint32_t lane = tid;
-                uint32_t qh = 0, qt = L.qtail, nh = 0, maxlev = 1, nbatch = 0, npick = 0;
-                uint64_t pick_cyc = 0;
-                bool fb = false;
-                for (;;) {
+            const uint32_t lane = tid & 63, wv = tid >> 6;
+            uint32_t qh = 0, nh = 0, nbatch = 0, npick = 0;  // (qh: wave 0's)
+            uint64_t pick_cyc = 0;
+            bool fb = false;
+            for (;;) {
+                // the ready closure (wave 0)
+                if (tid < 64) {
+                    uint32_t qt = L.qtail;
                     while (qh < qt) {
                         ++nbatch;
                         const uint32_t nb = min(64u, qt - qh);
-                        uint32_t x0 = 0, x1 = 0;
+                        uint32_t x0 = 0, x1 = 0, myl = 0;
                         if (lane < nb) {
                             const uint32_t p = (uint32_t)queue[qh + lane];
                             for (int t = 0; t < 3; ++t) {
@@ -1387,6 +1397,9 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
                             }
                             x0 = roff[p];
                             x1 = roff[p + 1];
+                            // (a heavy member's lvl may have been raised
+                            // while it waited in the queue: its level is 0)
+                            myl = pend[p] >= 0x100u ? 1u : lvl[p] + 1;
                         }
                         // the batch's dependents, one per lane per step; the
                         // members they make ready are appended in lane order
@@ -1399,17 +1412,8 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
                             uint32_t i = 0;
                             if (act) {
                                 i = (uint32_t)rev[x];
-                                if (atomicSub(&pend[i], 1u) == 1u && st[i] == 0) {  // last dependency placed (not heavy)
-                                    int lev = 0;
-                                    for (int t = 0; t < 3; ++t) {
-                                        const int d = idep[3 * i + t];
-                                        if (d >= 0) lev = max(lev, (int)rnd[d]);
-                                    }
-                                    rnd[i] = (int16_t)(lev + 1);
-                                    st[i] = 1;
-                                    maxlev = max(maxlev, (uint32_t)lev + 1);
-                                    ready = true;
-                                }
+                                atomicMax(&lvl[i], myl);
+                                ready = atomicSub(&pend[i], 1u) == 1u;  // its last slot
                             }
                             const uint64_t rm = __builtin_amdgcn_ballot_w64(ready);
                             if (ready)
@@ -1420,134 +1424,156 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
                         __builtin_amdgcn_wave_barrier();
                     }
                     if (lane == 0) L.qtail = qt;
-                    __builtin_amdgcn_wave_barrier();
-                    if (qt >= sz) break;  // every member placed (each enters the queue once)
-                    // a pick adds up to 2 heavy hinges: the heavy set stays
-                    // <= fvs_max, so forms and heavy rows (constant column
-                    // at nH) fit FW words
-                    if (nh + 2 > fvs_max) {
-                        fb = true;
-                        break;
-                    }
-                    // The next heavy hinges: the `want` open members of the
-                    // largest key (in-degree, then lowest index) -- the set
-                    // GOV_PICK_REPS rounds of "the best two" (the loop
-                    // below) pick, as nothing is placed between those rounds:
-                    // any feedback vertex set gives the same unique solution
-                    // and is singular exactly when the block is.  One sweep
-                    // bins the open members by in-degree (64 bins), a second
-                    // takes every member above the threshold bin and the
-                    // lowest-index ones of that bin.
-                    const uint64_t tpk = pc.acc ? clock64() : 0;
-                    ++npick;
-                    const uint32_t want = 2 * min((uint32_t)GOV_PICK_REPS, (fvs_max - nh) / 2);
-                    uint32_t *hb = L.hbin;
-                    hb[lane] = 0;
-                    __builtin_amdgcn_wave_barrier();
-                    for (uint32_t i0 = 0; i0 < sz; i0 += 64) {
-                        const uint32_t i = i0 + lane;
-                        if (i < sz && st[i] == 0) atomicAdd(&hb[min(indeg[i], 63u)], 1u);
-                    }
-                    __builtin_amdgcn_wave_barrier();
-                    uint32_t suf = hb[lane];  // -> open members of in-degree >= lane
+                }
+                __syncthreads();
+                const uint32_t qt = L.qtail;
+                if (qt >= sz) break;  // every member placed (each enters the queue once)
+                // a pick adds up to 2 heavy hinges: the heavy set stays
+                // <= fvs_max, so forms and heavy rows (constant column at nH)
+                // fit FW words
+                if (nh + 2 > fvs_max) {
+                    fb = true;
+                    break;
+                }
+                // The next heavy hinges: the `want` open members of the
+                // largest key (in-degree, then lowest index) -- the set
+                // GOV_PICK_REPS rounds of "the best two" (below) pick, as
+                // nothing is placed between those rounds: any feedback vertex
+                // set gives the same unique solution and is singular exactly
+                // when the block is.  The workgroup bins the open members by
+                // in-degree (64 bins), then takes every member above the
+                // threshold bin and the lowest-index ones of that bin.
+                const uint64_t tpk = pc.acc ? clock64() : 0;
+                ++npick;
+                const uint32_t want = 2 * min((uint32_t)GOV_PICK_REPS, (fvs_max - nh) / 2);
+                auto is_open = [&](uint32_t pv) { return pv != 0u && pv < 0x100u; };
+                auto make_heavy = [&](uint32_t i, uint32_t j, uint32_t slot) {
+                    pend[i] += 0x100u;
+                    lvl[i] = 0;
+                    hid[i] = (int16_t)j;
+                    queue[slot] = (int16_t)i;
+                };
+                uint32_t *hb = L.hbin;
+                if (tid < 64) hb[tid] = 0;
+                __syncthreads();
+                for (uint32_t i = tid; i < sz; i += GS_THREADS)
+                    if (is_open(pend[i])) atomicAdd(&hb[min(indeg[i], 63u)], 1u);
+                __syncthreads();
+                uint32_t suf = hb[lane];  // -> open members of in-degree >= lane (every wave alike)
 #pragma unroll
-                    for (int d = 1; d < 64; d <<= 1) {
-                        const uint32_t y = (uint32_t)__shfl_down((int)suf, d, 64);
-                        if (lane + d < 64) suf += y;
-                    }
-                    const uint64_t okm = __builtin_amdgcn_ballot_w64(suf >= want);
-                    const uint32_t T = okm ? 63u - (uint32_t)__builtin_clzll(okm) : 0u;
-                    const uint32_t above = T < 63 ? (uint32_t)__builtin_amdgcn_readlane((int)suf, (int)T + 1) : 0u;
-                    const uint32_t in_t = (uint32_t)__builtin_amdgcn_readlane((int)suf, (int)T) - above;
-                    const uint32_t take_t = okm ? want - above : in_t;  // (fewer open members than want: all)
-                    if (T < 63) {
-                        uint32_t run = 0, got = 0;
-                        for (uint32_t i0 = 0; i0 < sz; i0 += 64) {
-                            const uint32_t i = i0 + lane;
-                            const bool open = i < sz && st[i] == 0;
-                            const uint32_t dvc = open ? min(indeg[i], 63u) : 0u;
-                            const bool eq = open && dvc == T;
-                            const uint64_t em = __builtin_amdgcn_ballot_w64(eq);
-                            const uint32_t r = run + __builtin_amdgcn_mbcnt_hi((uint32_t)(em >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)em, 0u));
-                            const bool sel = (open && dvc > T) || (eq && r < take_t);
-                            run += (uint32_t)__builtin_popcountll(em);
-                            const uint64_t sm = __builtin_amdgcn_ballot_w64(sel);
-                            if (sel) {
-                                const uint32_t pos = got + __builtin_amdgcn_mbcnt_hi((uint32_t)(sm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)sm, 0u));
-                                st[i] = 2;
-                                hid[i] = (int16_t)(nh + pos);
-                                rnd[i] = 0;
-                                queue[qt + pos] = (int16_t)i;
-                            }
-                            got += (uint32_t)__builtin_popcountll(sm);
+                for (int dd = 1; dd < 64; dd <<= 1) {
+                    const uint32_t y = (uint32_t)__shfl_down((int)suf, dd, 64);
+                    if (lane + dd < 64) suf += y;
+                }
+                const uint64_t okm = __builtin_amdgcn_ballot_w64(suf >= want);
+                const uint32_t T = okm ? 63u - (uint32_t)__builtin_clzll(okm) : 0u;
+                const uint32_t above = T < 63 ? (uint32_t)__builtin_amdgcn_readlane((int)suf, (int)T + 1) : 0u;
+                const uint32_t in_t = (uint32_t)__builtin_amdgcn_readlane((int)suf, (int)T) - above;
+                const uint32_t take_t = okm ? want - above : in_t;  // (fewer open members than want: all)
+                if (T < 63) {
+                    // in index order: per chunk of GS_THREADS members, each
+                    // wave's counts of threshold-bin and above-threshold open
+                    // members (double-buffered by chunk), one barrier a chunk
+                    uint32_t *wc = L.deg + Lds::CMAX + 1;  // (past roff)
+                    uint32_t run_eq = 0, got = 0, par = 0;
+                    for (uint32_t k0 = 0; k0 < sz; k0 += GS_THREADS, par ^= 1u) {
+                        const uint32_t i = k0 + tid;
+                        const bool open = i < sz && is_open(pend[i]);
+                        const uint32_t dvc = open ? min(indeg[i], 63u) : 0u;
+                        const bool eq = open && dvc == T, gt = open && dvc > T;
+                        const uint64_t em = __builtin_amdgcn_ballot_w64(eq), gm = __builtin_amdgcn_ballot_w64(gt);
+                        if (lane == 0) {
+                            wc[32 * par + wv] = (uint32_t)__builtin_popcountll(em);
+                            wc[32 * par + 16 + wv] = (uint32_t)__builtin_popcountll(gm);
                         }
-                        nh += got;
-                        qt += got;
-                        if (lane == 0) L.qtail = qt;
-                        __builtin_amdgcn_wave_barrier();
-                        if (pc.acc) pick_cyc += clock64() - tpk;
-                        continue;
+                        __syncthreads();
+                        uint32_t eb = run_eq, sb = got, my_eb = 0, my_sb = 0;
+                        for (uint32_t w2 = 0; w2 < GS_THREADS / 64; ++w2) {
+                            if (w2 == wv) {
+                                my_eb = eb;
+                                my_sb = sb;
+                            }
+                            const uint32_t e_w = wc[32 * par + w2], g_w = wc[32 * par + 16 + w2];
+                            sb += g_w + min(e_w, take_t > eb ? take_t - eb : 0u);
+                            eb += e_w;
+                        }
+                        const uint32_t rk = my_eb + __builtin_amdgcn_mbcnt_hi((uint32_t)(em >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)em, 0u));
+                        const bool sel = gt || (eq && rk < take_t);
+                        const uint64_t sm = __builtin_amdgcn_ballot_w64(sel);
+                        if (sel) {
+                            const uint32_t pos = my_sb + __builtin_amdgcn_mbcnt_hi((uint32_t)(sm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)sm, 0u));
+                            make_heavy(i, nh + pos, qt + pos);
+                        }
+                        run_eq = eb;
+                        got = sb;
                     }
+                    nh += got;
+                    if (tid == 0) L.qtail = qt + got;
+                } else if (tid < 64) {
                     // (64+ open members of in-degree >= 63 reach the
-                    // threshold: the exact rounds, loads issued 8 at a time)
-                    for (int rep = 0; rep < GOV_PICK_REPS && nh + 2 <= fvs_max; ++rep) {
+                    // threshold: the exact rounds on wave 0, loads issued 8
+                    // at a time)
+                    uint32_t nh0 = nh, q = qt;
+                    for (int rep = 0; rep < GOV_PICK_REPS && nh0 + 2 <= fvs_max; ++rep) {
                         uint32_t key = 0, key2 = 0;
                         for (uint32_t q0 = 0; q0 * 64 < sz; q0 += 8) {
                             uint32_t sv[8], dv[8];
 #pragma unroll
-                            for (uint32_t q = 0; q < 8; ++q) {
-                                const uint32_t i = lane + 64 * (q0 + q);
-                                sv[q] = i < sz ? st[i] : 1u;
-                                dv[q] = i < sz ? indeg[i] : 0u;
+                            for (uint32_t u = 0; u < 8; ++u) {
+                                const uint32_t i = lane + 64 * (q0 + u);
+                                sv[u] = i < sz ? pend[i] : 0u;
+                                dv[u] = i < sz ? indeg[i] : 0u;
                             }
 #pragma unroll
-                            for (uint32_t q = 0; q < 8; ++q)
-                                if (sv[q] == 0) {
-                                    const uint32_t k = (dv[q] << 16) | (0xFFFFu - (lane + 64 * (q0 + q)));
+                            for (uint32_t u = 0; u < 8; ++u)
+                                if (is_open(sv[u])) {
+                                    const uint32_t k = (dv[u] << 16) | (0xFFFFu - (lane + 64 * (q0 + u)));
                                     key2 = max(key2, min(key, k));
                                     key = max(key, k);
                                 }
                         }
 #pragma unroll
-                        for (int d = 32; d >= 1; d >>= 1) {
-                            const uint32_t o1 = (uint32_t)__shfl_xor((int)key, d, 64), o2 = (uint32_t)__shfl_xor((int)key2, d, 64);
+                        for (int dd = 32; dd >= 1; dd >>= 1) {
+                            const uint32_t o1 = (uint32_t)__shfl_xor((int)key, dd, 64), o2 = (uint32_t)__shfl_xor((int)key2, dd, 64);
                             key2 = max(min(key, o1), max(key2, o2));
                             key = max(key, o1);
                         }
                         if (key == 0) break;  // (no open member left; wave-uniform)
                         if (lane == 0) {
-                            const uint32_t hsel = 0xFFFFu - (key & 0xFFFFu);
-                            st[hsel] = 2;
-                            hid[hsel] = (int16_t)nh;
-                            rnd[hsel] = 0;
-                            queue[qt] = (int16_t)hsel;
-                            uint32_t nt = qt + 1;
-                            if (key2) {
-                                const uint32_t h2 = 0xFFFFu - (key2 & 0xFFFFu);
-                                st[h2] = 2;
-                                hid[h2] = (int16_t)(nh + 1);
-                                rnd[h2] = 0;
-                                queue[nt++] = (int16_t)h2;
-                            }
-                            L.qtail = nt;
+                            make_heavy(0xFFFFu - (key & 0xFFFFu), nh0, q);
+                            if (key2) make_heavy(0xFFFFu - (key2 & 0xFFFFu), nh0 + 1, q + 1);
                         }
-                        nh += key2 ? 2 : 1;
+                        nh0 += key2 ? 2 : 1;
+                        q += key2 ? 2 : 1;
                         __builtin_amdgcn_wave_barrier();
-                        qt = L.qtail;
                     }
-                    __builtin_amdgcn_wave_barrier();
-                    qt = L.qtail;
+                    if (lane == 0) {
+                        L.qtail = q;
+                        L.nleft = nh0;
+                    }
                 }
+                __syncthreads();
+                if (T >= 63) nh = L.nleft;
+                if (pc.acc) pick_cyc += clock64() - tpk;
+            }
+            // st and the levels; the highest level
+            uint32_t ml = 1;
+            for (uint32_t i = tid; i < sz; i += GS_THREADS) {
+                const uint32_t pv = pend[i], lv = lvl[i];
+                const uint32_t s = pv == 0u ? 1u : pv >= 0x100u ? 2u : 0u;
+                st[i] = s;  // (lvl's word)
+                rnd[i] = (int16_t)(s == 1u ? lv : s == 2u ? 0u : 0xFFFFu);
+                if (s == 1u) ml = max(ml, lv);
+            }
 #pragma unroll
-                for (int d = 32; d >= 1; d >>= 1) maxlev = max(maxlev, (uint32_t)__shfl_xor((int)maxlev, d, 64));
-                if (lane == 0) {
-                    L.nleft = nh;
-                    L.rounds = maxlev + 1;
-                    L.chg = fb ? 1u : 0u;
-                    pc.add(GP_N_SEL_BATCHES, nbatch);
-                    pc.add(GP_N_SEL_PICKS, npick);
-                    pc.add(GP_SEL_PICK_CYCLES, pick_cyc);
-                }
+            for (int dd = 32; dd >= 1; dd >>= 1) ml = max(ml, (uint32_t)__shfl_xor((int)ml, dd, 64));
+            if (lane == 0) atomicMax(&L.rounds, ml + 1);
+            if (tid == 0) {
+                L.nleft = nh;
+                L.chg = fb ? 1u : 0u;
+                pc.add(GP_N_SEL_BATCHES, nbatch);
+                pc.add(GP_N_SEL_PICKS, npick);
+                pc.add(GP_SEL_PICK_CYCLES, pick_cyc);
             }
             __syncthreads();
             const uint32_t nH = L.nleft, r = L.rounds;
