@@ -1140,7 +1140,8 @@ static void print_gov_profile(const std::vector<uint64_t> &h, uint32_t solve_gri
                                "n_small_scc_fallbacks", "fvs_select", "fvs_forms", "fvs_gauss_jordan",
                                "n_fail_degenerate", "n_fail_orient", "n_fail_inconsistent", "failed_attempt_cycles",
                                "bfs_flip", "n_bfs_iters", "n_flip_steps", "n_sel_batches", "n_sel_picks",
-                               "sel_pick_cycles", "sel_prep_cycles", "n_singular_solved", "n_null_vectors", "n_speculative_lost"};
+                               "sel_pick_cycles", "sel_prep_cycles", "n_singular_solved", "n_null_vectors", "n_speculative_lost",
+                               "n_fvs_blocks", "n_form_levels", "n_heavy"};
     std::vector<double> tot(GP_N, 0.0);
     for (uint32_t w = 0; w < solve_grid; ++w)
         for (int k = 0; k < GP_N; ++k) {
@@ -1375,15 +1376,20 @@ static int gov_build_impl(bsdb_ctx *c, const GovSrc &src, uint64_t n_global, uin
                                                                         (uint8_t *)c->g_slabs, big_slab_bytes());
         HIP_OK(hipEventRecord(c->big_ev[1], c->big_stream));
     }
-    if (one_per_cu) HIP_OK(hipFuncSetAttribute((const void *)k_gov_solve, hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024));
-    k_gov_solve<<<solve_grid, GS_THREADS, one_per_cu ? 64 * 1024 : 0, s>>>(sa);  // A8
+    // (the phase counters are compiled only into k_gov_solve<true>)
+    const void *solve_fn = gprof ? (const void *)k_gov_solve<true> : (const void *)k_gov_solve<false>;
+    if (one_per_cu) HIP_OK(hipFuncSetAttribute(solve_fn, hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024));
+    if (gprof)
+        k_gov_solve<true><<<solve_grid, GS_THREADS, one_per_cu ? 64 * 1024 : 0, s>>>(sa);  // A8
+    else
+        k_gov_solve<false><<<solve_grid, GS_THREADS, one_per_cu ? 64 * 1024 : 0, s>>>(sa);
     if (nbig) HIP_OK(hipStreamWaitEvent(s, c->big_ev[1], 0));
     if (gprof) {
         std::vector<uint64_t> h((size_t)solve_grid * GP_N);
         HIP_OK(hipMemcpyAsync(h.data(), d_prof, h.size() * 8, hipMemcpyDeviceToHost, s));
         HIP_OK(hipStreamSynchronize(s));
         int per_cu = 0;
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_gov_solve, GS_THREADS, 0);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_gov_solve<true>, GS_THREADS, 0);
         fprintf(stderr, "[gov-profile] solver workgroups per CU: %d (LDS %zu B each)\n", per_cu, sizeof(SolveLds));
         print_gov_profile(h, solve_grid, m);
     }

@@ -497,7 +497,7 @@ enum GovProf { GP_EDGES, GP_PEEL, GP_GREEDY, GP_BFS, GP_TARJAN, GP_SINGLE, GP_DE
                GP_N_SCC_SWEEPS, GP_N_SMALL_S, GP_FVS_SEL, GP_FVS_FORMS, GP_FVS_GJ,
                GP_N_FAIL_DEGEN, GP_N_FAIL_ORIENT, GP_N_FAIL_INCONS, GP_FAILED_CYCLES, GP_BFS_FLIP, GP_N_BFS_ITERS,
                GP_N_FLIP_STEPS, GP_N_SEL_BATCHES, GP_N_SEL_PICKS, GP_SEL_PICK_CYCLES, GP_SEL_PREP_CYCLES,
-               GP_N_SING_SOLVED, GP_N_NULL_VECS, GP_N_SPEC_LOST, GP_N };
+               GP_N_SING_SOLVED, GP_N_NULL_VECS, GP_N_SPEC_LOST, GP_N_FVS_BLOCKS, GP_N_FORM_LEVELS, GP_N_HEAVY, GP_N };
 
 // Solver state for buckets of up to CMAX_ keys: LDS for GS_CMAX, a global
 // slab per workgroup for GB_CMAX (same code; indices fit int16 either way).
@@ -558,19 +558,23 @@ __device__ __forceinline__ void gf3_add(uint64_t &x1, uint64_t &x2, uint64_t y1,
     x2 = (a2 & ~y1 & ~y2) | (~a1 & ~a2 & y2) | (a1 & y1);
 }
 
+// Phase counters; P = false (production) compiles them away, so the
+// profiling pointer and clock hold no registers in the solver.
+template <bool P>
 struct PhaseClock {
     uint64_t *acc;  // nullptr = off
     uint64_t t;
-    __device__ void start() { if (acc) t = clock64(); }
+    __device__ bool on() const { return P && acc; }
+    __device__ void start() { if (on()) t = clock64(); }
     __device__ void lap(int slot) {
-        if (acc) {
+        if (on()) {
             const uint64_t now = clock64();
             if (threadIdx.x == 0) acc[slot] += now - t;
             t = now;
         }
     }
-    __device__ void add(int slot, uint64_t v) { if (acc && threadIdx.x == 0) acc[slot] += v; }
-    __device__ void max(int slot, uint64_t v) { if (acc && threadIdx.x == 0 && v > acc[slot]) acc[slot] = v; }
+    __device__ void add(int slot, uint64_t v) { if (on() && threadIdx.x == 0) acc[slot] += v; }
+    __device__ void max(int slot, uint64_t v) { if (on() && threadIdx.x == 0 && v > acc[slot]) acc[slot] = v; }
 };
 
 // In-place exclusive scan of a[0..n) by the whole workgroup, 3 * GS_THREADS
@@ -608,9 +612,9 @@ __device__ void wg_excl_scan3(uint32_t *a, uint32_t n, uint32_t *wsum) {
 
 // Tries local seed j on bucket (sig, cnt, nv).  Returns (WG-uniform) true on
 // success with L.xval / L.vowner describing the solution.
-template <class Lds>
+template <class Lds, class PC>
 __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t cnt, uint32_t nv, uint64_t seed_bits,
-                         uint64_t *scr, PhaseClock &pc, uint32_t fvs_max) {
+                         uint64_t *scr, PC &pc, uint32_t fvs_max) {
     const int tid = threadIdx.x;
     pc.start();
     pc.add(GP_N_SEEDS, 1);
@@ -813,7 +817,7 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
         const uint32_t lane = tid;
         uint32_t epoch = 0, ok = 1, nbfs = 0, npops = 0, ncore = 0, niters = 0, nflip = 0;
         uint64_t flip_cyc = 0;
-        if (pc.acc)
+        if (pc.on())
             for (uint32_t k = 0; k < cnt; ++k) ncore += L.round_of[k] < 0;
         // unmatched core edges, 64 at a time by ballot (a BFS only matches its
         // own root: the path it flips runs through matched edges, so the
@@ -879,7 +883,7 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
                 ok = 0;
                 break;
             }
-            const uint64_t tf = pc.acc ? clock64() : 0;
+            const uint64_t tf = pc.on() ? clock64() : 0;
             if (lane == 0) {
                 int k = found_e, v = found_v;
                 for (;;) {
@@ -892,7 +896,7 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
                     k = bfs_prev[k];
                 }
             }
-            if (pc.acc) flip_cyc += clock64() - tf;
+            if (pc.on()) flip_cyc += clock64() - tf;
             __builtin_amdgcn_wave_barrier();
         }
         if (lane == 0) {
@@ -1302,7 +1306,6 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
         constexpr uint32_t FVS_MIN = 96, FW = 6;  // <= 6 words per form / heavy row
         static_assert(FVS_NH_MAX + 1 <= 64 * FW, "heavy columns + the constant column must fit FW words");
         constexpr size_t V0 = (size_t)16 * Lds::CMAX;          // affine forms, past that region
-        auto V = [&](uint32_t i, uint32_t w, uint32_t q) -> uint64_t & { return scr[V0 + (size_t)(2 * w + q) * Lds::CMAX + i]; };
         bool solved = false;
         if (sz >= FVS_MIN) {
             uint32_t *st = L.xe, *indeg = L.claim;  // 0 open, 1 formed, 2 heavy, after the selection (dead arrays)
@@ -1404,7 +1407,9 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
                         // the batch's dependents, one per lane per step; the
                         // members they make ready are appended in lane order
                         // by ballot (the ready closure, the levels and so the
-                        // heavy set do not depend on the queue order)
+                        // heavy set do not depend on the queue order).  (Up
+                        // to 4 per lane per step, issued together: slower,
+                        // 7.3e6 -> 8.4e6 selection cycles.)
                         for (uint32_t x = x0;; ++x) {
                             const bool act = x < x1;
                             if (__builtin_amdgcn_ballot_w64(act) == 0) break;
@@ -1443,7 +1448,7 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
                 // when the block is.  The workgroup bins the open members by
                 // in-degree (64 bins), then takes every member above the
                 // threshold bin and the lowest-index ones of that bin.
-                const uint64_t tpk = pc.acc ? clock64() : 0;
+                const uint64_t tpk = pc.on() ? clock64() : 0;
                 ++npick;
                 const uint32_t want = 2 * min((uint32_t)GOV_PICK_REPS, (fvs_max - nh) / 2);
                 auto is_open = [&](uint32_t pv) { return pv != 0u && pv < 0x100u; };
@@ -1554,7 +1559,7 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
                 }
                 __syncthreads();
                 if (T >= 63) nh = L.nleft;
-                if (pc.acc) pick_cyc += clock64() - tpk;
+                if (pc.on()) pick_cyc += clock64() - tpk;
             }
             // st and the levels; the highest level
             uint32_t ml = 1;
@@ -1579,8 +1584,16 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
             const uint32_t nH = L.nleft, r = L.rounds;
             const bool fall_back = L.chg != 0;
             pc.lap(GP_FVS_SEL);
+            pc.add(GP_N_FVS_BLOCKS, 1);
+            pc.add(GP_N_FORM_LEVELS, r);
+            pc.add(GP_N_HEAVY, nH);
             if (!fall_back) {
                 const uint32_t HW = (nH + 1 + 63) / 64;  // words per form (column nH = constant)
+                // forms member-major: member i's 2 * HW words (planes of a
+                // word adjacent) in one piece, so a dependency's form is one
+                // or two cache lines (word-major they spanned 2 * HW lines
+                // per read; forms 7.97e6 -> 7.40e6 cycles)
+                auto V = [&](uint32_t i, uint32_t w, uint32_t q) -> uint64_t & { return scr[V0 + ((size_t)i * HW + w) * 2 + q]; };
                 for (uint32_t i = tid; i < sz; i += GS_THREADS)
                     if (st[i] == 2)
                         for (uint32_t w = 0; w < HW; ++w) {
@@ -1651,35 +1664,49 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
                 for (uint32_t i = tid; i < sz; i += GS_THREADS)
                     if (st[i] == 1) rlist[atomicAdd(&rcur[rnd[i]], 1u)] = (int16_t)i;
                 __syncthreads();
-                for (uint32_t R = 0; R < r; ++R) {
-                    const uint32_t o0 = roff[R], nR = roff[R + 1] - o0;
-                    if (nR == 0) continue;  // (uniform)
-                    for (uint32_t t = tid; t < nR; t += GS_THREADS) {
-                        const uint32_t i = (uint32_t)rlist[o0 + t];
-                        const int d0 = idep[3 * i], d1 = idep[3 * i + 1], d2 = idep[3 * i + 2];
-                        const uint32_t info = (uint32_t)rinfo[i];
-                        uint64_t a1[FW], a2[FW];
+                // the levels, with register arrays of exactly HW words (the
+                // FW-word form spilled part of them to scratch at the
+                // kernel's 128-VGPR limit: a scratch round trip per member)
+                auto form_levels = [&](auto hw) {
+                    constexpr uint32_t H = decltype(hw)::value;
+                    for (uint32_t R = 0; R < r; ++R) {
+                        const uint32_t o0 = roff[R], nR = roff[R + 1] - o0;
+                        if (nR == 0) continue;  // (uniform)
+                        for (uint32_t t = tid; t < nR; t += GS_THREADS) {
+                            const uint32_t i = (uint32_t)rlist[o0 + t];
+                            const int d0 = idep[3 * i], d1 = idep[3 * i + 1], d2 = idep[3 * i + 2];
+                            const uint32_t info = (uint32_t)rinfo[i];
+                            uint64_t a1[H], a2[H];
 #pragma unroll
-                        for (uint32_t w = 0; w < FW; ++w) a1[w] = a2[w] = 0;
-#pragma unroll
-                        for (uint32_t w = 0; w < FW; ++w)
-                            if (w < HW) {
+                            for (uint32_t w = 0; w < H; ++w) {
+                                a1[w] = a2[w] = 0;
                                 if (d0 >= 0) gf3_add(a1[w], a2[w], V(d0, w, 0), V(d0, w, 1));
                                 if (d1 >= 0) gf3_add(a1[w], a2[w], V(d1, w, 0), V(d1, w, 1));
                                 if (d2 >= 0) gf3_add(a1[w], a2[w], V(d2, w, 0), V(d2, w, 1));
                             }
-                        // x = cf * (h - sum): -sum has the planes swapped; add
-                        // h - cst in the constant column of (a2, a1)
-                        add_unit(a2, a1, nH, info & 3u);
+                            // x = cf * (h - sum): -sum has the planes swapped;
+                            // add h - cst in the constant column of (a2, a1)
+                            const uint32_t kk = info & 3u;
 #pragma unroll
-                        for (uint32_t w = 0; w < FW; ++w)
-                            if (w < HW) {
+                            for (uint32_t w = 0; w < H; ++w)
+                                if (w == cw) gf3_add(a2[w], a1[w], kk == 1 ? cbit : 0, kk == 2 ? cbit : 0);
+#pragma unroll
+                            for (uint32_t w = 0; w < H; ++w) {
                                 // times cf = 2 swaps the planes back
                                 V(i, w, 0) = (info & 4u) ? a1[w] : a2[w];
                                 V(i, w, 1) = (info & 4u) ? a2[w] : a1[w];
                             }
+                        }
+                        __syncthreads();
                     }
-                    __syncthreads();
+                };
+                switch (HW) {
+                    case 1: form_levels(std::integral_constant<uint32_t, 1>{}); break;
+                    case 2: form_levels(std::integral_constant<uint32_t, 2>{}); break;
+                    case 3: form_levels(std::integral_constant<uint32_t, 3>{}); break;
+                    case 4: form_levels(std::integral_constant<uint32_t, 4>{}); break;
+                    case 5: form_levels(std::integral_constant<uint32_t, 5>{}); break;
+                    default: form_levels(std::integral_constant<uint32_t, FW>{}); break;
                 }
                 pc.lap(GP_FVS_FORMS);
                 // the heavy members' equations: cf*x_j + forms = h, in LDS
@@ -1903,13 +1930,13 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
     return true;
 }
 
-template <class Lds>
-__device__ __forceinline__ void store_bucket(Lds &L, const SolveArgs &a, uint64_t b, uint32_t j, PhaseClock &pc);
+template <class Lds, class PC>
+__device__ __forceinline__ void store_bucket(Lds &L, const SolveArgs &a, uint64_t b, uint32_t j, PC &pc);
 
 // Solves bucket b with state L (LDS or a global slab) and stores its values
 // and local seed.  Workgroup-uniform.
-template <class Lds>
-__device__ __forceinline__ void solve_bucket(Lds &L, const SolveArgs &a, uint64_t b, uint64_t *scr, PhaseClock &pc) {
+template <class Lds, class PC>
+__device__ __forceinline__ void solve_bucket(Lds &L, const SolveArgs &a, uint64_t b, uint64_t *scr, PC &pc) {
     const uint64_t lo = a.E[b] & OFFSET_MASK, hi = a.E[b + 1] & OFFSET_MASK;
     const uint32_t cnt = (uint32_t)(hi - lo);
     const uint64_t vo = vertex_offset(lo);
@@ -1922,9 +1949,9 @@ __device__ __forceinline__ void solve_bucket(Lds &L, const SolveArgs &a, uint64_
     const ulonglong2 *sig = reinterpret_cast<const ulonglong2 *>(a.sig) + (lo - a.e0);
     uint32_t j = 0;
     for (; j < 256; ++j) {
-        const uint64_t t_try = pc.acc ? clock64() : 0;
+        const uint64_t t_try = pc.on() ? clock64() : 0;
         if (try_seed(L, sig, cnt, nv, (uint64_t)j << 56, scr, pc, a.fvs_max)) break;
-        if (pc.acc) pc.add(GP_FAILED_CYCLES, clock64() - t_try);
+        if (pc.on()) pc.add(GP_FAILED_CYCLES, clock64() - t_try);
     }
     pc.start();
     if (j == 256) {
@@ -1937,8 +1964,8 @@ __device__ __forceinline__ void solve_bucket(Lds &L, const SolveArgs &a, uint64_
 // Stores bucket b's solution (L after a successful try_seed with seed j):
 // its 2-bit values, the seed in E[b]'s top byte and the F2 / A11 / A13
 // outputs.  Workgroup-uniform.
-template <class Lds>
-__device__ __forceinline__ void store_bucket(Lds &L, const SolveArgs &a, uint64_t b, uint32_t j, PhaseClock &pc) {
+template <class Lds, class PC>
+__device__ __forceinline__ void store_bucket(Lds &L, const SolveArgs &a, uint64_t b, uint32_t j, PC &pc) {
     const uint64_t lo = a.E[b] & OFFSET_MASK, hi = a.E[b + 1] & OFFSET_MASK;
     const uint32_t cnt = (uint32_t)(hi - lo);
     const uint64_t vo = vertex_offset(lo);
@@ -2005,10 +2032,11 @@ __device__ __forceinline__ bool lower_seeds_failed(const SeedLedger &g, uint32_t
     return true;
 }
 
+template <bool PROF>
 __global__ __launch_bounds__(GS_THREADS, GS_THREADS * GS_PER_CU / 256) void k_gov_solve(SolveArgs a) {
     __shared__ SolveLds L;
     uint64_t *scr = a.scratch + (size_t)blockIdx.x * solve_scratch_words<SolveLds>();
-    PhaseClock pc{a.prof ? a.prof + (size_t)blockIdx.x * GP_N : nullptr, 0};
+    PhaseClock<PROF> pc{PROF && a.prof ? a.prof + (size_t)blockIdx.x * GP_N : nullptr, 0};
     const SeedLedger &g = a.led;
     const uint32_t nb = (uint32_t)(a.m - a.b0);
     // buckets from a queue (status[2], zeroed with the status word): seed
@@ -2084,7 +2112,7 @@ __global__ __launch_bounds__(GS_THREADS, GS_THREADS * GS_PER_CU / 256) void k_go
             continue;
         }
         const ulonglong2 *sig = reinterpret_cast<const ulonglong2 *>(a.sig) + (lo - a.e0);
-        const uint64_t t_try = pc.acc ? clock64() : 0;
+        const uint64_t t_try = pc.on() ? clock64() : 0;
         const bool ok = try_seed(L, sig, cnt, nv, (uint64_t)sd << 56, scr, pc, a.fvs_max);
         if (threadIdx.x == 0) {
             uint32_t win = 0;
@@ -2109,7 +2137,7 @@ __global__ __launch_bounds__(GS_THREADS, GS_THREADS * GS_PER_CU / 256) void k_go
         }
         __syncthreads();
         if (!ok) {
-            if (pc.acc) pc.add(GP_FAILED_CYCLES, clock64() - t_try);
+            if (pc.on()) pc.add(GP_FAILED_CYCLES, clock64() - t_try);
             continue;
         }
         if (!sh_win) {
@@ -2137,7 +2165,7 @@ __global__ __launch_bounds__(GS_THREADS) void k_gov_solve_mid(SolveArgs a, const
                                                               uint64_t *scratch) {
     __shared__ SolveMid L;
     uint64_t *scr = scratch + (size_t)blockIdx.x * solve_scratch_words<SolveMid>();
-    PhaseClock pc{nullptr, 0};
+    PhaseClock<false> pc{nullptr, 0};
     for (uint32_t li = blockIdx.x; li < nbig; li += gridDim.x)
         if (mid_bucket(a, a.b0 + list[li])) solve_bucket(L, a, a.b0 + list[li], scr, pc);
 }
@@ -2148,7 +2176,7 @@ __global__ __launch_bounds__(GS_THREADS) void k_gov_solve_big(SolveArgs a, const
                                                               uint8_t *slabs, size_t slab_bytes) {
     SolveBig &L = *reinterpret_cast<SolveBig *>(slabs + (size_t)blockIdx.x * slab_bytes);
     uint64_t *scr = reinterpret_cast<uint64_t *>(slabs + (size_t)blockIdx.x * slab_bytes + ((sizeof(SolveBig) + 255) & ~(size_t)255));
-    PhaseClock pc{nullptr, 0};
+    PhaseClock<false> pc{nullptr, 0};
     for (uint32_t li = blockIdx.x; li < nbig; li += gridDim.x)
         if (!mid_bucket(a, a.b0 + list[li])) solve_bucket(L, a, a.b0 + list[li], scr, pc);
 }
