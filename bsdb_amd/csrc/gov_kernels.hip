@@ -39,7 +39,10 @@ constexpr int GS_CMAX = 1664;    // keys per bucket solved in LDS (expected ~150
 constexpr int GS_NVMAX = 1872;   // > vertex_offset span of GS_CMAX keys
 constexpr int GS_TINY = 12;      // brute-force buckets (only in sets of < ~1500 keys)
 #ifndef GOV_PICK_REPS
-#define GOV_PICK_REPS 8  // FVS: pairs of heavy hinges taken per stuck cascade
+// FVS: pairs of heavy hinges taken per stuck cascade (with the in x out pick
+// key, C2 at 6 / 8 / 12 / 16 / 24: 522 / 536 / 553 / 558 / ~556 M keys/s,
+// profiles/r4/pick_size_ab/)
+#define GOV_PICK_REPS 16
 #endif
 constexpr int GS_WMAX = (GS_CMAX + 1 + 63) / 64;  // words per bit-sliced row
 // Oversized buckets (adversarial or skewed key sets: > GS_CMAX keys, 14 sigma
@@ -1441,17 +1444,30 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
                     break;
                 }
                 // The next heavy hinges: the `want` open members of the
-                // largest key (in-degree, then lowest index) -- the set
+                // largest key (pick_key below, then lowest index) -- the set
                 // GOV_PICK_REPS rounds of "the best two" (below) pick, as
                 // nothing is placed between those rounds: any feedback vertex
                 // set gives the same unique solution and is singular exactly
                 // when the block is.  The workgroup bins the open members by
-                // in-degree (64 bins), then takes every member above the
+                // key (64 bins), then takes every member above the
                 // threshold bin and the lowest-index ones of that bin.
                 const uint64_t tpk = pc.on() ? clock64() : 0;
                 ++npick;
                 const uint32_t want = 2 * min((uint32_t)GOV_PICK_REPS, (fvs_max - nh) / 2);
                 auto is_open = [&](uint32_t pv) { return pv != 0u && pv < 0x100u; };
+                // the pick key of an open member: its open dependents x its
+                // open dependency slots (the usual greedy feedback-vertex-set
+                // score: a member many others wait on and that waits on many
+                // breaks the most cycles).  Against open dependents alone:
+                // heavy set 223 -> 204 per block, C2 524 -> 537 M keys/s
+                // (`profiles/r4/pick_key_ab/`; GOV_PICK_KEY=0 builds that)
+                auto pick_key = [&](uint32_t i) -> uint32_t {
+#if defined(GOV_PICK_KEY) && GOV_PICK_KEY == 0
+                    return indeg[i];
+#else
+                    return indeg[i] * (pend[i] & 0xFFu);
+#endif
+                };
                 auto make_heavy = [&](uint32_t i, uint32_t j, uint32_t slot) {
                     pend[i] += 0x100u;
                     lvl[i] = 0;
@@ -1462,7 +1478,7 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
                 if (tid < 64) hb[tid] = 0;
                 __syncthreads();
                 for (uint32_t i = tid; i < sz; i += GS_THREADS)
-                    if (is_open(pend[i])) atomicAdd(&hb[min(indeg[i], 63u)], 1u);
+                    if (is_open(pend[i])) atomicAdd(&hb[min(pick_key(i), 63u)], 1u);
                 __syncthreads();
                 uint32_t suf = hb[lane];  // -> open members of in-degree >= lane (every wave alike)
 #pragma unroll
@@ -1484,7 +1500,7 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
                     for (uint32_t k0 = 0; k0 < sz; k0 += GS_THREADS, par ^= 1u) {
                         const uint32_t i = k0 + tid;
                         const bool open = i < sz && is_open(pend[i]);
-                        const uint32_t dvc = open ? min(indeg[i], 63u) : 0u;
+                        const uint32_t dvc = open ? min(pick_key(i), 63u) : 0u;
                         const bool eq = open && dvc == T, gt = open && dvc > T;
                         const uint64_t em = __builtin_amdgcn_ballot_w64(eq), gm = __builtin_amdgcn_ballot_w64(gt);
                         if (lane == 0) {
@@ -1527,7 +1543,7 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
                             for (uint32_t u = 0; u < 8; ++u) {
                                 const uint32_t i = lane + 64 * (q0 + u);
                                 sv[u] = i < sz ? pend[i] : 0u;
-                                dv[u] = i < sz ? indeg[i] : 0u;
+                                dv[u] = i < sz ? min(pick_key(i), 0xFFFFu) : 0u;
                             }
 #pragma unroll
                             for (uint32_t u = 0; u < 8; ++u)
