@@ -1306,7 +1306,10 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
         // when the block is, with the same null space dimension); a singular
         // one is then moved to the block's own canonical solution (free
         // columns 0) through that null space, below.
-        constexpr uint32_t FVS_MIN = 96, FW = 6;  // <= 6 words per form / heavy row
+#ifndef GOV_FVS_MIN
+#define GOV_FVS_MIN 96
+#endif
+        constexpr uint32_t FVS_MIN = GOV_FVS_MIN, FW = 6;  // <= 6 words per form / heavy row
         static_assert(FVS_NH_MAX + 1 <= 64 * FW, "heavy columns + the constant column must fit FW words");
         constexpr size_t V0 = (size_t)16 * Lds::CMAX;          // affine forms, past that region
         bool solved = false;

@@ -1,4 +1,6 @@
 #!/bin/bash
+# (Round 4: the panel Gauss-Jordan was not kept and its code is gone, DESIGN §4.3;
+# this is the script that ran that A/B.)
 # A/B of the heavy system's Gauss-Jordan: panels of 8 columns (default) against the column loop
 # (BSDB_GOV_GJ_COLUMN=1), same library: GOV parity tests in both modes, the phase profile at 1e7
 # keys and the C2 full build, alternated.
