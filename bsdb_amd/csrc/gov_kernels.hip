@@ -40,9 +40,9 @@ constexpr int GS_NVMAX = 1872;   // > vertex_offset span of GS_CMAX keys
 constexpr int GS_TINY = 12;      // brute-force buckets (only in sets of < ~1500 keys)
 #ifndef GOV_PICK_REPS
 // FVS: pairs of heavy hinges taken per stuck cascade (with the in x out pick
-// key, C2 at 6 / 8 / 12 / 16 / 24: 522 / 536 / 553 / 558 / ~556 M keys/s,
-// profiles/r4/pick_size_ab/)
-#define GOV_PICK_REPS 16
+// key, C2 at 6 / 8 / 12 / 16 / 20 / 24: 522 / 536 / 553 / 558 / 565 / ~563 M
+// keys/s, profiles/r4/pick_size_ab/, solver_sweep/)
+#define GOV_PICK_REPS 20
 #endif
 constexpr int GS_WMAX = (GS_CMAX + 1 + 63) / 64;  // words per bit-sliced row
 // Oversized buckets (adversarial or skewed key sets: > GS_CMAX keys, 14 sigma
@@ -729,17 +729,29 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
             if (f2 && c2 < bc) { best = (int)v2; }
             return best;
         };
+        // a chunk's edges and vertices are read one chunk ahead (neither
+        // changes here), so a chunk starts at its ownership reads
+        auto chunk_edges = [&](uint32_t k, bool &a, uint32_t &u0, uint32_t &u1, uint32_t &u2) {
+            a = k < cnt && L.round_of[k] < 0;
+            u0 = u1 = u2 = 0;
+            if (a) {
+                u0 = L.e[3 * k];
+                u1 = L.e[3 * k + 1];
+                u2 = L.e[3 * k + 2];
+            }
+        };
+        bool nact;
+        uint32_t n0, n1, n2;
+        chunk_edges(tid, nact, n0, n1, n2);
         for (uint32_t k0 = 0; k0 < cnt; k0 += 64) {
             const uint32_t k = k0 + tid;
-            const bool act = k < cnt && L.round_of[k] < 0;
-            uint32_t v0 = 0, v1 = 0, v2 = 0, c0 = 0, c1 = 0, c2 = 0;
+            const bool act = nact;
+            uint32_t v0 = n0, v1 = n1, v2 = n2, c0 = 0, c1 = 0, c2 = 0;
+            chunk_edges(k + 64, nact, n0, n1, n2);
             bool f0 = false, f1 = false, f2 = false;
             const uint32_t me = lane_tag | tid;
             lane_tag -= 64;
             if (act) {
-                v0 = L.e[3 * k];
-                v1 = L.e[3 * k + 1];
-                v2 = L.e[3 * k + 2];
                 f0 = L.vowner[v0] < 0;
                 f1 = L.vowner[v1] < 0;
                 f2 = L.vowner[v2] < 0;
@@ -813,7 +825,9 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
     // its lowest lane only (atomicMin over its stamp word), the first free
     // vertex in lane order ends the BFS (lanes after it do nothing, as the
     // sequential loop breaks there), and the newly reached owners are
-    // appended in lane order.  Same queue, same marks, same path.
+    // appended in lane order.  Same queue, same marks, same path.  (Queue
+    // entries carrying their edge's vertices, read by the appending lane, to
+    // save the next chunk a round trip: BFS 7.15e6 -> 8.30e6 cycles, not kept.)
     if (tid < 64) {
         int16_t *bfs_prev = L.a0, *queue = L.a1;
         uint32_t *first_lane = L.xe;  // (dead after peeling)
