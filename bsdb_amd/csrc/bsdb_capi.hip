@@ -1335,6 +1335,7 @@ static int gov_build_impl(bsdb_ctx *c, const GovSrc &src, uint64_t n_global, uin
     }
     uint32_t fvs_max = FVS_NH_MAX;
     if (const char *v = getenv("BSDB_GOV_FVS_MAX")) fvs_max = (uint32_t)std::max(2, std::min(atoi(v), (int)FVS_NH_MAX));
+    if (getenv("BSDB_GOV_PICK_EXACT")) fvs_max |= 0x80000000u;  // (test aid: the exact-rounds FVS picks)
     if (width && full) HIP_OK(hipMemsetAsync(d_sigbits, 0, ((n_global * width + 63) / 64 + 1) * 8, s));
     // the seed ledger: claim, won, done (u32 per bucket), fail (4 u64 per
     // bucket), zeroed; active (u32 per workgroup), all ones

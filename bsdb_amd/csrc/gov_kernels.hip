@@ -619,6 +619,10 @@ template <class Lds, class PC>
 __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t cnt, uint32_t nv, uint64_t seed_bits,
                          uint64_t *scr, PC &pc, uint32_t fvs_max) {
     const int tid = threadIdx.x;
+    // bit 31 (BSDB_GOV_PICK_EXACT, a test aid): every FVS pick by the exact
+    // rounds of wave 0 instead of the binned one, a different heavy set
+    const bool pick_exact = (fvs_max >> 31) != 0;
+    fvs_max &= 0x7FFFFFFFu;
     pc.start();
     pc.add(GP_N_SEEDS, 1);
     const bool tiny = cnt <= GS_TINY;
@@ -1508,7 +1512,7 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
                 const uint32_t above = T < 63 ? (uint32_t)__builtin_amdgcn_readlane((int)suf, (int)T + 1) : 0u;
                 const uint32_t in_t = (uint32_t)__builtin_amdgcn_readlane((int)suf, (int)T) - above;
                 const uint32_t take_t = okm ? want - above : in_t;  // (fewer open members than want: all)
-                if (T < 63) {
+                if (T < 63 && !pick_exact) {
                     // in index order: per chunk of GS_THREADS members, each
                     // wave's counts of threshold-bin and above-threshold open
                     // members (double-buffered by chunk), one barrier a chunk

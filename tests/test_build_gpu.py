@@ -271,6 +271,25 @@ def test_fvs_limit_fallback_is_identical(ctx, monkeypatch):
         np.testing.assert_array_equal(u64(v_d), vals)
 
 
+def test_fvs_pick_paths_are_identical(ctx, monkeypatch):
+    """Round 4: the heavy set is picked by the workgroup's binned pass, or by
+    wave 0's exact rounds when 64+ open members share the top bin; forcing the
+    exact rounds everywhere (a different heavy set, alone and with a small
+    heavy-set limit) gives the same, oracle-equal output."""
+    keys = O.gen_keys13(12, 400_000)
+    sig = O.hash_fixed_mt(keys, 13, THREADS)
+    rc, E, vals, sb, _ = O.gov_build_mt(sig, 4, THREADS)
+    assert rc == 0
+    monkeypatch.setenv("BSDB_GOV_PICK_EXACT", "1")
+    for lim in (None, "40"):
+        if lim:
+            monkeypatch.setenv("BSDB_GOV_FVS_MAX", lim)
+        E_d, v_d, s_d = ctx.gov_build(dev(sig.view(np.int64)), 4)
+        np.testing.assert_array_equal(u64(E_d), E)
+        np.testing.assert_array_equal(u64(v_d), vals)
+        np.testing.assert_array_equal(u64(s_d)[: sb.size], sb)
+
+
 @pytest.mark.parametrize("n,width", [(1, 4), (3001, 0), (777_777, 4), (400_000, 64)])
 def test_ranks_from_the_solve(ctx, n, width):
     """F2: the solve's ranks equal getLong of every key (oracle lookups), and
