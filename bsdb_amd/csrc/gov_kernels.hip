@@ -1704,21 +1704,14 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
                 // the levels, with register arrays of exactly HW words (the
                 // FW-word form spilled part of them to scratch at the
                 // kernel's 128-VGPR limit: a scratch round trip per member)
-#if defined(GOV_FORMS_ONE_WAVE)
-                // (variant: wave 0 alone, a wave fence per level)
-                constexpr uint32_t FT = 64;
-                const bool form_thread = tid < 64;
-#else
-                constexpr uint32_t FT = GS_THREADS;
-                const bool form_thread = true;
-#endif
+                // (wave 0 alone with a wave fence per level instead of the
+                // workgroup barrier: forms 4.13e6 -> 4.59e6 cycles, not kept)
                 auto form_levels = [&](auto hw) {
                     constexpr uint32_t H = decltype(hw)::value;
-                    if (!form_thread) return;
                     for (uint32_t R = 0; R < r; ++R) {
                         const uint32_t o0 = roff[R], nR = roff[R + 1] - o0;
                         if (nR == 0) continue;  // (uniform)
-                        for (uint32_t t = tid; t < nR; t += FT) {
+                        for (uint32_t t = tid; t < nR; t += GS_THREADS) {
                             const uint32_t i = (uint32_t)rlist[o0 + t];
                             const int d0 = idep[3 * i], d1 = idep[3 * i + 1], d2 = idep[3 * i + 2];
                             const uint32_t info = (uint32_t)rinfo[i];
@@ -1743,13 +1736,7 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
                                 V(i, w, 1) = (info & 4u) ? a2[w] : a1[w];
                             }
                         }
-#if defined(GOV_FORMS_ONE_WAVE)
-                        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-                        __builtin_amdgcn_wave_barrier();
-                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-#else
                         __syncthreads();
-#endif
                     }
                 };
                 switch (HW) {
@@ -1760,9 +1747,6 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
                     case 5: form_levels(std::integral_constant<uint32_t, 5>{}); break;
                     default: form_levels(std::integral_constant<uint32_t, FW>{}); break;
                 }
-#if defined(GOV_FORMS_ONE_WAVE)
-                __syncthreads();
-#endif
                 pc.lap(GP_FVS_FORMS);
                 // the heavy members' equations: cf*x_j + forms = h, in LDS
                 // (the forms' selection arrays are dead now) when they fit
