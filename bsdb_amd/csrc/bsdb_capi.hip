@@ -304,6 +304,28 @@ int launch_status() {
     return e == hipSuccess ? BSDB_OK : hip_fail(e, "kernel launch", 0);
 }
 
+// CPUs this process may use: its affinity mask, capped by a cgroup v2 CPU
+// quota (a container's share of a large host shows the host's CPUs in both
+// std::thread::hardware_concurrency() and the affinity mask)
+int usable_cpus() {
+    static const int n = [] {
+        int c = (int)std::max(1u, std::thread::hardware_concurrency());
+        cpu_set_t cs;
+        if (sched_getaffinity(0, sizeof(cs), &cs) == 0) c = std::max(1, CPU_COUNT(&cs));
+        if (FILE *f = fopen("/sys/fs/cgroup/cpu.max", "r")) {
+            char q[32] = {0};
+            unsigned long long per = 0;
+            if (fscanf(f, "%31s %llu", q, &per) == 2 && strcmp(q, "max") != 0 && per > 0) {
+                const unsigned long long quota = strtoull(q, nullptr, 10);
+                if (quota > 0) c = std::min<int>(c, (int)std::max<unsigned long long>(1, (quota + per - 1) / per));
+            }
+            fclose(f);
+        }
+        return c;
+    }();
+    return n;
+}
+
 // ---- pass-1 dispatch over (source layout, epilogue) ------------------------
 // One-tile-per-workgroup launches: tiles * 512 work-items must stay below 2^32
 // (a dispatch packet's grid size is 32-bit), so callers split larger key sets.

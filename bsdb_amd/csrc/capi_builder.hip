@@ -167,9 +167,7 @@ int write_slots(int device, const OutFile &f, const uint64_t *d_src, uint64_t nl
                 const OutFile *fa) {
     if (nl == 0) return BSDB_OK;
     constexpr uint64_t PIECE = XFER_PIECE / 8;  // slots
-    cpu_set_t cs_set;
-    int ncpu = 1;
-    if (sched_getaffinity(0, sizeof(cs_set), &cs_set) == 0) ncpu = CPU_COUNT(&cs_set);
+    const int ncpu = usable_cpus();
     const uint64_t npieces = (nl + PIECE - 1) / PIECE;
     const uint64_t T = std::max<uint64_t>(1, std::min<uint64_t>({(uint64_t)16, (uint64_t)ncpu, npieces}));
     std::atomic<int> rc{BSDB_OK};

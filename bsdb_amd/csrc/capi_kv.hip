@@ -156,7 +156,7 @@ int bsdb_kv_scan(const char *kv_base, int partitions, int format, uint32_t block
         return BSDB_EINVAL;
     *out = nullptr;
     std::vector<KvPart> parts(partitions);
-    const int T = std::max(1, std::min(threads > 0 ? threads : (int)std::thread::hardware_concurrency(), partitions));
+    const int T = std::max(1, std::min(threads > 0 ? threads : usable_cpus(), partitions));
     std::atomic<int> next{0};
     auto worker = [&] {
         for (int p; (p = next.fetch_add(1)) < partitions;) {
@@ -290,7 +290,8 @@ int bsdb_kv_build_index(bsdb_ctx *c, const char *kv_base, int partitions, int fo
     if (rc) return rc;
     std::unique_ptr<bsdb_builder, int (*)(bsdb_builder *)> guard(b, bsdb_builder_free);
     std::mutex add_mu;
-    const int T = std::max(1, std::min(threads > 0 ? threads : (int)std::thread::hardware_concurrency(), partitions));
+    // (partitions in flight = threads: the host memory bound)
+    const int T = std::max(1, std::min(threads > 0 ? threads : usable_cpus(), partitions));
     std::atomic<int> next{0};
     std::atomic<int> err{BSDB_OK};
     auto worker = [&] {

@@ -318,9 +318,7 @@ int write_files(int device, FILE *const *files, const void *const *d_srcs, int n
         }
         return BSDB_OK;
     }
-    cpu_set_t cs_set;
-    int ncpu = 1;
-    if (sched_getaffinity(0, sizeof(cs_set), &cs_set) == 0) ncpu = CPU_COUNT(&cs_set);
+    const int ncpu = usable_cpus();
     const uint64_t npieces = (bytes + XFER_PIECE - 1) / XFER_PIECE;
     const uint64_t T = std::max<uint64_t>(1, std::min<uint64_t>({(uint64_t)8, (uint64_t)ncpu, npieces}));
     for (int fi = 0; fi < nfiles; ++fi) {
