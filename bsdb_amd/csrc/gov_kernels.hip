@@ -40,8 +40,8 @@ constexpr int GS_NVMAX = 1872;   // > vertex_offset span of GS_CMAX keys
 constexpr int GS_TINY = 12;      // brute-force buckets (only in sets of < ~1500 keys)
 #ifndef GOV_PICK_REPS
 // FVS: pairs of heavy hinges taken per stuck cascade (with the in x out pick
-// key, C2 at 6 / 8 / 12 / 16 / 20 / 24: 522 / 536 / 553 / 558 / 565 / ~563 M
-// keys/s, profiles/r4/pick_size_ab/, solver_sweep/)
+// key, C2 at 6 / 8 / 12 / 16 / 20 / 24 / 28: 522 / 536 / 553 / 558 / 566–569 /
+// 565 / 560 M keys/s, profiles/r4/pick_size_ab/, solver_sweep/)
 #define GOV_PICK_REPS 20
 #endif
 constexpr int GS_WMAX = (GS_CMAX + 1 + 63) / 64;  // words per bit-sliced row
