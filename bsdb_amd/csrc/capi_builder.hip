@@ -90,6 +90,15 @@ struct bsdb_builder {
     bool borrowed_records = false;  // one-call forms: the caller's record arrays cover every key
     int failed = BSDB_OK;  // an add that failed part-way leaves the builder unusable
     bool finished = false;
+    std::mutex mu;  // one add (or the finish) at a time: adds may come from several threads
+    // the record arrays' pages, populated in the background from the open
+    // (first-touch faults of ~2 µs a page were most of an add's time)
+    Populator pop_addr, pop_v8;
+    void stop_prefault() {
+        pop_addr.finish();
+        pop_v8.finish();
+    }
+    ~bsdb_builder() { stop_prefault(); }
 };
 
 namespace {
@@ -256,6 +265,8 @@ int builder_check_records(const bsdb_builder *b, uint64_t count, const uint64_t 
 int builder_add_records(bsdb_builder *b, uint64_t count, const uint64_t *h_addr, const uint64_t *h_value8,
                         const uint8_t *h_vlen) {
     if (b->borrowed_records) return BSDB_OK;
+    if ((!b->stride && b->addr.n + count > b->addr.cap) || (b->approx && b->value8.n + count > b->value8.cap))
+        b->stop_prefault();  // (a growing array may move)
     if (!b->stride && !b->addr.append(h_addr, count)) return BSDB_ENOMEM;
     if (b->approx && (!b->value8.append(h_value8, count) || !b->vlen.append(h_vlen, count))) return BSDB_ENOMEM;
     return BSDB_OK;
@@ -315,8 +326,14 @@ int builder_add_var_locked(bsdb_builder *b, const uint8_t *h_blob, const uint64_
     if ((rc = dev_reserve(c, (void **)&b->d_off, &b->off_cap, (b->n + 1) * 8, (b->n + count + 1) * 8))) return rc;
     if (bytes) HIP_OK(hipMemcpyAsync(b->d_keys + b->key_bytes, h_blob + o0, bytes, hipMemcpyHostToDevice, c->stream));
     uint64_t *dst = b->d_off + b->n + 1;
-    HIP_OK(hipMemcpyAsync(dst, h_off + 1, count * 8, hipMemcpyHostToDevice, c->stream));
-    k_rebase_offsets<<<grid_for(c, count), 256, 0, c->stream>>>(dst, count, b->key_bytes - o0);
+    if (uni != 0xFFFFFFFFu) {
+        // one length (a kv.db partition of fixed-size keys): the offsets are
+        // a formula, written on the device instead of copied
+        k_fill_offsets<<<grid_for(c, count), 256, 0, c->stream>>>(dst, count, b->key_bytes, uni);
+    } else {
+        HIP_OK(hipMemcpyAsync(dst, h_off + 1, count * 8, hipMemcpyHostToDevice, c->stream));
+        k_rebase_offsets<<<grid_for(c, count), 256, 0, c->stream>>>(dst, count, b->key_bytes - o0);
+    }
     HIP_OK(hipStreamSynchronize(c->stream));  // the caller may reuse its buffers
     if ((rc = launch_status())) return rc;
     if (b->n == 0) b->uni_len = uni;
@@ -329,6 +346,7 @@ int builder_add_var_locked(bsdb_builder *b, const uint8_t *h_blob, const uint64_
 template <class Add>
 int builder_add(bsdb_builder *b, uint64_t count, const uint64_t *h_addr, const uint64_t *h_value8,
                 const uint8_t *h_vlen, Add &&add) {
+    std::lock_guard<std::mutex> gb(b->mu);
     if (b->failed) return b->failed;
     if (b->finished) return BSDB_EINVAL;
     int rc = builder_check_records(b, count, h_addr, h_value8, h_vlen);
@@ -495,6 +513,7 @@ int builder_finish_locked(bsdb_builder *b, uint32_t width, uint32_t passes, cons
 }
 
 void builder_release(bsdb_builder *b) {
+    b->stop_prefault();
     (void)hipSetDevice(b->c->device);
     (void)hipFree(b->d_keys);
     (void)hipFree(b->d_off);
@@ -542,6 +561,8 @@ int builder_open(bsdb_ctx *c, uint32_t key_len, uint64_t key_capacity, uint64_t 
         delete b;
         return rc;
     }
+    if (!b->stride && b->addr.cap) b->pop_addr.start(reinterpret_cast<uint8_t *>(b->addr.p), b->addr.cap * 8);
+    if (b->approx && b->value8.cap) b->pop_v8.start(reinterpret_cast<uint8_t *>(b->value8.p), b->value8.cap * 8);
     *out = b;
     return BSDB_OK;
 }
@@ -561,6 +582,7 @@ static int host_passes_build(bsdb_ctx *c, const uint8_t *h_keys, uint32_t key_le
     int rc = builder_open(c, var ? 0 : key_len, n, blob, approximate, addr_base, h_addr ? 0 : addr_stride, &b);
     if (rc) return rc;
     // the caller's record arrays outlive the call: borrowed, not copied
+    b->stop_prefault();
     b->borrowed_records = true;
     if (h_addr) b->addr.borrow(h_addr, n);
     if (approximate) {
@@ -648,6 +670,7 @@ int bsdb_builder_finish(bsdb_builder *b, uint32_t width, uint32_t passes, const 
                         const char *index_a_path, bsdb_mph **out, uint32_t *passes_used) {
     if (!b || !out || width > 64 || passes > 4096 || (b->approx && index_path && !index_a_path)) return BSDB_EINVAL;
     *out = nullptr;
+    std::lock_guard<std::mutex> gb(b->mu);
     if (b->failed) return b->failed;
     if (b->finished || b->n / BUCKET_SIZE + 1 > 0x7FFFFFFFULL) return BSDB_EINVAL;
     bsdb_ctx *c = b->c;

@@ -140,6 +140,43 @@ def test_streamed_adds_in_any_order(ctx, tmp_path, host_gather, var, approx):
     b.close(); m1.close(); m2.close()
 
 
+@pytest.mark.parametrize("var", [False, True])
+def test_concurrent_adds_from_threads(ctx, tmp_path, var):
+    """Round 4: adds from several threads at once (a JVM's put threads) are
+    serialised by the builder: the same MPHF and files as one-call build."""
+    import threading
+    n = 240_000
+    keys, blob, off, addr, value8, vlen = make_records(n, var, True, seed=21)
+    m1, ip1, ap1 = f2_reference(ctx, str(tmp_path), n, var, True, keys, blob, off, addr, value8, vlen)
+    b = ctx.builder(0 if var else 13, key_capacity=n // 4, blob_capacity=1000, approximate=True)
+    cuts = np.linspace(0, n, 25).astype(np.int64)
+    errors = []
+
+    def worker(t):
+        try:
+            for j in range(t, len(cuts) - 1, 6):
+                lo, hi = int(cuts[j]), int(cuts[j + 1])
+                if var:
+                    b.add_var(blob, off[lo:hi + 1], addr[lo:hi], value8[lo:hi], vlen[lo:hi])
+                else:
+                    b.add_fixed(keys[13 * lo:13 * hi], 13, addr[lo:hi], value8[lo:hi], vlen[lo:hi])
+        except Exception as e:  # noqa: BLE001 (reported below)
+            errors.append(e)
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(6)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errors
+    assert b.count() == n
+    ip2, ap2 = str(tmp_path / "index.db"), str(tmp_path / "index_a.db")
+    m2, _ = b.finish(4, ip2, ap2, passes=2)
+    assert same_mph(m1, m2)
+    assert same_files(ip1, ip2) and same_files(ap1, ap2)
+    b.close(); m1.close(); m2.close()
+
+
 def test_var_builder_with_one_key_length_takes_the_fixed_kernels(ctx, tmp_path):
     """A variable-length builder whose keys all have one length (the kv.db
     scan of fixed-size keys) builds over the fixed-length kernels: same files;
