@@ -1163,7 +1163,8 @@ static void print_gov_profile(const std::vector<uint64_t> &h, uint32_t solve_gri
                                "n_fail_degenerate", "n_fail_orient", "n_fail_inconsistent", "failed_attempt_cycles",
                                "bfs_flip", "n_bfs_iters", "n_flip_steps", "n_sel_batches", "n_sel_picks",
                                "sel_pick_cycles", "sel_prep_cycles", "n_singular_solved", "n_null_vectors", "n_speculative_lost",
-                               "n_fvs_blocks", "n_form_levels", "n_heavy"};
+                               "n_fvs_blocks", "n_form_levels", "n_heavy", "gj_columns", "gj_barrier_wait_cycles",
+                               "unused"};
     std::vector<double> tot(GP_N, 0.0);
     for (uint32_t w = 0; w < solve_grid; ++w)
         for (int k = 0; k < GP_N; ++k) {

@@ -500,7 +500,8 @@ enum GovProf { GP_EDGES, GP_PEEL, GP_GREEDY, GP_BFS, GP_TARJAN, GP_SINGLE, GP_DE
                GP_N_SCC_SWEEPS, GP_N_SMALL_S, GP_FVS_SEL, GP_FVS_FORMS, GP_FVS_GJ,
                GP_N_FAIL_DEGEN, GP_N_FAIL_ORIENT, GP_N_FAIL_INCONS, GP_FAILED_CYCLES, GP_BFS_FLIP, GP_N_BFS_ITERS,
                GP_N_FLIP_STEPS, GP_N_SEL_BATCHES, GP_N_SEL_PICKS, GP_SEL_PICK_CYCLES, GP_SEL_PREP_CYCLES,
-               GP_N_SING_SOLVED, GP_N_NULL_VECS, GP_N_SPEC_LOST, GP_N_FVS_BLOCKS, GP_N_FORM_LEVELS, GP_N_HEAVY, GP_N };
+               GP_N_SING_SOLVED, GP_N_NULL_VECS, GP_N_SPEC_LOST, GP_N_FVS_BLOCKS, GP_N_FORM_LEVELS, GP_N_HEAVY,
+               GP_GJ_COLUMNS, GP_GJ_BARRIER, GP_GJ_ROWS_WAVE7, GP_N };
 
 // Solver state for buckets of up to CMAX_ keys: LDS for GS_CMAX, a global
 // slab per workgroup for GB_CMAX (same code; indices fit int16 either way).
@@ -1285,7 +1286,15 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
                     const uint64_t bal = __builtin_amdgcn_ballot_w64(cand);
                     if (cand && (uint32_t)__builtin_ctzll(bal) == (tid & 63)) atomicMin(&bid[cn % 3], rr);
                 }
+                // (profiling: columns, and thread 0's wait at the column's
+                // barrier -- the time the workgroup's slowest row takes
+                // beyond thread 0's own)
+                const uint64_t tb = pc.on() ? clock64() : 0;
                 __syncthreads();
+                if (pc.on()) {
+                    pc.add(GP_GJ_COLUMNS, 1);
+                    pc.add(GP_GJ_BARRIER, clock64() - tb);
+                }
             }
             // column cc's pivot row reads cf * x + (free columns, all 0) = rhs
             // with cf in {1, 2} (every other pivot column eliminated), so
