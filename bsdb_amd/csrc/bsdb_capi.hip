@@ -15,6 +15,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <cerrno>
 #include <functional>
 #include <chrono>
 #include <cmath>
@@ -241,18 +242,51 @@ PinnedPool &pinned_pool() {
     return *pool;
 }
 
+// Reserves the file blocks of [off, off + len) (fallocate, mode 0): 0 when
+// they are reserved, 1 when the file system cannot reserve blocks ahead
+// (EOPNOTSUPP: such a file is written with pwrite, never through a mapping),
+// -1 when they cannot be had (ENOSPC, a tmpfs size limit ...).  A store into
+// a shared mapping of a hole the file system cannot back raises SIGBUS, which
+// would kill the process (a JVM included), so every mapped store goes to a
+// reserved range.
+int file_reserve(int fd, uint64_t off, uint64_t len) {
+    if (fd < 0 || !len) return 0;
+    int r;
+    do {
+        r = fallocate(fd, 0, (off_t)off, (off_t)len);
+    } while (r != 0 && errno == EINTR);
+    if (r == 0) return 0;
+    return errno == EOPNOTSUPP || errno == ENOSYS ? 1 : -1;
+}
+
 // Faults a mapped index file's pages in, in file order, on one thread (the
 // writers follow in file order: the builder's pass slices, write_files'
 // pieces): a tmpfs/page-cache page is allocated on its first touch, and 16
 // writer threads faulting the same file concurrently measured 0.84 GB/s
-// against ~5 GB/s for one thread walking it.  MADV_POPULATE_WRITE (Linux
-// 5.14) prefaults without touching the data; elsewhere a read of one byte
-// per page allocates the page the same way (MAP_SHARED) and changes nothing.
+// against ~5 GB/s for one thread walking it.  For a file mapping (fd >= 0)
+// each 64 MiB step first reserves its blocks (file_reserve) and `ready`
+// advances past it, so a writer stores into [0, ready) without a reservation
+// of its own (ensure()); a step that cannot be reserved ends the walk and the
+// writers reserve their own pieces (and fail cleanly).  MADV_POPULATE_WRITE
+// (Linux 5.14) then prefaults without touching the data, and reports failure
+// instead of raising SIGBUS; elsewhere (EINVAL: an older kernel) a read of one
+// byte per page of a reserved step allocates the page the same way.  An
+// anonymous mapping (fd < 0: the builder's record arrays) needs no
+// reservation.
 struct Populator {
     std::thread th;
     std::atomic<bool> stop{false};
+    std::atomic<uint64_t> ready{0};  // bytes from base whose blocks are reserved
+    int fd = -1;
+    uint64_t file_off = 0;           // the file offset of base
     double seconds = 0;
-    void start(uint8_t *base, uint64_t bytes) {
+    Populator() = default;
+    Populator(const Populator &) = delete;
+    Populator &operator=(const Populator &) = delete;
+    ~Populator() { finish(); }
+    void start(uint8_t *base, uint64_t bytes, int file_fd = -1, uint64_t base_off = 0) {
+        fd = file_fd;
+        file_off = base_off;
         if (!base || !bytes || getenv("BSDB_NO_PREFAULT")) return;
         th = std::thread([this, base, bytes] {
             const auto t0 = std::chrono::steady_clock::now();
@@ -261,12 +295,24 @@ struct Populator {
             bool madv = true;
             for (uint64_t o = 0; o < bytes && !stop.load(std::memory_order_relaxed); o += STEP) {
                 const uint64_t k = std::min(STEP, bytes - o);
-                if (madv && madvise(base + o, k, MADV_POPULATE_WRITE_) == 0) continue;
-                madv = false;
+                if (fd >= 0) {
+                    if (file_reserve(fd, file_off + o, k) != 0) break;
+                    ready.store(o + k, std::memory_order_release);
+                }
+                if (madv) {
+                    if (madvise(base + o, k, MADV_POPULATE_WRITE_) == 0) continue;
+                    if (errno != EINVAL) break;  // (the kernel reports what a store would have faulted on)
+                    madv = false;
+                }
                 for (uint64_t q = 0; q < k; q += 4096) (void)*(volatile const uint8_t *)(base + o + q);
             }
             seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
         });
+    }
+    // whether [off, off + len) from base may be stored into
+    bool ensure(uint64_t off, uint64_t len) {
+        if (fd < 0 || off + len <= ready.load(std::memory_order_acquire)) return true;
+        return file_reserve(fd, file_off + off, len) == 0;
     }
     void finish() {
         stop.store(true);

@@ -164,6 +164,7 @@ struct OutFile {
     int fd = -1;
     uint8_t *map = nullptr;
     uint64_t bytes = 0;
+    Populator *pop = nullptr;  // the mapping's populator: stores go to reserved blocks only (file_reserve)
 };
 
 // nl slots of a device buffer to byte 8 * slot0 of f (W:166-179 writes <= 128
@@ -183,6 +184,8 @@ int write_slots(int device, const OutFile &f, const uint64_t *d_src, uint64_t nl
     auto put = [&](const OutFile &o, const void *buf, uint64_t bytes, uint64_t off) {
         if (o.map) {
             if (off + bytes > o.bytes) return false;
+            // (an unreserved hole would raise SIGBUS on a full file system)
+            if (o.pop ? !o.pop->ensure(off, bytes) : file_reserve(o.fd, off, bytes) != 0) return false;
             memcpy(o.map + off, buf, bytes);
             return true;
         }
@@ -226,7 +229,9 @@ int write_slots(int device, const OutFile &f, const uint64_t *d_src, uint64_t nl
             uint64_t *piece = (uint64_t *)pin[i];
             uint64_t *pa = nullptr;
             if (xf && fa) {
-                if (fa->map && off + len * 8 > fa->bytes) ok = false;
+                if (fa->map && (off + len * 8 > fa->bytes ||
+                                (fa->pop ? !fa->pop->ensure(off, len * 8) : file_reserve(fa->fd, off, len * 8) != 0)))
+                    ok = false;
                 pa = fa->map ? reinterpret_cast<uint64_t *>(fa->map + off) : a_piece.data();
             }
             if (ok && xf) (*xf)(piece, len, pa);
@@ -376,7 +381,12 @@ int open_out(const char *path, uint64_t bytes, OutFile *o) {
     if (fstat(o->fd, &st) != 0) return BSDB_EFILE;
     if (!S_ISREG(st.st_mode) || !bytes) return BSDB_OK;
     if (ftruncate(o->fd, (off_t)bytes) != 0) return BSDB_EFILE;
-    void *m = getenv("BSDB_NO_MMAP_WRITE") ? MAP_FAILED : mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_SHARED, o->fd, 0);
+    // mapped only where blocks can be reserved ahead of the stores (a file
+    // system without fallocate is written with pwrite, which reports ENOSPC)
+    const int res = file_reserve(o->fd, 0, std::min<uint64_t>(bytes, 1u << 16));
+    if (res < 0) return BSDB_EFILE;
+    void *m = getenv("BSDB_NO_MMAP_WRITE") || res ? MAP_FAILED
+                                                   : mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_SHARED, o->fd, 0);
     if (m != MAP_FAILED) {
         o->map = (uint8_t *)m;
         o->bytes = bytes;
@@ -416,18 +426,27 @@ int builder_finish_locked(bsdb_builder *b, uint32_t width, uint32_t passes, cons
         if (!rc) *out = p;
         return rc;
     };
+    // (every failure from here on goes through done(): the files, their
+    // populators, the device buffers and the MPHF are released)
+#define FIN_OK(x)                                                         \
+    do {                                                                  \
+        const hipError_t e_ = (x);                                        \
+        if (e_ != hipSuccess) return done(hip_fail(e_, #x, __LINE__));    \
+    } while (0)
     // W:124-127: both files created first; index_a.db stays empty in exact mode
     int rc = BSDB_OK;
     if (index_path && ((rc = open_out(index_path, n * 8, &fo)) ||
                        (index_a_path && (rc = open_out(index_a_path, b->approx ? n * 8 : 0, &fao)))))
         return done(rc);
-    pop_o.start(fo.map, fo.bytes);
-    pop_a.start(fao.map, fao.bytes);
+    pop_o.start(fo.map, fo.bytes, fo.fd, 0);
+    pop_a.start(fao.map, fao.bytes, fao.fd, 0);
+    fo.pop = &pop_o;
+    fao.pop = &pop_a;
     if ((rc = mph_alloc(c, n, width, &p))) return done(rc);
     if (n == 0) {  // E = {0}, no values beyond the trailing word (GOV:484)
-        HIP_OK(hipMemsetAsync(p->E, 0, (p->m + 1) * 8, c->stream));
-        HIP_OK(hipMemsetAsync(p->values, 0, p->values_words * 8, c->stream));
-        if (width) HIP_OK(hipMemsetAsync(p->sigbits, 0, p->sig_words * 8, c->stream));
+        FIN_OK(hipMemsetAsync(p->E, 0, (p->m + 1) * 8, c->stream));
+        FIN_OK(hipMemsetAsync(p->values, 0, p->values_words * 8, c->stream));
+        if (width) FIN_OK(hipMemsetAsync(p->sigbits, 0, p->sig_words * 8, c->stream));
         return done(BSDB_OK);
     }
     GovSrc src;
@@ -447,7 +466,7 @@ int builder_finish_locked(bsdb_builder *b, uint32_t width, uint32_t passes, cons
         // where the addresses (and value bytes) are read: HBM if they fit in a
         // quarter of what the keys left free, else host memory
         size_t free_b = 0, total_b = 0;
-        HIP_OK(hipMemGetInfo(&free_b, &total_b));
+        FIN_OK(hipMemGetInfo(&free_b, &total_b));
         const uint64_t rec_bytes = n * ((b->stride ? 0 : 8) + (b->approx ? 9 : 0));
         const bool host_gather = getenv("BSDB_BUILDER_HOST_GATHER") != nullptr || rec_bytes > free_b / 4;
         if (!host_gather) {
@@ -510,6 +529,7 @@ int builder_finish_locked(bsdb_builder *b, uint32_t width, uint32_t passes, cons
     rc = passes_build(c, src, n, width, passes, dev_addr, b->addr_base, b->addr_stride, p->E, p->values, p->sigbits,
                       sink, passes_used, c->stream);
     return done(rc);
+#undef FIN_OK
 }
 
 void builder_release(bsdb_builder *b) {

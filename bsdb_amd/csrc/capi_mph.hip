@@ -333,15 +333,23 @@ int write_files(int device, FILE *const *files, const void *const *d_srcs, int n
         // into a shared mapping do not (capi_builder.hip's OutFile)
         uint8_t *map = nullptr;
         size_t map_len = 0, map_skip = 0;
+        off_t map_base = 0;
+        Populator pop;
         {
             struct stat st;
             if (!getenv("BSDB_NO_MMAP_WRITE") && fstat(fd, &st) == 0 && S_ISREG(st.st_mode)) {
                 const off_t end = base + (off_t)bytes;
-                if (st.st_size >= end || ftruncate(fd, end) == 0) {
+                // (mapped only where the blocks can be reserved ahead of the
+                // stores: Populator / file_reserve; otherwise pwrite, which
+                // reports a full file system instead of raising SIGBUS)
+                const int res = file_reserve(fd, (uint64_t)base, std::min<uint64_t>(bytes, 1u << 16));
+                if (res < 0) return BSDB_EFILE;
+                if (res == 0 && (st.st_size >= end || ftruncate(fd, end) == 0)) {
                     const off_t pg = (off_t)sysconf(_SC_PAGESIZE);
                     const off_t mbase = base / pg * pg;
                     map_skip = (size_t)(base - mbase);
                     map_len = map_skip + (size_t)bytes;
+                    map_base = mbase;
                     void *m = mmap(nullptr, map_len, PROT_READ | PROT_WRITE, MAP_SHARED, fd, mbase);
                     if (m != MAP_FAILED) map = (uint8_t *)m;
                 }
@@ -369,6 +377,11 @@ int write_files(int device, FILE *const *files, const void *const *d_srcs, int n
                 if (!ok) break;
                 const uint64_t len = len_of(j);
                 if (map) {
+                    if (!pop.ensure(map_skip + j * XFER_PIECE, len)) {
+                        rc.store(BSDB_EFILE);
+                        ok = false;
+                        break;
+                    }
                     memcpy(map + map_skip + j * XFER_PIECE, pin[i], len);
                     continue;
                 }
@@ -394,8 +407,7 @@ int write_files(int device, FILE *const *files, const void *const *d_srcs, int n
             }
             if (st) (void)hipStreamDestroy(st);
         };
-        Populator pop;
-        pop.start(map, map_len);
+        pop.start(map, map_len, map ? fd : -1, (uint64_t)map_base);
         std::vector<std::thread> th;
         for (uint64_t t = 1; t < T; ++t) th.emplace_back(work, t);
         work(0);
@@ -495,6 +507,16 @@ int bsdb_mph_build_index_var(bsdb_ctx *c, const uint8_t *h_blob, const uint64_t 
                                  index_path, index_a_path, out, nullptr);
     return mph_build_index(c, n, width, h_addr, h_value8, h_vlen, approximate != 0, index_path, index_a_path, out,
                            [&](uint64_t *d_sig) { return host_hash_var_dev(c, h_blob, h_off, n, 0, d_sig); });
+}
+
+int bsdb_mph_sizes(uint64_t n, uint32_t width, uint64_t *num_buckets, uint64_t *values_words, uint64_t *value_bits,
+                   uint64_t *sig_words) {
+    if (width > 64 || n / BUCKET_SIZE + 1 > 0x7FFFFFFFULL) return BSDB_EINVAL;  // (GOV:348)
+    if (num_buckets) *num_buckets = n / BUCKET_SIZE + 1;
+    if (values_words) *values_words = bsdb_values_words(n);
+    if (value_bits) *value_bits = 2 * (1 + ((n * 281) >> 8));
+    if (sig_words) *sig_words = mph_sig_words(n, width);
+    return BSDB_OK;
 }
 
 int bsdb_mph_info(const bsdb_mph *p, uint64_t *n, uint64_t *m, uint32_t *width, uint64_t *values_words,

@@ -88,6 +88,7 @@ SIGNATURES = [
     ("bsdb_mph_build_index_var", _i, [_vp, _vp, _vp, _u64, _u32, _vp, _vp, _vp, _i, C.c_char_p, C.c_char_p,
                                       C.POINTER(_vp)]),
     ("bsdb_mph_info", _i, [_vp, C.POINTER(_u64), C.POINTER(_u64), C.POINTER(_u32), C.POINTER(_u64), C.POINTER(_u64)]),
+    ("bsdb_mph_sizes", _i, [_u64, _u32, C.POINTER(_u64), C.POINTER(_u64), C.POINTER(_u64), C.POINTER(_u64)]),
     ("bsdb_mph_export", _i, [_vp, _vp, _vp, _vp]),
     ("bsdb_mph_import", _i, [_vp, _u64, _u32, _vp, _vp, _vp, C.POINTER(_vp)]),
     ("bsdb_mph_dump", _i, [_vp, C.c_char_p]),
@@ -158,6 +159,13 @@ def _check(fn: str, rc: int):
 
 def num_buckets(n: int) -> int:
     return int(lib().bsdb_num_buckets(n))
+
+
+def mph_sizes(n: int, width: int) -> dict:
+    """bsdb_mph_sizes: the field sizes of an MPHF on n keys (no device needed)."""
+    m, vw, vb, sw = C.c_uint64(), C.c_uint64(), C.c_uint64(), C.c_uint64()
+    _check("bsdb_mph_sizes", lib().bsdb_mph_sizes(n, width, C.byref(m), C.byref(vw), C.byref(vb), C.byref(sw)))
+    return {"num_buckets": m.value, "values_words": vw.value, "value_bits": vb.value, "sig_words": sw.value}
 
 
 def _ptr(t) -> int:

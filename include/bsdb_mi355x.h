@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define BSDB_ABI_VERSION 4
+#define BSDB_ABI_VERSION 5
 
 /* Return codes (negative errno-style). */
 #define BSDB_OK          0
@@ -372,6 +372,17 @@ int bsdb_mph_build_var(bsdb_ctx *ctx, const uint8_t *h_blob, const uint64_t *h_o
                        bsdb_mph **out);
 int bsdb_mph_info(const bsdb_mph *mph, uint64_t *n, uint64_t *num_buckets, uint32_t *width, uint64_t *values_words,
                   uint64_t *sig_words);
+/* The sizes of an MPHF's fields on n keys with `width` checksum bits, without
+ * a device or a handle (ABI 5; bsdb_mph_info returns the same numbers for a
+ * built MPHF): num_buckets = n/1500 + 1 (GOV:350; E has num_buckets + 1
+ * words, GOV:355); value_bits = 2 (1 + (n 281 >> 8)), the length of GOV's
+ * 2-bit value vector with its trailing 0 (GOV:357,483-485), in values_words
+ * u64 words; sig_words = ceil(n width / 64) + 1 words for the n width-bit
+ * checksums (GOV:494; one zero word of slack), 0 when width == 0.  A JVM
+ * sizes the arrays it exports into and wraps them with these
+ * (LongArrayBitVector.wrap(values, value_bits)). */
+int bsdb_mph_sizes(uint64_t n, uint32_t width, uint64_t *num_buckets, uint64_t *values_words, uint64_t *value_bits,
+                   uint64_t *sig_words);
 int bsdb_mph_export(bsdb_mph *mph, uint64_t *h_E, uint64_t *h_values, uint64_t *h_sigbits);
 int bsdb_mph_import(bsdb_ctx *ctx, uint64_t n, uint32_t width, const uint64_t *h_E, const uint64_t *h_values,
                     const uint64_t *h_sigbits, bsdb_mph **out);

@@ -72,6 +72,10 @@ public final class GpuBuild {
     public static native void builderFree(long b);
     public static native long[] mphInfo(long mph);        // {n, numBuckets, width, valuesWords, sigWords}
     public static native void mphExport(long mph, long outE, long outValues, long outSigBits);
+    // {numBuckets, valuesWords, valueBits, sigWords} of an MPHF on n keys, no handle needed (GOV:350-357,494)
+    public static native long[] mphSizes(long n, int checksumBits);
+    // the export into Java arrays of the mphInfo sizes (sigBits null when checksumBits == 0): GovAssembler
+    public static native void mphExportArrays(long mph, long[] outE, long[] outValues, long[] outSigBits);
     public static native long mphImport(long ctx, long n, int width, long E, long values, long sigBits);
     public static native void mphDump(long mph, String path);
     public static native long mphLoad(long ctx, String path);

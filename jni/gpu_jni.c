@@ -194,6 +194,37 @@ JNIEXPORT jlongArray JF(mphInfo)(JNIEnv *env, jclass c, jlong mph) {
 JNIEXPORT void JF(mphExport)(JNIEnv *env, jclass c, jlong mph, jlong E, jlong values, jlong sig) {
     CHECK(bsdb_mph_export(P(mph), P(E), P(values), P(sig)));
 }
+/* {numBuckets, valuesWords, valueBits, sigWords} of an MPHF on n keys (no handle) */
+JNIEXPORT jlongArray JF(mphSizes)(JNIEnv *env, jclass c, jlong n, jint w) {
+    uint64_t m, vw, vb, sw;
+    int rc = bsdb_mph_sizes((uint64_t)n, (uint32_t)w, &m, &vw, &vb, &sw);
+    if (rc) { fail(env, rc); return NULL; }
+    jlong v[4] = {(jlong)m, (jlong)vw, (jlong)vb, (jlong)sw};
+    jlongArray a = (*env)->NewLongArray(env, 4);
+    (*env)->SetLongArrayRegion(env, a, 0, 4, v);
+    return a;
+}
+/* the export straight into Java long[] arrays (GovAssembler): each array is
+ * held for the copy (GetPrimitiveArrayCritical: no second copy of a multi-GB
+ * array) and released with mode 0 (written back); sig may be null (width 0);
+ * every array must hold the mphInfo sizes (checked) */
+JNIEXPORT void JF(mphExportArrays)(JNIEnv *env, jclass c, jlong mph, jlongArray E, jlongArray values, jlongArray sig) {
+    uint64_t n, m, vw, sw; uint32_t w;
+    int rc = bsdb_mph_info(P(mph), &n, &m, &w, &vw, &sw);
+    if (!rc && (!E || !values || (w && !sig) || (uint64_t)(*env)->GetArrayLength(env, E) < m + 1 ||
+                (uint64_t)(*env)->GetArrayLength(env, values) < vw ||
+                (w && (uint64_t)(*env)->GetArrayLength(env, sig) < sw)))
+        rc = BSDB_EINVAL;
+    if (rc) { fail(env, rc); return; }
+    void *pe = (*env)->GetPrimitiveArrayCritical(env, E, NULL);
+    void *pv = (*env)->GetPrimitiveArrayCritical(env, values, NULL);
+    void *ps = w ? (*env)->GetPrimitiveArrayCritical(env, sig, NULL) : NULL;
+    rc = (!pe || !pv || (w && !ps)) ? BSDB_ENOMEM : bsdb_mph_export(P(mph), pe, pv, ps);
+    if (ps) (*env)->ReleasePrimitiveArrayCritical(env, sig, ps, 0);
+    if (pv) (*env)->ReleasePrimitiveArrayCritical(env, values, pv, 0);
+    if (pe) (*env)->ReleasePrimitiveArrayCritical(env, E, pe, 0);
+    if (rc) fail(env, rc);
+}
 JNIEXPORT jlong JF(mphImport)(JNIEnv *env, jclass c, jlong ctx, jlong n, jint w, jlong E, jlong values, jlong sig) {
     bsdb_mph *m = NULL; CHECK(bsdb_mph_import(P(ctx), (uint64_t)n, (uint32_t)w, P(E), P(values), P(sig), &m));
     return (jlong)(intptr_t)m;

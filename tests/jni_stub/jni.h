@@ -32,6 +32,8 @@ struct JNINativeInterface_ {
     void (*SetLongArrayRegion)(const struct JNINativeInterface_ **, jlongArray, jsize, jsize, const jlong *);
     const char *(*GetStringUTFChars)(const struct JNINativeInterface_ **, jstring, jboolean *);
     void (*ReleaseStringUTFChars)(const struct JNINativeInterface_ **, jstring, const char *);
+    void *(*GetPrimitiveArrayCritical)(const struct JNINativeInterface_ **, jarray, jboolean *);
+    void (*ReleasePrimitiveArrayCritical)(const struct JNINativeInterface_ **, jarray, void *, jint);
 };
 typedef const struct JNINativeInterface_ *JNIEnv;
 #endif

@@ -47,7 +47,7 @@ def test_host_only_calls(lib):
     lib.bsdb_num_buckets.argtypes = [C.c_uint64]
     assert lib.bsdb_num_buckets(13_193_787_549) == 8_795_859
     assert lib.bsdb_num_buckets(0) == 1
-    assert lib.bsdb_abi_version() == 4
+    assert lib.bsdb_abi_version() == 5
     hdr = open(os.path.join(ROOT, "include", "bsdb_mi355x.h")).read()
     assert f"#define BSDB_ABI_VERSION {lib.bsdb_abi_version()}" in hdr
 
@@ -55,6 +55,39 @@ def test_host_only_calls(lib):
     assert lib.bsdb_strerror(-17) == b"duplicate key signature"
     lib.bsdb_open.argtypes = [C.c_int, C.POINTER(C.c_void_p)]
     assert lib.bsdb_open(0, None) == -22
+
+
+@pytest.mark.parametrize("n", [0, 1, 1_499, 1_500, 1_000_000, 13_193_787_549])
+@pytest.mark.parametrize("width", [0, 4, 16, 64])
+def test_mph_sizes_equal_gov_field_arithmetic(n, width):
+    """the sizes a JVM allocates for the export (and that
+    bsdb_mph_info reports for a built MPHF) are GOV's own field arithmetic:
+    numBuckets = n/1500 + 1 (GOV:350) with edgeOffsetAndSeed of numBuckets + 1
+    longs (GOV:355); the 2-bit value vector holds one value per vertex,
+    vertexOffset(n) = n*C_TIMES_256 >> 8 with C_TIMES_256 = floor(1.10*256) =
+    281 (GOV:160-162,315-317), plus the trailing 0 of values.add(0) (GOV:484);
+    the checksums are n width-bit entries (GOV:493-494)."""
+    from bsdb_amd.native import mph_sizes
+    s = mph_sizes(n, width)
+    C_TIMES_256 = int(1.10 * 256)
+    assert C_TIMES_256 == 281
+    buckets = n // 1500 + 1
+    vertices = n * C_TIMES_256 >> 8
+    value_bits = 2 * (vertices + 1)
+    assert s["num_buckets"] == buckets
+    assert s["value_bits"] == value_bits
+    assert s["values_words"] == -(-value_bits // 64)
+    assert s["sig_words"] == (0 if width == 0 else -(-(n * width) // 64) + 1)  # (+1: a zero word of slack)
+    if n == 13_193_787_549:
+        assert buckets == 8_795_859  # SURVEY.md §8 C4
+
+
+def test_mph_sizes_rejects_what_gov_rejects():
+    from bsdb_amd.native import BsdbError, mph_sizes
+    with pytest.raises(BsdbError):
+        mph_sizes(10, 65)
+    with pytest.raises(BsdbError):  # GOV:348: at most (2^31 - 2) * 1500 - 1 keys
+        mph_sizes((0x7FFFFFFF) * 1500, 4)
 
 
 def test_var_host_argument_checks():

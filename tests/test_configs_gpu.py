@@ -191,6 +191,161 @@ def test_c5_checksum16_build_on_a_sample(ctx):
     np.testing.assert_array_equal(u64(sb)[: osb.size], osb)
 
 
+def solver_report(name, n, E, extra=None):
+    """What the solve went through on a key set: seeds per
+    bucket (E's top byte, GOV:434-436) and the oversized buckets that take
+    k_gov_solve_mid (> 1 664 keys) or the global-slab solver (> 2 048).  With
+    BSDB_TEST_REPORT=<file> it is appended there as one JSON line."""
+    import json
+    seeds = (E[:-1] >> np.uint64(56)).astype(np.int64)
+    size = np.diff((E & np.uint64((1 << 56) - 1)).astype(np.int64))
+    rep = {"test": name, "n": int(n), "buckets": int(size.size),
+           "buckets_seed_ge1": int((seeds >= 1).sum()), "buckets_seed_ge2": int((seeds >= 2).sum()),
+           "buckets_seed_ge4": int((seeds >= 4).sum()), "max_seed": int(seeds.max()),
+           "mean_attempts": float(seeds.mean() + 1), "max_bucket": int(size.max()),
+           "buckets_mid_solver": int(((size > 1664) & (size <= 2048)).sum()),
+           "buckets_global_slab": int((size > 2048).sum())}
+    rep.update(extra or {})
+    print(rep)
+    path = os.environ.get("BSDB_TEST_REPORT")
+    if path:
+        with open(path, "a") as f:
+            f.write(json.dumps(rep) + "\n")
+    return rep
+
+
+def gov_profile_counts(text):
+    """The counters of the last `[gov-profile] m=...` line (BSDB_GOV_PROFILE)."""
+    lines = [ln for ln in text.splitlines() if ln.startswith("[gov-profile] m=")]
+    out = {}
+    for tok in (lines[-1].split() if lines else []):
+        if "=" in tok:
+            k, v = tok.split("=", 1)
+            try:
+                out[k] = float(v)
+            except ValueError:
+                pass
+    return out
+
+
+@pytest.mark.timeout(900)
+def test_c2_passes_build_equals_oracle_field_for_field(ctx, capfd):
+    """the production solver pinned at C2's size.  1e8
+    13-byte keys, cb = 4, built by the bucket-range pass path (3 passes, the
+    C4 form) and compared FIELD FOR FIELD with the oracle's independent build
+    (bo_gov_build_mt, oracle/bsdb_oracle.c): every E word (offsets + local
+    seeds, GOV:385-436), every 2-bit value word (GOV:438-442,483-485), every
+    checksum word (GOV:492-508), and every index.db slot against W:129-145
+    (slot = getLong(key), byte-reversed address).  At 1e8 keys the rare paths
+    fire naturally: buckets over 1 664 keys (k_gov_solve_mid), high seeds, the
+    FVS blocks; the report counts them, and a second build through the
+    profiling solver instance must give the same structure."""
+    n, width, passes, base, stride = 100_000_000, 4, 3, 0x1000, 48
+    keys = O.gen_keys13_mt(0, n, THREADS)
+
+    def oracle():
+        sig = O.hash_fixed_mt(keys, 13, THREADS)
+        O.solve_stats(True)
+        rc, E, vals, sb, dt = O.gov_build_mt(sig, width, THREADS)
+        st = O.solve_stats(True)
+        ranks = O.lookup_batch_mt(sig, n, E, vals, width, sb, True, THREADS) if rc == 0 else None
+        return rc, E, vals, sb, dt, st, ranks
+
+    th, box = in_background(oracle)
+    dk = torch.from_numpy(keys).cuda()
+    d_index = torch.zeros(n, dtype=torch.int64, device="cuda")
+    E, vals, sb, used = ctx.mph_build_index_passes(dk, 13, n, width, passes, addr_base=base, addr_stride=stride,
+                                                   index=d_index)
+    torch.cuda.synchronize()
+    assert used == passes
+    hE, hv, hs, hidx = u64(E), u64(vals), u64(sb), u64(d_index)
+    del E, vals, sb, d_index
+    # the same build through the profiling instance of the solver, its counters
+    os.environ["BSDB_GOV_PROFILE"] = "1"
+    try:
+        capfd.readouterr()
+        E2, v2, s2, _ = ctx.mph_build_index_passes(dk, 13, n, width, passes)
+        torch.cuda.synchronize()
+        prof_text = capfd.readouterr().err
+    finally:
+        del os.environ["BSDB_GOV_PROFILE"]
+    np.testing.assert_array_equal(u64(E2), hE)
+    np.testing.assert_array_equal(u64(v2), hv)
+    np.testing.assert_array_equal(u64(s2), hs)
+    del E2, v2, s2, dk
+    torch.cuda.empty_cache()
+    th.join()
+    rc, oE, ov, osb, dt, st, ranks = box["r"]
+    assert rc == 0
+    np.testing.assert_array_equal(hE, oE)                 # offsets + every bucket's seed
+    np.testing.assert_array_equal(hv, ov)                 # every 2-bit value word
+    np.testing.assert_array_equal(hs[: osb.size], osb)    # every checksum word
+    assert ranks.min() >= 0 and np.array_equal(np.bincount(ranks, minlength=n), np.ones(n, np.int64))
+    exp = np.zeros(n, np.uint64)
+    exp[ranks] = (np.uint64(base) + np.uint64(stride) * np.arange(n, dtype=np.uint64)).byteswap()
+    np.testing.assert_array_equal(hidx, exp)              # index.db slots (W:129-145)
+    # the last profile line is the last pass's; the passes together:
+    lines = [ln for ln in prof_text.splitlines() if ln.startswith("[gov-profile] m=")]
+    tot = {}
+    for ln in lines:
+        for k, v in gov_profile_counts(ln).items():
+            if k.startswith("n_"):
+                tot[k] = tot.get(k, 0) + v
+    rep = solver_report("c2_passes_1e8", n, hE, {
+        "oracle_seconds": dt, "oracle_attempts": st["attempts"], "oracle_unorientable": st["unorientable"],
+        "oracle_inconsistent": st["inconsistent"], "oracle_degenerate": st["degenerate"],
+        "oracle_singular_solved": st["singular_solved"], "profile_passes": len(lines),
+        **{"device_" + k: int(v) for k, v in tot.items() if k in (
+            "n_seeds", "n_fvs_blocks", "n_singular_solved", "n_null_vectors", "n_speculative_lost",
+            "n_fail_degenerate", "n_fail_orient", "n_fail_inconsistent", "n_small_scc_fallbacks",
+            "n_rows_in_blocks_over_440", "n_heavy")}})
+    assert len(lines) == passes
+    # the rare paths did fire at this size
+    assert rep["buckets_seed_ge4"] > 0
+    assert rep["buckets_mid_solver"] >= 1  # (this key set's largest bucket: 1 669 keys)
+
+
+@pytest.mark.timeout(900)
+def test_c3_approx_host_passes_equals_oracle_on_a_2e8_slice(ctx, tmp_path):
+    """VERDICT r4 item 1, C3's mode: index.approximate = true from host
+    buffers through the streaming builder's bucket-range passes (4 passes),
+    on the first 2e8 C3 keys.  The MPHF equals the oracle's build field for
+    field, index.db and index_a.db equal the W:129-145 restatement (slot =
+    getLong(key): byte-reversed address, and the value's first 8 bytes) byte
+    for byte."""
+    n, width, passes = 200_000_000, 4, 4
+    keys = O.gen_keys13_mt(0, n, THREADS)
+
+    def oracle():
+        sig = O.hash_fixed_mt(keys, 13, THREADS)
+        rc, E, vals, sb, dt = O.gov_build_mt(sig, width, THREADS)
+        ranks = O.lookup_batch_mt(sig, n, E, vals, width, sb, True, THREADS) if rc == 0 else None
+        return rc, E, vals, sb, ranks
+
+    th, box = in_background(oracle)
+    addr, value8, vlen = records(0, n)
+    d = big_tmp(tmp_path, 16 * n)
+    ip, ap = os.path.join(d, "index.db"), os.path.join(d, "index_a.db")
+    mph, used = ctx.mph_build_index_passes_host(keys, 13, width, ip, addr_np=addr, value8_np=value8, vlen_np=vlen,
+                                                approximate=True, index_a_path=ap, passes=passes)
+    assert used == passes
+    dE, dv, ds = mph.export()
+    mph.close()
+    th.join()
+    rc, E, vals, sb, ranks = box["r"]
+    assert rc == 0
+    np.testing.assert_array_equal(dE, E)
+    np.testing.assert_array_equal(dv, vals)
+    np.testing.assert_array_equal(ds[: sb.size], sb)
+    exp = np.zeros(n, ">u8")
+    exp[ranks] = addr
+    assert np.array_equal(np.fromfile(ip, ">u8"), exp)
+    expa = np.zeros(n, "<u8")
+    expa[ranks] = value8
+    assert np.array_equal(np.fromfile(ap, "<u8"), expa)
+    solver_report("c3_approx_host_passes_2e8", n, dE)
+
+
 def big_tmp(tmp_path, need_bytes):
     """A directory with room for the index files: the candidate with the most
     free space among pytest's tmp, /dev/shm, /tmp and the tree's build/.  A box

@@ -125,29 +125,83 @@ def test_strings_go_through_the_null_safe_helpers():
 
 # classes of the JDK (java.lang is implicit) and of the reference the Java class may use
 _JAVA_LANG = {"String", "System", "Object", "Override", "Exception", "RuntimeException", "Integer", "Long", "Boolean",
-              "Math", "Thread", "Class", "Deprecated", "SuppressWarnings", "IllegalArgumentException"}
+              "Math", "Thread", "Class", "Deprecated", "SuppressWarnings", "IllegalArgumentException", "ThreadLocal",
+              "ReflectiveOperationException", "InterruptedException", "IllegalStateException"}
+REF_JAVA = "/root/reference/src/main/java"
+# classes of a file's own package that live in the reference tree (no import needed)
+_SAME_PACKAGE = {"tech.bsdb.write": {"KVWriter", "SimpleCompactKVWriter", "SimpleBlockedKVWriter", "KVWriterCompressed",
+                                     "PartitionedKVWriter", "BlockedKVWriter", "BSDBWriter"},
+                 "tech.bsdb.gpu": {"GpuBuild", "GovAssembler"}}
+JAVA_FILES = ["GpuBuild.java", "GovAssembler.java", "GpuBSDBWriter.java"]
 
 
-def test_java_class_resolves_every_simple_name():
+@pytest.mark.parametrize("name", JAVA_FILES)
+def test_java_class_resolves_every_simple_name(name):
     """GpuBuild.java used NativeUtils (tech.bsdb.io,
     src/main/java/tech/bsdb/io/NativeUtils.java) without importing it.  Every
-    capitalised simple name in the class must be java.lang, imported, or the
-    class itself (javac is not in this image: this is the check that stands in
-    for it)."""
-    src = _strip_comments(open(JAVA).read())
+    capitalised simple name in each committed Java class (the natives class,
+    the GOV assembler and the BSDBWriter drop-in) must be
+    java.lang, imported, the class itself, or a class of its own package;
+    ALL_CAPS names need a static wildcard import (tech.bsdb.util.Common.*).
+    javac is not in this image: this is the check that stands in for it.  Where
+    the reference tree is present (this container), every import of a
+    tech.bsdb / it.unimi.dsi.sux4j class and every same-package class names a
+    file of the reference."""
+    src = _strip_comments(open(os.path.join(ROOT, "jni", name)).read())
     src_nostr = re.sub(r'"[^"\n]*"', '""', src)
     pkg = re.search(r"^package\s+([\w.]+);", src_nostr, re.M).group(1)
-    imported = {m.group(1).split(".")[-1] for m in re.finditer(r"^import\s+([\w.]+);", src_nostr, re.M)}
+    imports = [m.group(1) for m in re.finditer(r"^import\s+([\w.]+);", src_nostr, re.M)]
+    statics = [m.group(1) for m in re.finditer(r"^import\s+static\s+([\w.]+)\.\*;", src_nostr, re.M)]
+    imported = {i.split(".")[-1] for i in imports}
     own = set(re.findall(r"\b(?:class|interface|enum)\s+(\w+)", src_nostr))
     body = re.sub(r"^(package|import)\s+[^;]+;", "", src_nostr, flags=re.M)
     used = set(re.findall(r"\b([A-Z]\w*)\b(?=\s*[.(\[<\w])", body)) | set(re.findall(r"\bnew\s+([A-Z]\w*)", body))
+    used |= set(re.findall(r"\(\(?([A-Z]\w*)\)", body))  # casts
     used -= {"JNI"}
-    missing = {u for u in used if u not in _JAVA_LANG and u not in imported and u not in own}
+    # variables and parameters with capitalised names (long[] E)
+    used -= set(re.findall(r"\b(?:long|int|byte|boolean|short|char|double|float)(?:\[\])+\s+([A-Z]\w*)\s*(?=[=;,)])", body))
+    consts = {u for u in used if re.fullmatch(r"[A-Z][A-Z0-9_]+", u)}
+    local_consts = set(re.findall(r"\bstatic\s+final\s+\w+\s+([A-Z][A-Z0-9_]+)", body)) | \
+        set(re.findall(r",\s*([A-Z][A-Z0-9_]+)\s*=", body))
+    same = _SAME_PACKAGE.get(pkg, set())
+    missing = {u for u in used - consts if u not in _JAVA_LANG and u not in imported and u not in own and u not in same}
     assert not missing, f"{pkg}: unresolved simple names {sorted(missing)}"
-    assert "NativeUtils" in imported
-    ref = "/root/reference/src/main/java/tech/bsdb/io/NativeUtils.java"
-    if os.path.exists(ref):  # (this container only) the import names the reference's own class
-        assert "package tech.bsdb.io;" in open(ref).read()
+    assert not (consts - local_consts) or statics, f"constants {sorted(consts - local_consts)} without a static import"
+    if name == "GpuBuild.java":
+        assert "NativeUtils" in imported
+    if os.path.isdir(REF_JAVA):  # (this container only) the names are the reference's own classes
+        for imp in imports + statics:
+            if imp.startswith(("tech.bsdb.", "it.unimi.dsi.sux4j.")) and not imp.startswith("tech.bsdb.gpu."):
+                assert os.path.exists(os.path.join(REF_JAVA, *imp.split(".")) + ".java"), imp
+        for cls in same & (used | set(re.findall(r"\b([A-Z]\w*)\b", body))):
+            if pkg != "tech.bsdb.gpu":
+                assert os.path.exists(os.path.join(REF_JAVA, *pkg.split("."), cls + ".java")), cls
+
+
+def test_writer_drop_in_keeps_the_reference_api():
+    """GpuBSDBWriter has BSDBWriter's public constructor and
+    methods with the same parameter types (W:39,67,71,75,91,99,107) and reads
+    only package fields that exist in the reference's writers."""
+    src = _strip_comments(open(os.path.join(ROOT, "jni", "GpuBSDBWriter.java")).read())
+    sig = lambda s: re.sub(r"\s+", " ", s).strip()
+    want = ["public GpuBSDBWriter(File basePath, File tmpDir, int checksumBits, long passCacheSize, boolean compact, "
+            "boolean compress, int compressBlockSize, int sharedDictSize, boolean approximateMode) throws Exception",
+            "public void sample(byte[] key, byte[] value)", "public void onSampleFinished()",
+            "public void put(byte[] key, byte[] value) throws IOException, InterruptedException",
+            "public void build() throws IOException, InterruptedException",
+            "public GOVMinimalPerfectHashFunctionModified<byte[]> buildHash() throws IOException",
+            "public void buildIndex(GOVMinimalPerfectHashFunctionModified<byte[]> hashFunction) throws IOException, "
+            "InterruptedException"]
+    flat = sig(src)
+    for w in want:
+        assert sig(w) in flat, w
+    ref = os.path.join(REF_JAVA, "tech", "bsdb", "write")
+    if os.path.isdir(ref):  # the package-private fields it reads, and the reference's own API
+        assert re.search(r"\bfinal int partitions;", open(os.path.join(ref, "PartitionedKVWriter.java")).read())
+        assert re.search(r"\bfinal int blockSize;", open(os.path.join(ref, "BlockedKVWriter.java")).read())
+        rsrc = sig(_strip_comments(open(os.path.join(ref, "BSDBWriter.java")).read()))
+        for w in want[1:]:
+            assert sig(w) in rsrc, w
 
 
 @pytest.mark.skipif(shutil.which("gcc") is None, reason="no gcc")
