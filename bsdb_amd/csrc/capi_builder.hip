@@ -90,10 +90,34 @@ struct bsdb_builder {
     bool borrowed_records = false;  // one-call forms: the caller's record arrays cover every key
     int failed = BSDB_OK;  // an add that failed part-way leaves the builder unusable
     bool finished = false;
-    std::mutex mu;  // one add (or the finish) at a time: adds may come from several threads
+    // Adds may come from several threads (put() threads, the kv.db scan
+    // threads).  mu is held only to RESERVE an add's ranges (its keys' index
+    // range and key bytes, room in the key area and the record arrays); the
+    // copies into those ranges then run outside it, concurrently, each
+    // holding grow_mu shared.  A growth of the key area or of the record
+    // arrays (which may move them) takes grow_mu exclusively, so it waits for
+    // the copies in flight.  Lock order: mu, then grow_mu, then the context's.
+    std::mutex mu;
+    std::shared_mutex grow_mu;
     // the record arrays' pages, populated in the background from the open
     // (first-touch faults of ~2 µs a page were most of an add's time)
     Populator pop_addr, pop_v8;
+    // Spill mode: keys beyond the device's key area.  The
+    // reference bounds a README-size build by spilling every key's signature
+    // (sig0, sig1, record rank: 24 B, CBHS:379-395) to one of 256 segment
+    // files by sig0's top byte and solving segment by segment (CBHS:852-978).
+    // When an add does not fit the device key area (dev_key_cap, or an HBM
+    // allocation fails), the resident keys are hashed on the device and moved
+    // the same way into 256 host segments of (sig0, sig1) + add position, the
+    // key area is released, and every later add is hashed on the device and
+    // appended there; the finish uploads each pass's segments (section
+    // "spill" below).
+    bool spill = false;
+    uint64_t dev_key_cap = ~0ull;  // key-area bytes (BSDB_BUILDER_DEVICE_KEY_BYTES: a test knob)
+    HostVec<ulonglong2> seg_sig[256];
+    HostVec<uint64_t> seg_pos[256];
+    void *d_stage = nullptr;       // spill adds: the batch's keys, offsets, signatures, segment order
+    size_t stage_cap = 0;
     void stop_prefault() {
         pop_addr.finish();
         pop_v8.finish();
@@ -134,10 +158,10 @@ __global__ __launch_bounds__(256) void k_fill_offsets(uint64_t *off, uint64_t co
 // Device buffer that keeps its first `used` bytes when it grows (a new
 // allocation + a device copy; the add batches normally fit the capacity the
 // builder was opened with).
-int dev_reserve(bsdb_ctx *c, void **p, size_t *cap, size_t used, size_t need) {
+int dev_reserve(bsdb_ctx *c, void **p, size_t *cap, size_t used, size_t need, size_t limit = ~(size_t)0) {
     if (need <= *cap) return BSDB_OK;
     void *q = nullptr;
-    size_t nc = std::max(need, *cap + *cap / 2);
+    size_t nc = std::max(need, std::min(limit, *cap + *cap / 2));
     if (dmalloc(&q, nc) != hipSuccess) {
         nc = need;
         if (dmalloc(&q, nc) != hipSuccess) return BSDB_ENOMEM;
@@ -267,37 +291,6 @@ int builder_check_records(const bsdb_builder *b, uint64_t count, const uint64_t 
     return BSDB_OK;
 }
 
-int builder_add_records(bsdb_builder *b, uint64_t count, const uint64_t *h_addr, const uint64_t *h_value8,
-                        const uint8_t *h_vlen) {
-    if (b->borrowed_records) return BSDB_OK;
-    if ((!b->stride && b->addr.n + count > b->addr.cap) || (b->approx && b->value8.n + count > b->value8.cap))
-        b->stop_prefault();  // (a growing array may move)
-    if (!b->stride && !b->addr.append(h_addr, count)) return BSDB_ENOMEM;
-    if (b->approx && (!b->value8.append(h_value8, count) || !b->vlen.append(h_vlen, count))) return BSDB_ENOMEM;
-    return BSDB_OK;
-}
-
-// one add of fixed-length keys (caller holds the context lock, device set)
-int builder_add_fixed_locked(bsdb_builder *b, const uint8_t *h_keys, uint32_t key_len, uint64_t count) {
-    bsdb_ctx *c = b->c;
-    const uint64_t bytes = (uint64_t)key_len * count;
-    int rc = dev_reserve(c, (void **)&b->d_keys, &b->keys_cap, b->key_bytes, b->key_bytes + bytes + 16);
-    if (rc) return rc;
-    if (bytes) HIP_OK(hipMemcpyAsync(b->d_keys + b->key_bytes, h_keys, bytes, hipMemcpyHostToDevice, c->stream));
-    if (!b->key_len) {  // a variable-length builder: offsets key_bytes + (i + 1) L
-        if ((rc = dev_reserve(c, (void **)&b->d_off, &b->off_cap, (b->n + 1) * 8, (b->n + count + 1) * 8))) return rc;
-        if (count)
-            k_fill_offsets<<<grid_for(c, count), 256, 0, c->stream>>>(b->d_off + b->n + 1, count, b->key_bytes,
-                                                                      key_len);
-        if (b->n == 0) b->uni_len = key_len;
-        b->uniform = b->uniform && key_len == b->uni_len;
-    }
-    HIP_OK(hipStreamSynchronize(c->stream));  // the caller may reuse its buffers
-    if ((rc = launch_status())) return rc;
-    b->key_bytes += bytes;
-    return BSDB_OK;
-}
-
 // The lengths of a batch of variable-length keys: checked non-decreasing,
 // and whether they all equal one length (*len, or 0xFFFFFFFF when they
 // differ).  No builder state: callers may run it outside the lock.
@@ -319,55 +312,339 @@ __global__ __launch_bounds__(256) void k_rebase_offsets(uint64_t *off, uint64_t 
     for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < count; i += step) off[i] += shift;
 }
 
-// one add of variable-length keys whose lengths var_batch_lengths has
-// checked (uni: their common length or 0xFFFFFFFF)
-int builder_add_var_locked(bsdb_builder *b, const uint8_t *h_blob, const uint64_t *h_off, uint64_t count,
-                           uint32_t uni) {
-    bsdb_ctx *c = b->c;
-    if (count == 0) return BSDB_OK;
-    const uint64_t o0 = h_off[0], bytes = h_off[count] - o0;
-    int rc = dev_reserve(c, (void **)&b->d_keys, &b->keys_cap, b->key_bytes, b->key_bytes + bytes + 16);
-    if (rc) return rc;
-    if ((rc = dev_reserve(c, (void **)&b->d_off, &b->off_cap, (b->n + 1) * 8, (b->n + count + 1) * 8))) return rc;
-    if (bytes) HIP_OK(hipMemcpyAsync(b->d_keys + b->key_bytes, h_blob + o0, bytes, hipMemcpyHostToDevice, c->stream));
-    uint64_t *dst = b->d_off + b->n + 1;
-    if (uni != 0xFFFFFFFFu) {
-        // one length (a kv.db partition of fixed-size keys): the offsets are
-        // a formula, written on the device instead of copied
-        k_fill_offsets<<<grid_for(c, count), 256, 0, c->stream>>>(dst, count, b->key_bytes, uni);
-    } else {
-        HIP_OK(hipMemcpyAsync(dst, h_off + 1, count * 8, hipMemcpyHostToDevice, c->stream));
-        k_rebase_offsets<<<grid_for(c, count), 256, 0, c->stream>>>(dst, count, b->key_bytes - o0);
+// One batch of an add: fixed-length keys (keys, key_len) or variable-length
+// ones (the blob indexed by off[0..count], lengths checked by
+// var_batch_lengths; uni = their common length or 0xFFFFFFFF).
+struct AddBatch {
+    const uint8_t *keys = nullptr;
+    const uint64_t *off = nullptr;
+    uint32_t key_len = 0;
+    uint32_t uni = 0xFFFFFFFFu;
+    uint64_t count = 0;
+    uint64_t o0() const { return off ? off[0] : 0; }
+    uint64_t bytes() const { return off ? off[count] - off[0] : (uint64_t)key_len * count; }
+    const uint8_t *first() const { return keys + o0(); }
+};
+
+// ---- spill mode (keys beyond the device's key area) -------------------------
+// 256 segments by sig0's top byte, as CBHS:379-395 (sig0 >>> 56); a key's
+// entry is its (sig0, sig1) and its add position (its record's rank in the
+// add order, CBHS:386-388's "data" word).
+constexpr uint32_t NSEG = 256;
+constexpr uint64_t SEG_CHUNK = 256 * 16;  // keys a workgroup places per round
+
+__global__ __launch_bounds__(256) void k_seg_count(const ulonglong2 *sig, uint64_t n, uint32_t *counts) {
+    __shared__ uint32_t c[NSEG];
+    c[threadIdx.x] = 0;
+    __syncthreads();
+    const uint64_t step = (uint64_t)gridDim.x * 256;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += step) atomicAdd(&c[sig[i].x >> 56], 1u);
+    __syncthreads();
+    if (c[threadIdx.x]) atomicAdd(counts + threadIdx.x, c[threadIdx.x]);
+}
+
+// entries grouped by segment: per round a workgroup ranks its SEG_CHUNK keys
+// in LDS and reserves one run per segment (one cursor atomic each); the order
+// inside a segment is arbitrary (the solve sorts each bucket, CBHS:939-955)
+__global__ __launch_bounds__(256) void k_seg_scatter(const ulonglong2 *sig, uint64_t n, uint64_t pos0,
+                                                     unsigned long long *cursor, ulonglong2 *out_sig, uint64_t *out_pos) {
+    __shared__ uint32_t c[NSEG];
+    __shared__ unsigned long long base[NSEG];
+    for (uint64_t lo = (uint64_t)blockIdx.x * SEG_CHUNK; lo < n; lo += (uint64_t)gridDim.x * SEG_CHUNK) {
+        c[threadIdx.x] = 0;
+        __syncthreads();
+        uint32_t seg[16], rank[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const uint64_t i = lo + (uint64_t)j * 256 + threadIdx.x;
+            seg[j] = i < n ? (uint32_t)(sig[i].x >> 56) : 0;
+            rank[j] = i < n ? atomicAdd(&c[seg[j]], 1u) : 0;
+        }
+        __syncthreads();
+        if (c[threadIdx.x]) base[threadIdx.x] = atomicAdd(cursor + threadIdx.x, (unsigned long long)c[threadIdx.x]);
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const uint64_t i = lo + (uint64_t)j * 256 + threadIdx.x;
+            if (i < n) {
+                const uint64_t p = base[seg[j]] + rank[j];
+                out_sig[p] = sig[i];
+                out_pos[p] = pos0 + i;
+            }
+        }
+        __syncthreads();
     }
-    HIP_OK(hipStreamSynchronize(c->stream));  // the caller may reuse its buffers
-    if ((rc = launch_status())) return rc;
-    if (b->n == 0) b->uni_len = uni;
-    b->uniform = b->uniform && uni != 0xFFFFFFFFu && uni == b->uni_len;
-    b->key_bytes += bytes;
+}
+
+// the keys of buckets [b_lo, b_hi) among uploaded segment entries (a segment
+// at either end of the range also holds keys of the neighbouring buckets)
+__global__ __launch_bounds__(256) void k_range_compact(const ulonglong2 *in, const uint64_t *in_pos, uint64_t n,
+                                                       uint32_t mult, uint32_t b_lo, uint32_t b_hi, ulonglong2 *out,
+                                                       uint64_t *out_pos, unsigned long long *count) {
+    const uint32_t lane = threadIdx.x & 63;
+    for (uint64_t i0 = (uint64_t)blockIdx.x * 256; i0 < n; i0 += (uint64_t)gridDim.x * 256) {
+        const uint64_t i = i0 + threadIdx.x;
+        bool keep = false;
+        ulonglong2 s{0, 0};
+        if (i < n) {
+            s = in[i];
+            const uint32_t b = bucket_of_w(w64(s.x), mult);
+            keep = b >= b_lo && b < b_hi;
+        }
+        const uint64_t bal = __builtin_amdgcn_ballot_w64(keep);
+        if (!bal) continue;
+        unsigned long long base = 0;
+        if (lane == 0) base = atomicAdd(count, (unsigned long long)__builtin_popcountll(bal));
+        const uint32_t lo32 = (uint32_t)__shfl((int)(uint32_t)base, 0, 64);
+        const uint32_t hi32 = (uint32_t)__shfl((int)(uint32_t)(base >> 32), 0, 64);
+        if (keep) {
+            const uint64_t p = (((uint64_t)hi32 << 32) | lo32) + (uint64_t)__builtin_popcountll(bal & ((1ULL << lane) - 1));
+            out[p] = s;
+            out_pos[p] = in_pos[i];
+        }
+    }
+}
+
+// Device scratch of the spill path (grown, kept until the builder is released).
+int stage_reserve(bsdb_builder *b, size_t bytes) {
+    if (bytes <= b->stage_cap) return BSDB_OK;
+    (void)hipFree(b->d_stage);
+    b->d_stage = nullptr;
+    b->stage_cap = 0;
+    if (dmalloc(&b->d_stage, bytes) != hipSuccess) return BSDB_ENOMEM;
+    b->stage_cap = bytes;
     return BSDB_OK;
 }
 
-// Runs an add under the context lock; a failure marks the builder failed.
-template <class Add>
-int builder_add(bsdb_builder *b, uint64_t count, const uint64_t *h_addr, const uint64_t *h_value8,
-                const uint8_t *h_vlen, Add &&add) {
-    std::lock_guard<std::mutex> gb(b->mu);
-    if (b->failed) return b->failed;
-    if (b->finished) return BSDB_EINVAL;
-    int rc = builder_check_records(b, count, h_addr, h_value8, h_vlen);
-    if (rc) return rc;
-    if (count == 0) return BSDB_OK;
+// count device signatures (at the stage's front) with add positions pos0..:
+// grouped by segment on the device, then appended to the host segments
+// (caller holds the builder and context locks, device set)
+int spill_segments(bsdb_builder *b, const ulonglong2 *d_sig, uint64_t count, uint64_t pos0, uint8_t *scr, hipStream_t s) {
     bsdb_ctx *c = b->c;
-    {
-        std::lock_guard<std::mutex> g(c->mu);
-        if (hipSetDevice(c->device) != hipSuccess) return b->failed = BSDB_EIO;
-        Ordered ord(c, c->stream);
-        rc = add();
+    uint32_t *d_cnt = (uint32_t *)scr;
+    unsigned long long *d_cur = (unsigned long long *)(scr + 1024);
+    ulonglong2 *o_sig = (ulonglong2 *)(scr + 1024 + 2048);
+    uint64_t *o_pos = (uint64_t *)(o_sig + count);
+    HIP_OK(hipMemsetAsync(d_cnt, 0, NSEG * 4, s));
+    const uint32_t g = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((count + SEG_CHUNK - 1) / SEG_CHUNK, (uint64_t)c->num_cus * 4));
+    k_seg_count<<<g, 256, 0, s>>>(d_sig, count, d_cnt);
+    uint32_t cnt[NSEG];
+    unsigned long long base[NSEG];
+    HIP_OK(hipMemcpyAsync(cnt, d_cnt, sizeof(cnt), hipMemcpyDeviceToHost, s));
+    HIP_OK(hipStreamSynchronize(s));
+    unsigned long long run = 0;
+    for (uint32_t k = 0; k < NSEG; ++k) {
+        base[k] = run;
+        run += cnt[k];
     }
-    if (!rc) rc = builder_add_records(b, count, h_addr, h_value8, h_vlen);
-    if (rc) return b->failed = rc;
-    b->n += count;
+    if (run != count) return BSDB_EIO;
+    HIP_OK(hipMemcpyAsync(d_cur, base, sizeof(base), hipMemcpyHostToDevice, s));
+    k_seg_scatter<<<g, 256, 0, s>>>(d_sig, count, pos0, d_cur, o_sig, o_pos);
+    int rc = launch_status();
+    if (rc) return rc;
+    HIP_OK(hipStreamSynchronize(s));
+    for (uint32_t k = 0; k < NSEG; ++k) {
+        if (!cnt[k]) continue;
+        HostVec<ulonglong2> &vs = b->seg_sig[k];
+        HostVec<uint64_t> &vp = b->seg_pos[k];
+        if (!vs.reserve(vs.n + cnt[k]) || !vp.reserve(vp.n + cnt[k])) return BSDB_ENOMEM;
+        HIP_OK(hipMemcpyAsync(vs.p + vs.n, o_sig + base[k], (size_t)cnt[k] * 16, hipMemcpyDeviceToHost, s));
+        HIP_OK(hipMemcpyAsync(vp.p + vp.n, o_pos + base[k], (size_t)cnt[k] * 8, hipMemcpyDeviceToHost, s));
+        vs.n += cnt[k];
+        vp.n += cnt[k];
+    }
+    HIP_OK(hipStreamSynchronize(s));
     return BSDB_OK;
+}
+
+// stage bytes for k keys of a spill round: signatures + the segment scratch
+size_t spill_scratch_bytes(uint64_t k) { return 1024 + 2048 + (size_t)k * (16 + 16 + 8) + 256; }
+
+// Switches a builder to spill mode: every resident key hashed on the device
+// and moved to the host segments (its add position = its index), the key
+// area released.  Caller holds mu, grow_mu exclusively (no copy in flight),
+// the context lock, device set.
+int builder_to_spill(bsdb_builder *b) {
+    bsdb_ctx *c = b->c;
+    hipStream_t s = c->stream;
+    const uint64_t n = b->n;
+    uint64_t chunk = 1ull << 24;  // keys a round (a multiple of 16: 16-B aligned fixed-length rounds)
+    while (chunk >= 4096 && stage_reserve(b, spill_scratch_bytes(chunk) + chunk * 16))
+        chunk >>= 1;
+    if (chunk < 4096) return BSDB_ENOMEM;
+    uint8_t *stage = (uint8_t *)b->d_stage;
+    for (uint64_t k0 = 0; k0 < n; k0 += chunk) {
+        const uint64_t k = std::min(chunk, n - k0);
+        ulonglong2 *d_sig = (ulonglong2 *)stage;
+        int rc = b->key_len ? hash_impl(c, b->d_keys + k0 * b->key_len, nullptr, k * b->key_len, b->key_len, k, 0,
+                                        (uint64_t *)d_sig, s)
+                            : hash_impl(c, b->d_keys, b->d_off + k0, b->key_bytes, 0, k, 0, (uint64_t *)d_sig, s);
+        if (!rc) rc = spill_segments(b, d_sig, k, k0, stage + (size_t)chunk * 16, s);
+        if (rc) return rc;
+    }
+    HIP_OK(hipStreamSynchronize(s));
+    (void)hipFree(b->d_keys);
+    (void)hipFree(b->d_off);
+    b->d_keys = nullptr;
+    b->d_off = nullptr;
+    b->keys_cap = b->off_cap = 0;
+    b->spill = true;
+    if (getenv("BSDB_BUILDER_PROFILE"))
+        fprintf(stderr, "[bsdb builder] spill mode after %llu keys (%llu key bytes)\n", (unsigned long long)n,
+                (unsigned long long)b->key_bytes);
+    return BSDB_OK;
+}
+
+// An add in spill mode (caller holds mu): the batch hashed on the device in
+// rounds and appended to the host segments with positions n0..
+int spill_add_locked(bsdb_builder *b, const AddBatch &a, uint64_t n0) {
+    bsdb_ctx *c = b->c;
+    std::lock_guard<std::mutex> g(c->mu);
+    HIP_OK(hipSetDevice(c->device));
+    Ordered ord(c, c->stream);
+    hipStream_t s = c->stream;
+    constexpr uint64_t ROUND_KEYS = 1ull << 23, ROUND_BYTES = 512ull << 20;
+    for (uint64_t i0 = 0; i0 < a.count;) {
+        uint64_t i1 = std::min(a.count, i0 + ROUND_KEYS);
+        if (a.off)
+            while (i1 - i0 > 1 && a.off[i1] - a.off[i0] > ROUND_BYTES) i1 = i0 + (i1 - i0) / 2;
+        else
+            i1 = std::min(i1, i0 + std::max<uint64_t>(1, ROUND_BYTES / a.key_len));
+        const uint64_t k = i1 - i0;
+        const uint64_t kbytes = a.off ? a.off[i1] - a.off[i0] : k * a.key_len;
+        const size_t key_room = ((size_t)kbytes + 16 + 255) & ~(size_t)255, off_room = a.off ? ((k + 1) * 8 + 255) & ~(size_t)255 : 0;
+        int rc = stage_reserve(b, key_room + off_room + (size_t)k * 16 + spill_scratch_bytes(k));
+        if (rc) return rc;
+        uint8_t *d_k = (uint8_t *)b->d_stage;
+        uint64_t *d_o = (uint64_t *)(d_k + key_room);
+        ulonglong2 *d_sig = (ulonglong2 *)(d_k + key_room + off_room);
+        if (kbytes) HIP_OK(hipMemcpyAsync(d_k, a.off ? a.keys + a.off[i0] : a.keys + i0 * a.key_len, kbytes, hipMemcpyHostToDevice, s));
+        if (a.off) {
+            HIP_OK(hipMemcpyAsync(d_o, a.off + i0, (k + 1) * 8, hipMemcpyHostToDevice, s));
+            k_rebase_offsets<<<grid_for(c, k + 1), 256, 0, s>>>(d_o, k + 1, (uint64_t)0 - a.off[i0]);
+        }
+        rc = a.off ? hash_impl(c, d_k, d_o, kbytes, 0, k, 0, (uint64_t *)d_sig, s)
+                   : hash_impl(c, d_k, nullptr, kbytes, a.key_len, k, 0, (uint64_t *)d_sig, s);
+        if (!rc) rc = spill_segments(b, d_sig, k, n0 + i0, (uint8_t *)(d_sig + k), s);
+        if (rc) return rc;
+        i0 = i1;
+    }
+    return BSDB_OK;
+}
+
+// Room for an add of `count` keys and `bytes` key bytes past the reserved
+// ranges (caller holds mu).  A growth waits for the copies in flight
+// (grow_mu exclusive); a key area that cannot grow (the device's HBM, or
+// dev_key_cap) switches the builder to spill mode.
+int builder_make_room(bsdb_builder *b, uint64_t count, uint64_t bytes) {
+    const uint64_t n1 = b->n + count;
+    const bool gh = !b->borrowed_records &&
+                    ((!b->stride && n1 > b->addr.cap) || (b->approx && (n1 > b->value8.cap || n1 > b->vlen.cap)));
+    const bool gk = !b->spill && (b->key_bytes + bytes + 16 > b->keys_cap || (!b->key_len && (n1 + 1) * 8 > b->off_cap));
+    if (!gh && !gk) return BSDB_OK;
+    std::unique_lock<std::shared_mutex> ex(b->grow_mu);
+    if (gh) {
+        b->stop_prefault();  // (a growing array may move)
+        if ((!b->stride && !b->addr.reserve(n1)) || (b->approx && (!b->value8.reserve(n1) || !b->vlen.reserve(n1))))
+            return BSDB_ENOMEM;
+    }
+    if (!gk) return BSDB_OK;
+    bsdb_ctx *c = b->c;
+    std::lock_guard<std::mutex> g(c->mu);
+    HIP_OK(hipSetDevice(c->device));
+    Ordered ord(c, c->stream);
+    const uint64_t want = b->key_bytes + bytes + 16;
+    int rc = want > b->dev_key_cap ? BSDB_ENOMEM
+                                   : dev_reserve(c, (void **)&b->d_keys, &b->keys_cap, b->key_bytes, want, b->dev_key_cap);
+    if (!rc && !b->key_len) rc = dev_reserve(c, (void **)&b->d_off, &b->off_cap, (b->n + 1) * 8, (n1 + 1) * 8);
+    if (rc == BSDB_ENOMEM) rc = builder_to_spill(b);
+    return rc;
+}
+
+// The batch's keys (and offsets) into the key area at key index n0 / key byte
+// kb0, on a stream of the calling thread's own: adds run concurrently.
+int add_copy_device(bsdb_builder *b, const AddBatch &a, uint64_t n0, uint64_t kb0) {
+    bsdb_ctx *c = b->c;
+    hipStream_t s = nullptr;
+    hipError_t e = hipSetDevice(c->device);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+    const uint64_t bytes = a.bytes();
+    if (e == hipSuccess && bytes) e = hipMemcpyAsync(b->d_keys + kb0, a.first(), bytes, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess && !b->key_len && a.count) {  // a variable-length builder's offsets
+        uint64_t *dst = b->d_off + n0 + 1;
+        if (a.uni != 0xFFFFFFFFu) {
+            // one length (a kv.db partition of fixed-size keys): the offsets
+            // are a formula, written on the device instead of copied
+            k_fill_offsets<<<grid_for(c, a.count), 256, 0, s>>>(dst, a.count, kb0, a.uni);
+            e = hipGetLastError();
+        } else {
+            e = hipMemcpyAsync(dst, a.off + 1, a.count * 8, hipMemcpyHostToDevice, s);
+            if (e == hipSuccess) {
+                k_rebase_offsets<<<grid_for(c, a.count), 256, 0, s>>>(dst, a.count, kb0 - a.o0());
+                e = hipGetLastError();
+            }
+        }
+    }
+    if (e == hipSuccess) e = hipStreamSynchronize(s);  // the caller may reuse its buffers
+    if (s) (void)hipStreamDestroy(s);
+    return e == hipSuccess ? BSDB_OK : hip_fail(e, "builder add copy", __LINE__);
+}
+
+void add_copy_records(bsdb_builder *b, uint64_t n0, uint64_t count, const uint64_t *h_addr, const uint64_t *h_value8,
+                      const uint8_t *h_vlen) {
+    if (b->borrowed_records || !count) return;
+    if (!b->stride) memcpy(b->addr.p + n0, h_addr, count * 8);
+    if (b->approx) {
+        memcpy(b->value8.p + n0, h_value8, count * 8);
+        memcpy(b->vlen.p + n0, h_vlen, count);
+    }
+}
+
+// One add: its ranges reserved under the builder's lock, the copies outside
+// it (concurrently with other adds); a failure marks the builder failed.
+int builder_add(bsdb_builder *b, const AddBatch &a, const uint64_t *h_addr, const uint64_t *h_value8,
+                const uint8_t *h_vlen) {
+    std::shared_lock<std::shared_mutex> copying;
+    uint64_t n0 = 0, kb0 = 0;
+    {
+        std::lock_guard<std::mutex> gb(b->mu);
+        if (b->failed) return b->failed;
+        if (b->finished) return BSDB_EINVAL;
+        int rc = builder_check_records(b, a.count, h_addr, h_value8, h_vlen);
+        if (rc) return rc;
+        if (a.count == 0) return BSDB_OK;
+        const uint64_t bytes = a.bytes();
+        if ((rc = builder_make_room(b, a.count, bytes))) return b->failed = rc;
+        n0 = b->n;
+        kb0 = b->key_bytes;
+        if (!b->key_len) {
+            const uint32_t len = a.off ? a.uni : a.key_len;
+            if (n0 == 0) b->uni_len = len;
+            b->uniform = b->uniform && len != 0xFFFFFFFFu && len == b->uni_len;
+        }
+        if (b->spill) {
+            // (serialised: the device hash and the segment appends)
+            if ((rc = spill_add_locked(b, a, n0))) return b->failed = rc;
+            add_copy_records(b, n0, a.count, h_addr, h_value8, h_vlen);
+        } else {
+            copying = std::shared_lock<std::shared_mutex>(b->grow_mu);  // (before mu is released: no growth between)
+        }
+        b->n += a.count;
+        b->key_bytes += bytes;
+        if (!b->borrowed_records) {
+            if (!b->stride) b->addr.n = b->n;
+            if (b->approx) b->value8.n = b->vlen.n = b->n;
+        }
+        if (b->spill) return BSDB_OK;
+    }
+    int rc = add_copy_device(b, a, n0, kb0);
+    add_copy_records(b, n0, a.count, h_addr, h_value8, h_vlen);
+    copying.unlock();
+    if (rc) {
+        std::lock_guard<std::mutex> gb(b->mu);
+        if (!b->failed) b->failed = rc;
+    }
+    return rc;
 }
 
 // creates (truncates) an index file at its final size and maps a regular
@@ -412,10 +689,12 @@ int builder_finish_locked(bsdb_builder *b, uint32_t width, uint32_t passes, cons
     void *d_addr = nullptr, *d_v8 = nullptr, *d_vl = nullptr;
     void *slot_a[2] = {nullptr, nullptr};
     size_t slot_a_bytes[2] = {0, 0};
+    void *sp_in = nullptr, *sp_out = nullptr;  // spill mode: a pass's uploaded segments, its compacted keys
+    size_t sp_in_bytes = 0, sp_out_bytes = 0;
     bsdb_mph *p = nullptr;
     auto done = [&](int rc) {
         (void)hipStreamSynchronize(c->stream);
-        for (void *q : {d_addr, d_v8, d_vl, slot_a[0], slot_a[1]}) (void)hipFree(q);
+        for (void *q : {d_addr, d_v8, d_vl, slot_a[0], slot_a[1], sp_in, sp_out}) (void)hipFree(q);
         pop_o.finish();
         pop_a.finish();
         if (getenv("BSDB_BUILDER_PROFILE") && fo.map)
@@ -480,27 +759,30 @@ int builder_finish_locked(bsdb_builder *b, uint32_t width, uint32_t passes, cons
                 return done(up_rc ? up_rc : BSDB_ENOMEM);
             dev_addr = (const uint64_t *)d_addr;
         }
-        if (!b->approx && !host_gather) {
+        if (!b->approx && !host_gather && !b->spill) {
             // the solve stores the final slots (addr[p] or base + stride p)
             sink.job = [&](int, const uint64_t *d_slice, uint64_t nl, uint64_t e_lo) {
                 return write_slots(c->device, fo, d_slice, nl, e_lo, nullptr, nullptr);
             };
         } else if (!host_gather) {
-            // approximate: positions in the slots, gathered on the device
+            // approximate (or spill mode): positions in the slots, gathered on the device
             sink.positions = true;
-            sink.job_bytes_per_key = 16;
-            sink.prepare = [&](int sl, uint64_t nl) { return grow(&slot_a[sl], &slot_a_bytes[sl], std::max<uint64_t>(nl, 1) * 8); };
+            sink.job_bytes_per_key = b->approx ? 16 : 8;
+            sink.prepare = [&](int sl, uint64_t nl) {
+                return b->approx ? grow(&slot_a[sl], &slot_a_bytes[sl], std::max<uint64_t>(nl, 1) * 8) : BSDB_OK;
+            };
             sink.job = [&](int sl, const uint64_t *d_slice, uint64_t nl, uint64_t e_lo) {
                 hipStream_t st = nullptr;
                 if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return BSDB_EIO;
                 k_slot_gather<<<grid_for(c, nl), 256, 0, st>>>(const_cast<uint64_t *>(d_slice), nl, dev_addr,
                                                                 b->addr_base, b->addr_stride, (const uint64_t *)d_v8,
-                                                                (const uint8_t *)d_vl, (uint64_t *)slot_a[sl]);
+                                                                (const uint8_t *)d_vl,
+                                                                b->approx ? (uint64_t *)slot_a[sl] : nullptr);
                 const bool ok = hipGetLastError() == hipSuccess && hipStreamSynchronize(st) == hipSuccess;
                 (void)hipStreamDestroy(st);
                 if (!ok) return BSDB_EIO;
                 int r = write_slots(c->device, fo, d_slice, nl, e_lo, nullptr, nullptr);
-                if (!r) r = write_slots(c->device, fao, (const uint64_t *)slot_a[sl], nl, e_lo, nullptr, nullptr);
+                if (!r && b->approx) r = write_slots(c->device, fao, (const uint64_t *)slot_a[sl], nl, e_lo, nullptr, nullptr);
                 return r;
             };
         } else {
@@ -526,6 +808,51 @@ int builder_finish_locked(bsdb_builder *b, uint32_t width, uint32_t passes, cons
             };
         }
     }
+    if (b->spill) {
+        // Spill mode: pass p's keys are those of the 256 host segments that
+        // can hold its buckets [b_lo, b_hi) -- the segment is sig0's top byte
+        // and the bucket is monotone in sig0 (CBHS:129-138, 900, 965), so a
+        // contiguous run of segments, the two at its ends shared with the
+        // neighbouring passes -- uploaded and compacted to the range on the
+        // device; each key's add position goes into its slot (positions mode).
+        const uint64_t mult = 2 * (n / BUCKET_SIZE + 1);
+        sink.positions = true;
+        sink.source_bytes_per_key = 2 * 24 + 8;
+        sink.source = [&](uint64_t b_lo, uint64_t b_hi, GovSrc &ps, const uint64_t **pos) -> int {
+            auto x_first = [&](uint64_t bk) { return (((unsigned __int128)bk << 64) + mult - 1) / mult; };  // first sig0 >>> 1 of bucket bk
+            const uint32_t s_a = (uint32_t)(x_first(b_lo) >> 55), s_b = (uint32_t)((x_first(b_hi) - 1) >> 55);
+            uint64_t tot = 0;
+            for (uint32_t k = s_a; k <= s_b && k < NSEG; ++k) tot += b->seg_sig[k].n;
+            int r;
+            if ((r = grow(&sp_in, &sp_in_bytes, tot * 24 + 256)) || (r = grow(&sp_out, &sp_out_bytes, tot * 24 + 512)))
+                return r;
+            ulonglong2 *in_sig = (ulonglong2 *)sp_in, *out_sig = (ulonglong2 *)sp_out;
+            uint64_t *in_pos = (uint64_t *)(in_sig + tot), *out_pos = (uint64_t *)(out_sig + tot);
+            unsigned long long *d_cnt = (unsigned long long *)(out_pos + tot);
+            hipStream_t st = c->stream;
+            uint64_t at = 0;
+            for (uint32_t k = s_a; k <= s_b && k < NSEG; ++k) {
+                const uint64_t kn = b->seg_sig[k].n;
+                if (!kn) continue;
+                HIP_OK(hipMemcpyAsync(in_sig + at, b->seg_sig[k].p, kn * 16, hipMemcpyHostToDevice, st));
+                HIP_OK(hipMemcpyAsync(in_pos + at, b->seg_pos[k].p, kn * 8, hipMemcpyHostToDevice, st));
+                at += kn;
+            }
+            HIP_OK(hipMemsetAsync(d_cnt, 0, 8, st));
+            if (tot)
+                k_range_compact<<<grid_for(c, tot), 256, 0, st>>>(in_sig, in_pos, tot, (uint32_t)mult, (uint32_t)b_lo,
+                                                                  (uint32_t)b_hi, out_sig, out_pos, d_cnt);
+            if ((r = launch_status())) return r;
+            unsigned long long got = 0;
+            HIP_OK(hipMemcpyAsync(&got, d_cnt, 8, hipMemcpyDeviceToHost, st));
+            HIP_OK(hipStreamSynchronize(st));
+            ps = GovSrc{};
+            ps.sig = tot ? (const uint64_t *)out_sig : reinterpret_cast<const uint64_t *>(16);  // (n == 0: never read)
+            ps.n = got;
+            *pos = out_pos;
+            return BSDB_OK;
+        };
+    }
     rc = passes_build(c, src, n, width, passes, dev_addr, b->addr_base, b->addr_stride, p->E, p->values, p->sigbits,
                       sink, passes_used, c->stream);
     return done(rc);
@@ -537,16 +864,24 @@ void builder_release(bsdb_builder *b) {
     (void)hipSetDevice(b->c->device);
     (void)hipFree(b->d_keys);
     (void)hipFree(b->d_off);
+    (void)hipFree(b->d_stage);
     b->d_keys = nullptr;
     b->d_off = nullptr;
-    b->keys_cap = b->off_cap = 0;
+    b->d_stage = nullptr;
+    b->keys_cap = b->off_cap = b->stage_cap = 0;
+    for (uint32_t k = 0; k < NSEG; ++k) {
+        b->seg_sig[k].release();
+        b->seg_pos[k].release();
+    }
     b->addr.release();
     b->value8.release();
     b->vlen.release();
 }
 
+// borrowed: the caller's record arrays will be borrowed (host_passes_build):
+// no host arrays reserved, no populator started
 int builder_open(bsdb_ctx *c, uint32_t key_len, uint64_t key_capacity, uint64_t blob_capacity, int approximate,
-                 uint64_t addr_base, uint64_t addr_stride, bsdb_builder **out) {
+                 uint64_t addr_base, uint64_t addr_stride, bsdb_builder **out, bool borrowed = false) {
     if (!c || !out || (key_len && bad_key_len(key_len))) return BSDB_EINVAL;
     *out = nullptr;
     bsdb_builder *b = new (std::nothrow) bsdb_builder();
@@ -557,6 +892,10 @@ int builder_open(bsdb_ctx *c, uint32_t key_len, uint64_t key_capacity, uint64_t 
     b->stride = addr_stride != 0;
     b->addr_base = addr_base;
     b->addr_stride = addr_stride;
+    b->borrowed_records = borrowed;
+    // BSDB_BUILDER_DEVICE_KEY_BYTES (a test knob): the most key bytes the
+    // device key area may hold; adds past it switch to spill mode
+    if (const char *v = getenv("BSDB_BUILDER_DEVICE_KEY_BYTES")) b->dev_key_cap = std::max<uint64_t>(4096, strtoull(v, nullptr, 0));
     int rc = BSDB_OK;
     {
         std::lock_guard<std::mutex> g(c->mu);
@@ -564,8 +903,10 @@ int builder_open(bsdb_ctx *c, uint32_t key_len, uint64_t key_capacity, uint64_t 
             rc = BSDB_EIO;
         } else {
             Ordered ord(c, c->stream);
-            const uint64_t kb = key_len ? key_capacity * key_len : blob_capacity;
-            rc = dev_reserve(c, (void **)&b->d_keys, &b->keys_cap, 0, kb + 16);
+            const uint64_t kb = std::min<uint64_t>((key_len ? key_capacity * key_len : blob_capacity) + 16, b->dev_key_cap);
+            rc = dev_reserve(c, (void **)&b->d_keys, &b->keys_cap, 0, kb);
+            // (a capacity HBM cannot hold: a smaller area now, spill mode when the adds outgrow what HBM allows)
+            if (rc == BSDB_ENOMEM && kb > (64ull << 20)) rc = dev_reserve(c, (void **)&b->d_keys, &b->keys_cap, 0, 64ull << 20);
             if (!rc && !key_len) {
                 rc = dev_reserve(c, (void **)&b->d_off, &b->off_cap, 0, (key_capacity + 1) * 8);
                 if (!rc && hipMemsetAsync(b->d_off, 0, 8, c->stream) != hipSuccess) rc = BSDB_EIO;
@@ -573,16 +914,17 @@ int builder_open(bsdb_ctx *c, uint32_t key_len, uint64_t key_capacity, uint64_t 
             }
         }
     }
-    if (!rc && ((!b->stride && !b->addr.reserve(key_capacity)) ||
-                (b->approx && (!b->value8.reserve(key_capacity) || !b->vlen.reserve(key_capacity)))))
+    if (!rc && !borrowed &&
+        ((!b->stride && !b->addr.reserve(key_capacity)) ||
+         (b->approx && (!b->value8.reserve(key_capacity) || !b->vlen.reserve(key_capacity)))))
         rc = BSDB_ENOMEM;
     if (rc) {
         builder_release(b);
         delete b;
         return rc;
     }
-    if (!b->stride && b->addr.cap) b->pop_addr.start(reinterpret_cast<uint8_t *>(b->addr.p), b->addr.cap * 8);
-    if (b->approx && b->value8.cap) b->pop_v8.start(reinterpret_cast<uint8_t *>(b->value8.p), b->value8.cap * 8);
+    if (!borrowed && !b->stride && b->addr.cap) b->pop_addr.start(reinterpret_cast<uint8_t *>(b->addr.p), b->addr.cap * 8);
+    if (!borrowed && b->approx && b->value8.cap) b->pop_v8.start(reinterpret_cast<uint8_t *>(b->value8.p), b->value8.cap * 8);
     *out = b;
     return BSDB_OK;
 }
@@ -599,11 +941,9 @@ static int host_passes_build(bsdb_ctx *c, const uint8_t *h_keys, uint32_t key_le
     const bool var = h_off != nullptr;
     const uint64_t blob = var ? (n ? h_off[n] - h_off[0] : 0) : 0;
     bsdb_builder *b = nullptr;
-    int rc = builder_open(c, var ? 0 : key_len, n, blob, approximate, addr_base, h_addr ? 0 : addr_stride, &b);
+    int rc = builder_open(c, var ? 0 : key_len, n, blob, approximate, addr_base, h_addr ? 0 : addr_stride, &b, true);
     if (rc) return rc;
     // the caller's record arrays outlive the call: borrowed, not copied
-    b->stop_prefault();
-    b->borrowed_records = true;
     if (h_addr) b->addr.borrow(h_addr, n);
     if (approximate) {
         b->value8.borrow(h_value8, n);
@@ -618,17 +958,25 @@ static int host_passes_build(bsdb_ctx *c, const uint8_t *h_keys, uint32_t key_le
             while (k1 - k0 > 1 && h_off[k1] - h_off[k0] > BATCH) k1 = k0 + (k1 - k0) / 2;
             uint32_t uni = 0;
             rc = var_batch_lengths(h_off + k0, k1 - k0, &uni);
-            if (!rc)
-                rc = builder_add(b, k1 - k0, nullptr, nullptr, nullptr,
-                                 [&] { return builder_add_var_locked(b, h_blob, h_off + k0, k1 - k0, uni); });
+            AddBatch a;
+            a.keys = h_blob;
+            a.off = h_off + k0;
+            a.count = k1 - k0;
+            a.uni = uni;
+            if (!rc) rc = builder_add(b, a, nullptr, nullptr, nullptr);
         } else {
             k1 = std::min(n, k0 + std::max<uint64_t>(1, BATCH / key_len));
-            rc = builder_add(b, k1 - k0, nullptr, nullptr, nullptr,
-                             [&] { return builder_add_fixed_locked(b, h_keys + k0 * key_len, key_len, k1 - k0); });
+            AddBatch a;
+            a.keys = h_keys + k0 * key_len;
+            a.key_len = a.uni = key_len;
+            a.count = k1 - k0;
+            rc = builder_add(b, a, nullptr, nullptr, nullptr);
         }
         k0 = k1;
     }
     if (!rc) {
+        std::lock_guard<std::mutex> gb(b->mu);
+        std::unique_lock<std::shared_mutex> settled(b->grow_mu);
         std::lock_guard<std::mutex> g(c->mu);
         if (hipSetDevice(c->device) != hipSuccess) {
             rc = BSDB_EIO;
@@ -667,8 +1015,11 @@ int bsdb_builder_open(bsdb_ctx *c, uint32_t key_len, uint64_t key_capacity, uint
 int bsdb_builder_add_fixed(bsdb_builder *b, const uint8_t *h_keys, uint32_t key_len, uint64_t count,
                            const uint64_t *h_addr, const uint64_t *h_value8, const uint8_t *h_vlen) {
     if (!b || bad_key_len(key_len) || (count && !h_keys) || (b->key_len && key_len != b->key_len)) return BSDB_EINVAL;
-    return builder_add(b, count, h_addr, h_value8, h_vlen,
-                       [&] { return builder_add_fixed_locked(b, h_keys, key_len, count); });
+    AddBatch a;
+    a.keys = h_keys;
+    a.key_len = a.uni = key_len;
+    a.count = count;
+    return builder_add(b, a, h_addr, h_value8, h_vlen);
 }
 
 int bsdb_builder_add_var(bsdb_builder *b, const uint8_t *h_blob, const uint64_t *h_off, uint64_t count,
@@ -676,12 +1027,17 @@ int bsdb_builder_add_var(bsdb_builder *b, const uint8_t *h_blob, const uint64_t 
     if (!b || b->key_len || (count && (!h_blob || !h_off))) return BSDB_EINVAL;
     uint32_t uni = 0;
     if (count && var_batch_lengths(h_off, count, &uni)) return BSDB_EINVAL;
-    return builder_add(b, count, h_addr, h_value8, h_vlen,
-                       [&] { return builder_add_var_locked(b, h_blob, h_off, count, uni); });
+    AddBatch a;
+    a.keys = h_blob;
+    a.off = h_off;
+    a.count = count;
+    a.uni = uni;
+    return builder_add(b, a, h_addr, h_value8, h_vlen);
 }
 
 int bsdb_builder_count(const bsdb_builder *b, uint64_t *n) {
     if (!b || !n) return BSDB_EINVAL;
+    std::lock_guard<std::mutex> gb(const_cast<bsdb_builder *>(b)->mu);  // (adds reserve under it: ADVICE r4)
     *n = b->n;
     return BSDB_OK;
 }
@@ -696,6 +1052,7 @@ int bsdb_builder_finish(bsdb_builder *b, uint32_t width, uint32_t passes, const 
     bsdb_ctx *c = b->c;
     int rc;
     {
+        std::unique_lock<std::shared_mutex> settled(b->grow_mu);  // every add's copies are done
         std::lock_guard<std::mutex> g(c->mu);
         HIP_OK(hipSetDevice(c->device));
         Ordered ord(c, c->stream);

@@ -289,7 +289,6 @@ int bsdb_kv_build_index(bsdb_ctx *c, const char *kv_base, int partitions, int fo
                           (uint64_t)(per_byte_blob * (double)file_bytes * 1.02) + 65536, approximate, 0, 0, &b);
     if (rc) return rc;
     std::unique_ptr<bsdb_builder, int (*)(bsdb_builder *)> guard(b, bsdb_builder_free);
-    std::mutex add_mu;
     // (partitions in flight = threads: the host memory bound)
     const int T = std::max(1, std::min(threads > 0 ? threads : usable_cpus(), partitions));
     std::atomic<int> next{0};
@@ -314,10 +313,15 @@ int bsdb_kv_build_index(bsdb_ctx *c, const char *kv_base, int partitions, int fo
             uint32_t uni = 0;
             if (!r) r = var_batch_lengths(part.off.data(), k, &uni);
             if (!r) {
-                std::lock_guard<std::mutex> g(add_mu);
+                // (adds from the scan threads run concurrently: the builder
+                // reserves each one's ranges under its lock and copies outside it)
                 const auto t1 = std::chrono::steady_clock::now();
-                r = builder_add(b, k, part.addr.data(), part.value8.data(), part.vlen.data(),
-                                [&] { return builder_add_var_locked(b, part.blob.data(), part.off.data(), k, uni); });
+                AddBatch a;
+                a.keys = part.blob.data();
+                a.off = part.off.data();
+                a.count = k;
+                a.uni = uni;
+                r = builder_add(b, a, part.addr.data(), part.value8.data(), part.vlen.data());
                 add_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t1).count();
             }
             if (r) {
@@ -334,7 +338,7 @@ int bsdb_kv_build_index(bsdb_ctx *c, const char *kv_base, int partitions, int fo
     const double t_scanned = since();
     rc = bsdb_builder_finish(b, width, 0, index_path, index_a_path, out, nullptr);
     if (prof)
-        fprintf(stderr, "[bsdb kv] %llu records: scan+add %.3f s (thread scan %.3f s, adds %.3f s under the lock), finish %.3f s\n",
+        fprintf(stderr, "[bsdb kv] %llu records: scan+add %.3f s (thread scan %.3f s, thread adds %.3f s), finish %.3f s\n",
                 (unsigned long long)b->n, t_scanned, scan_ns.load() / 1e9, add_ns.load() / 1e9, since() - t_scanned);
     return rc;
 }

@@ -36,6 +36,13 @@ struct PassSink {
     std::function<int(int sl, const uint64_t *d_slice, uint64_t nl, uint64_t e_lo)> job;
     uint64_t job_bytes_per_key = 0;  // device bytes per key of a pass the job holds (both slot buffers)
     bool positions = false;
+    // (optional) where a pass's keys come from when they are not resident:
+    // the range's signatures (src.sig, src.n) and each one's add position
+    // (*pos: the solve stores it byte-reversed in the key's slot, so the sink
+    // works in positions mode); source_bytes_per_key: its device bytes per key
+    // of a pass.  The builder's spill mode (capi_builder.hip).
+    std::function<int(uint64_t b_lo, uint64_t b_hi, GovSrc &src, const uint64_t **pos)> source;
+    uint64_t source_bytes_per_key = 0;
     bool slices() const { return h_index || job; }
 };
 
@@ -43,7 +50,7 @@ struct PassSink {
 // the pass's index slots (twice when they go out of the device: one buffer is
 // copied out while the next pass fills the other)
 uint64_t pass_bytes_per_key(const PassSink &sink) {
-    return 16 + 8 + (sink.slices() ? 16 + sink.job_bytes_per_key : 0);
+    return 16 + 8 + (sink.slices() ? 16 + sink.job_bytes_per_key : 0) + sink.source_bytes_per_key;
 }
 
 int passes_build(bsdb_ctx *c, const GovSrc &src, uint64_t n, uint32_t width, uint32_t passes, const uint64_t *d_addr,
@@ -61,7 +68,7 @@ int passes_build(bsdb_ctx *c, const GovSrc &src, uint64_t n, uint32_t width, uin
     const auto t_start = std::chrono::steady_clock::now();
     auto since = [&] { return std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count(); };
     const bool fixed_ok = src.off || (!bad_key_len(src.key_len) && aligned16(src.keys));
-    if (n >= (1ULL << 16) && fixed_ok) {
+    if (n >= (1ULL << 16) && fixed_ok && !sink.source) {
         void *q = nullptr;
         HIP_OK(dmalloc(&q, m * 4));
         counts_all.reset(q);
@@ -141,7 +148,15 @@ int passes_build(bsdb_ctx *c, const GovSrc &src, uint64_t n, uint32_t width, uin
         }  // (neither: the structure only)
         uint64_t nl = 0;
         const double t_pass = since();
-        int rc = gov_build_impl(c, gsrc, n, b_lo, b_hi, e_lo, width, d_E, d_values, d_sigbits, nullptr, ixo, s, false, &nl);
+        GovSrc psrc = gsrc;
+        if (sink.source) {  // the pass's signatures, each with its add position as the slot's "address"
+            const uint64_t *pos = nullptr;
+            int rs = sink.source(b_lo, b_hi, psrc, &pos);
+            if (rs) return finish(rs);
+            ixo.addr = pos;
+            ixo.addr_base = ixo.addr_stride = 0;
+        }
+        int rc = gov_build_impl(c, psrc, n, b_lo, b_hi, e_lo, width, d_E, d_values, d_sigbits, nullptr, ixo, s, false, &nl);
         if (rc) return finish(rc);
         if (prof) fprintf(stderr, "[bsdb passes] pass %u: %llu keys, start %.3f s, built in %.3f s\n", p,
                           (unsigned long long)nl, t_pass, since() - t_pass);

@@ -334,3 +334,140 @@ def test_kv_streamed_build_equals_in_memory_scan(ctx, tmp_path, fmt, var, approx
     assert same_mph(m1, m2)
     assert same_files(ip1, ip2) and same_files(ap1, ap2)
     m1.close(); m2.close()
+
+
+@pytest.fixture
+def device_key_cap(request):
+    """BSDB_BUILDER_DEVICE_KEY_BYTES: the builder's device key area capped (read
+    at bsdb_builder_open), so adds past it take the spill path."""
+    os.environ["BSDB_BUILDER_DEVICE_KEY_BYTES"] = str(request.param)
+    yield request.param
+    os.environ.pop("BSDB_BUILDER_DEVICE_KEY_BYTES", None)
+
+
+@pytest.mark.parametrize("device_key_cap", [1_000_000], indirect=True)
+@pytest.mark.parametrize("host_gather", [False, True], indirect=True)
+@pytest.mark.parametrize("var,approx,stride,threads", [
+    (False, False, False, 1), (False, True, False, 3), (True, True, False, 1), (True, False, True, 4),
+    (False, False, True, 2)])
+def test_spill_mode_equals_one_shot(ctx, tmp_path, device_key_cap, host_gather, var, approx, stride, threads):
+    """keys beyond the device key area.  With the key area
+    capped at 1 MB, the first adds stay resident, the add that outgrows it
+    moves them (hashed on the device) into the 256 host segments of (sig0,
+    sig1, add position) by sig0's top byte (CBHS:379-395), and every later add
+    is hashed and appended there; the finish uploads each pass's segments.
+    MPHF and files byte-identical to the one-shot build."""
+    import threading
+    n = 300_000
+    keys, blob, off, addr, value8, vlen = make_records(n, var, approx, seed=31)
+    if stride:
+        addr = np.uint64(0x2000) + np.uint64(64) * np.arange(n, dtype=np.uint64)
+    m1, ip1, ap1 = f2_reference(ctx, str(tmp_path), n, var, approx, keys, blob, off, addr, value8, vlen)
+    kw = dict(addr_base=0x2000, addr_stride=64) if stride else {}
+    b = ctx.builder(0 if var else 13, key_capacity=n // 8, blob_capacity=1000, approximate=approx, **kw)
+    cuts = np.linspace(0, n, 13).astype(np.int64)
+    errors = []
+
+    def worker(t):
+        try:
+            for j in range(t, len(cuts) - 1, threads):
+                lo, hi = int(cuts[j]), int(cuts[j + 1])
+                a = None if stride else addr[lo:hi]
+                v8 = value8[lo:hi] if approx else None
+                vl = vlen[lo:hi] if approx else None
+                if var:
+                    b.add_var(blob, off[lo:hi + 1], a, v8, vl)
+                else:
+                    b.add_fixed(keys[13 * lo:13 * hi], 13, a, v8, vl)
+        except Exception as e:  # noqa: BLE001 (reported below)
+            errors.append(e)
+
+    if stride:  # (addresses by the add order: one thread, in order)
+        worker_threads, threads = [threading.Thread(target=worker, args=(0,))], 1
+    else:
+        worker_threads = [threading.Thread(target=worker, args=(t,)) for t in range(threads)]
+    for t in worker_threads:
+        t.start()
+    for t in worker_threads:
+        t.join()
+    assert not errors
+    assert b.count() == n
+    ip2, ap2 = str(tmp_path / "index.db"), str(tmp_path / "index_a.db")
+    m2, used = b.finish(4, ip2, ap2, passes=3)
+    assert used == 3
+    assert same_mph(m1, m2)
+    assert same_files(ip1, ip2) and same_files(ap1, ap2)
+    b.close(); m1.close(); m2.close()
+
+
+@pytest.mark.parametrize("device_key_cap", [1_000_000], indirect=True)
+def test_spill_mode_duplicates_and_empty(ctx, tmp_path, device_key_cap):
+    from bsdb_amd.native import BsdbError
+    keys = O.gen_keys13(0, 200_000)
+    addr = np.arange(200_000, dtype=np.uint64)
+    b = ctx.builder(13)
+    b.add_fixed(keys, 13, addr)                     # 2.6 MB: past the cap, spilled
+    b.add_fixed(keys[:13 * 5], 13, addr[:5])
+    with pytest.raises(BsdbError) as e:
+        b.finish(4, str(tmp_path / "i.db"), None, passes=2)
+    assert e.value.code == -17                      # EDUP (CBHS:969-972) found in the spilled segments
+    b.close()
+
+
+@pytest.mark.timeout(900)
+def test_spill_build_2e8_keys_equals_resident_build():
+    """VERDICT r4 item 6 at size: 2e8 13-byte keys (2.6 GB) through a builder
+    whose device key area is capped at 0.8 GB, so ~70 % of the keys are
+    spilled to the host segments, added by 4 threads at once, in approximate
+    mode with explicit addresses; 4 passes.  The MPHF, index.db and
+    index_a.db are byte-identical to the same records' build with every key
+    resident in HBM."""
+    import threading
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from bsdb_amd import Context
+    n = 200_000_000
+    ctx = Context(0)
+    keys = O.gen_keys13_mt(0, n, O.cpu_threads())
+    i = np.arange(n, dtype=np.uint64)
+    addr = np.uint64(0x1000) + np.uint64(48) * i
+    value8 = O.splitmix64_np(np.uint64(0xB5DB0002) + i)
+    vlen = np.full(n, 8, np.uint8)
+    vlen[::5] = 3
+    del i
+    d = big_tmp(4 * 8 * n)
+    try:
+        ip1, ap1 = os.path.join(d, "resident.db"), os.path.join(d, "resident_a.db")
+        m1, used1 = ctx.mph_build_index_passes_host(keys, 13, 4, ip1, ap1, addr_np=addr, approximate=True,
+                                                    value8_np=value8, vlen_np=vlen, passes=4)
+        os.environ["BSDB_BUILDER_DEVICE_KEY_BYTES"] = str(800_000_000)
+        try:
+            b = ctx.builder(13, key_capacity=n, approximate=True)
+        finally:
+            os.environ.pop("BSDB_BUILDER_DEVICE_KEY_BYTES", None)
+        cuts = np.linspace(0, n, 41).astype(np.int64)
+        errors = []
+
+        def worker(t):
+            try:
+                for j in range(t, len(cuts) - 1, 4):
+                    lo, hi = int(cuts[j]), int(cuts[j + 1])
+                    b.add_fixed(keys[13 * lo:13 * hi], 13, addr[lo:hi], value8[lo:hi], vlen[lo:hi])
+            except Exception as e:  # noqa: BLE001 (reported below)
+                errors.append(e)
+
+        th = [threading.Thread(target=worker, args=(t,)) for t in range(4)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        assert not errors and b.count() == n
+        ip2, ap2 = os.path.join(d, "index.db"), os.path.join(d, "index_a.db")
+        m2, used2 = b.finish(4, ip2, ap2, passes=4)
+        assert used1 == used2 == 4
+        assert same_mph(m1, m2)
+        assert same_files(ip1, ip2) and same_files(ap1, ap2)
+        b.close(); m1.close(); m2.close()
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
+        ctx.close()
