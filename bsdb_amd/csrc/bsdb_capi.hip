@@ -335,6 +335,38 @@ int copy_on_own_stream(int dev, void *dst, const void *src, size_t bytes, hipMem
     if (s) (void)hipStreamDestroy(s);
     return e == hipSuccess ? BSDB_OK : hip_fail(e, kind == hipMemcpyHostToDevice ? "H2D copy (own stream)" : "D2H copy (own stream)", __LINE__);
 }
+// H2D of pageable memory through two pooled pinned pieces on the caller's
+// stream (the memcpy of piece i + 1 beside the DMA of piece i).  For copies
+// that run on several host threads at once (the builder's concurrent adds):
+// the runtime's own pageable path serialised them (8 kv.db partitions' adds
+// at ~1 GB/s each, profiles/r5/kv/), each thread's bounce copies on its own.
+int h2d_bounce(hipStream_t s, void *dst, const void *src, size_t bytes) {
+    if (bytes == 0) return BSDB_OK;
+    void *pin[2] = {pinned_pool().take(), pinned_pool().take()};
+    hipEvent_t ev[2] = {nullptr, nullptr};
+    int rc = pin[0] && pin[1] ? BSDB_OK : BSDB_ENOMEM;
+    for (int i = 0; i < 2 && !rc; ++i)
+        if (hipEventCreateWithFlags(&ev[i], hipEventDisableTiming) != hipSuccess) rc = BSDB_EIO;
+    bool pending[2] = {false, false};
+    for (size_t o = 0, k = 0; o < bytes && !rc; o += XFER_PIECE, ++k) {
+        const int i = (int)(k & 1);
+        const size_t len = std::min(XFER_PIECE, bytes - o);
+        if (pending[i] && hipEventSynchronize(ev[i]) != hipSuccess) rc = BSDB_EIO;  // the piece's buffer is free again
+        if (rc) break;
+        memcpy(pin[i], (const uint8_t *)src + o, len);
+        if (hipMemcpyAsync((uint8_t *)dst + o, pin[i], len, hipMemcpyHostToDevice, s) != hipSuccess ||
+            hipEventRecord(ev[i], s) != hipSuccess)
+            rc = BSDB_EIO;
+        pending[i] = true;
+    }
+    if (hipStreamSynchronize(s) != hipSuccess && !rc) rc = BSDB_EIO;
+    for (int i = 0; i < 2; ++i) {
+        pinned_pool().give(pin[i]);
+        if (ev[i]) (void)hipEventDestroy(ev[i]);
+    }
+    return rc;
+}
+
 int d2h_pageable(int dev, void *dst, const void *src, size_t bytes) {
     return copy_on_own_stream(dev, dst, src, bytes, hipMemcpyDeviceToHost);
 }

@@ -118,6 +118,15 @@ struct bsdb_builder {
     HostVec<uint64_t> seg_pos[256];
     void *d_stage = nullptr;       // spill adds: the batch's keys, offsets, signatures, segment order
     size_t stage_cap = 0;
+    // The records' addresses (and index_a.db value bytes) on the device as
+    // well, uploaded by each add beside its keys, when they fit an eighth of
+    // the free HBM at the open: the finish then starts without their upload
+    // (C2 from kv.db: 0.1 s of 0.42).  Dropped when they cannot grow.
+    bool dev_rec = false;
+    void *d_raddr = nullptr, *d_rv8 = nullptr, *d_rvl = nullptr;
+    size_t raddr_cap = 0, rv8_cap = 0, rvl_cap = 0;
+    std::atomic<int> copying{0};   // adds copying right now (> 1: each through pinned pieces)
+    std::atomic<uint64_t> add_copy_ns{0}, add_rec_ns{0};  // (BSDB_BUILDER_PROFILE)
     void stop_prefault() {
         pop_addr.finish();
         pop_v8.finish();
@@ -460,6 +469,15 @@ int spill_segments(bsdb_builder *b, const ulonglong2 *d_sig, uint64_t count, uin
 // stage bytes for k keys of a spill round: signatures + the segment scratch
 size_t spill_scratch_bytes(uint64_t k) { return 1024 + 2048 + (size_t)k * (16 + 16 + 8) + 256; }
 
+void builder_drop_dev_records(bsdb_builder *b) {
+    for (void **q : {&b->d_raddr, &b->d_rv8, &b->d_rvl}) {
+        (void)hipFree(*q);
+        *q = nullptr;
+    }
+    b->raddr_cap = b->rv8_cap = b->rvl_cap = 0;
+    b->dev_rec = false;
+}
+
 // Switches a builder to spill mode: every resident key hashed on the device
 // and moved to the host segments (its add position = its index), the key
 // area released.  Caller holds mu, grow_mu exclusively (no copy in flight),
@@ -488,6 +506,7 @@ int builder_to_spill(bsdb_builder *b) {
     b->d_keys = nullptr;
     b->d_off = nullptr;
     b->keys_cap = b->off_cap = 0;
+    builder_drop_dev_records(b);  // (spill adds keep their records in host memory only)
     b->spill = true;
     if (getenv("BSDB_BUILDER_PROFILE"))
         fprintf(stderr, "[bsdb builder] spill mode after %llu keys (%llu key bytes)\n", (unsigned long long)n,
@@ -543,16 +562,21 @@ int builder_make_room(bsdb_builder *b, uint64_t count, uint64_t bytes) {
     const bool gk = !b->spill && (b->key_bytes + bytes + 16 > b->keys_cap || (!b->key_len && (n1 + 1) * 8 > b->off_cap));
     if (!gh && !gk) return BSDB_OK;
     std::unique_lock<std::shared_mutex> ex(b->grow_mu);
-    if (gh) {
-        b->stop_prefault();  // (a growing array may move)
-        if ((!b->stride && !b->addr.reserve(n1)) || (b->approx && (!b->value8.reserve(n1) || !b->vlen.reserve(n1))))
-            return BSDB_ENOMEM;
-    }
-    if (!gk) return BSDB_OK;
     bsdb_ctx *c = b->c;
     std::lock_guard<std::mutex> g(c->mu);
     HIP_OK(hipSetDevice(c->device));
     Ordered ord(c, c->stream);
+    if (gh) {
+        b->stop_prefault();  // (a growing array may move)
+        if ((!b->stride && !b->addr.reserve(n1)) || (b->approx && (!b->value8.reserve(n1) || !b->vlen.reserve(n1))))
+            return BSDB_ENOMEM;
+        if (b->dev_rec && (dev_reserve(c, &b->d_raddr, &b->raddr_cap, b->n * 8, b->addr.cap * 8) ||
+                           (b->approx && (dev_reserve(c, &b->d_rv8, &b->rv8_cap, b->n * 8, b->value8.cap * 8) ||
+                                          dev_reserve(c, &b->d_rvl, &b->rvl_cap, b->n, b->vlen.cap))))) {
+            builder_drop_dev_records(b);  // (the finish uploads them from host memory instead)
+        }
+    }
+    if (!gk) return BSDB_OK;
     const uint64_t want = b->key_bytes + bytes + 16;
     int rc = want > b->dev_key_cap ? BSDB_ENOMEM
                                    : dev_reserve(c, (void **)&b->d_keys, &b->keys_cap, b->key_bytes, want, b->dev_key_cap);
@@ -563,13 +587,29 @@ int builder_make_room(bsdb_builder *b, uint64_t count, uint64_t bytes) {
 
 // The batch's keys (and offsets) into the key area at key index n0 / key byte
 // kb0, on a stream of the calling thread's own: adds run concurrently.
-int add_copy_device(bsdb_builder *b, const AddBatch &a, uint64_t n0, uint64_t kb0) {
+int add_copy_device(bsdb_builder *b, const AddBatch &a, uint64_t n0, uint64_t kb0, const uint64_t *h_addr,
+                    const uint64_t *h_value8, const uint8_t *h_vlen) {
     bsdb_ctx *c = b->c;
     hipStream_t s = nullptr;
     hipError_t e = hipSetDevice(c->device);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
     const uint64_t bytes = a.bytes();
-    if (e == hipSuccess && bytes) e = hipMemcpyAsync(b->d_keys + kb0, a.first(), bytes, hipMemcpyHostToDevice, s);
+    // one add alone: the runtime's pageable copy (56 GB/s for C4's 4 GiB
+    // batches); several at once: each through pinned pieces
+    const bool bounce = b->copying.fetch_add(1) > 0;
+    auto h2d = [&](void *dst, const void *src, size_t len) -> hipError_t {
+        if (!len || e != hipSuccess) return e;
+        if (bounce) return h2d_bounce(s, dst, src, len) ? hipErrorUnknown : hipSuccess;
+        return hipMemcpyAsync(dst, src, len, hipMemcpyHostToDevice, s);
+    };
+    e = h2d(b->d_keys + kb0, a.first(), bytes);
+    if (b->dev_rec && !b->borrowed_records && a.count) {
+        if (!b->stride) e = h2d((uint64_t *)b->d_raddr + n0, h_addr, a.count * 8);
+        if (b->approx) {
+            e = h2d((uint64_t *)b->d_rv8 + n0, h_value8, a.count * 8);
+            e = h2d((uint8_t *)b->d_rvl + n0, h_vlen, a.count);
+        }
+    }
     if (e == hipSuccess && !b->key_len && a.count) {  // a variable-length builder's offsets
         uint64_t *dst = b->d_off + n0 + 1;
         if (a.uni != 0xFFFFFFFFu) {
@@ -587,6 +627,7 @@ int add_copy_device(bsdb_builder *b, const AddBatch &a, uint64_t n0, uint64_t kb
     }
     if (e == hipSuccess) e = hipStreamSynchronize(s);  // the caller may reuse its buffers
     if (s) (void)hipStreamDestroy(s);
+    b->copying.fetch_sub(1);
     return e == hipSuccess ? BSDB_OK : hip_fail(e, "builder add copy", __LINE__);
 }
 
@@ -637,8 +678,12 @@ int builder_add(bsdb_builder *b, const AddBatch &a, const uint64_t *h_addr, cons
         }
         if (b->spill) return BSDB_OK;
     }
-    int rc = add_copy_device(b, a, n0, kb0);
+    const auto t0 = std::chrono::steady_clock::now();
+    int rc = add_copy_device(b, a, n0, kb0, h_addr, h_value8, h_vlen);
+    const auto t1 = std::chrono::steady_clock::now();
     add_copy_records(b, n0, a.count, h_addr, h_value8, h_vlen);
+    b->add_copy_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(t1 - t0).count();
+    b->add_rec_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t1).count();
     copying.unlock();
     if (rc) {
         std::lock_guard<std::mutex> gb(b->mu);
@@ -692,15 +737,25 @@ int builder_finish_locked(bsdb_builder *b, uint32_t width, uint32_t passes, cons
     void *sp_in = nullptr, *sp_out = nullptr;  // spill mode: a pass's uploaded segments, its compacted keys
     size_t sp_in_bytes = 0, sp_out_bytes = 0;
     bsdb_mph *p = nullptr;
+    // BSDB_BUILDER_PROFILE=1: the finish's phases on stderr
+    const bool prof = getenv("BSDB_BUILDER_PROFILE") != nullptr;
+    const auto t_start = std::chrono::steady_clock::now();
+    auto mark = [&](const char *what) {
+        if (prof)
+            fprintf(stderr, "[bsdb builder] finish %s at %.3f s\n", what,
+                    std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count());
+    };
     auto done = [&](int rc) {
         (void)hipStreamSynchronize(c->stream);
         for (void *q : {d_addr, d_v8, d_vl, slot_a[0], slot_a[1], sp_in, sp_out}) (void)hipFree(q);
         pop_o.finish();
         pop_a.finish();
-        if (getenv("BSDB_BUILDER_PROFILE") && fo.map)
+        if (prof && fo.map)
             fprintf(stderr, "[bsdb builder] index pages prefaulted in %.3f s (index_a %.3f s)\n", pop_o.seconds, pop_a.seconds);
+        mark("buffers released");
         if (close_out(fo) && !rc) rc = BSDB_EFILE;
         if (close_out(fao) && !rc) rc = BSDB_EFILE;
+        mark("files closed");
         if (rc && p) mph_release(p);
         if (!rc) *out = p;
         return rc;
@@ -722,6 +777,10 @@ int builder_finish_locked(bsdb_builder *b, uint32_t width, uint32_t passes, cons
     fo.pop = &pop_o;
     fao.pop = &pop_a;
     if ((rc = mph_alloc(c, n, width, &p))) return done(rc);
+    mark("files opened");
+    if (prof)
+        fprintf(stderr, "[bsdb builder] adds: device copies %.3f s, record copies %.3f s (thread totals)%s\n",
+                b->add_copy_ns.load() / 1e9, b->add_rec_ns.load() / 1e9, b->dev_rec ? ", records on the device" : "");
     if (n == 0) {  // E = {0}, no values beyond the trailing word (GOV:484)
         FIN_OK(hipMemsetAsync(p->E, 0, (p->m + 1) * 8, c->stream));
         FIN_OK(hipMemsetAsync(p->values, 0, p->values_words * 8, c->stream));
@@ -747,8 +806,17 @@ int builder_finish_locked(bsdb_builder *b, uint32_t width, uint32_t passes, cons
         size_t free_b = 0, total_b = 0;
         FIN_OK(hipMemGetInfo(&free_b, &total_b));
         const uint64_t rec_bytes = n * ((b->stride ? 0 : 8) + (b->approx ? 9 : 0));
-        const bool host_gather = getenv("BSDB_BUILDER_HOST_GATHER") != nullptr || rec_bytes > free_b / 4;
-        if (!host_gather) {
+        const bool host_gather = getenv("BSDB_BUILDER_HOST_GATHER") != nullptr || (!b->dev_rec && rec_bytes > free_b / 4);
+        if (!host_gather && b->dev_rec) {
+            // uploaded by the adds: the finish takes them over
+            d_addr = b->d_raddr;
+            d_v8 = b->d_rv8;
+            d_vl = b->d_rvl;
+            b->d_raddr = b->d_rv8 = b->d_rvl = nullptr;
+            b->raddr_cap = b->rv8_cap = b->rvl_cap = 0;
+            b->dev_rec = false;
+            dev_addr = (const uint64_t *)d_addr;
+        } else if (!host_gather) {
             const int dev = c->device;
             int up_rc = BSDB_OK;
             if (!b->stride && (dmalloc(&d_addr, n * 8) != hipSuccess || (up_rc = h2d_pageable(dev, d_addr, b->addr.p, n * 8))))
@@ -808,6 +876,7 @@ int builder_finish_locked(bsdb_builder *b, uint32_t width, uint32_t passes, cons
             };
         }
     }
+    mark("records placed");
     if (b->spill) {
         // Spill mode: pass p's keys are those of the 256 host segments that
         // can hold its buckets [b_lo, b_hi) -- the segment is sig0's top byte
@@ -855,6 +924,7 @@ int builder_finish_locked(bsdb_builder *b, uint32_t width, uint32_t passes, cons
     }
     rc = passes_build(c, src, n, width, passes, dev_addr, b->addr_base, b->addr_stride, p->E, p->values, p->sigbits,
                       sink, passes_used, c->stream);
+    mark("passes done");
     return done(rc);
 #undef FIN_OK
 }
@@ -865,6 +935,7 @@ void builder_release(bsdb_builder *b) {
     (void)hipFree(b->d_keys);
     (void)hipFree(b->d_off);
     (void)hipFree(b->d_stage);
+    builder_drop_dev_records(b);
     b->d_keys = nullptr;
     b->d_off = nullptr;
     b->d_stage = nullptr;
@@ -918,6 +989,19 @@ int builder_open(bsdb_ctx *c, uint32_t key_len, uint64_t key_capacity, uint64_t 
         ((!b->stride && !b->addr.reserve(key_capacity)) ||
          (b->approx && (!b->value8.reserve(key_capacity) || !b->vlen.reserve(key_capacity)))))
         rc = BSDB_ENOMEM;
+    if (!rc && !borrowed && key_capacity && (!b->stride || b->approx)) {
+        // the records on the device too, when they fit an eighth of the free HBM
+        std::lock_guard<std::mutex> g(c->mu);
+        size_t free_b = 0, total_b = 0;
+        const uint64_t cap = b->stride ? b->value8.cap : b->addr.cap;
+        const uint64_t want = cap * ((b->stride ? 0 : 8) + (b->approx ? 9 : 0));
+        if (hipSetDevice(c->device) == hipSuccess && hipMemGetInfo(&free_b, &total_b) == hipSuccess && want <= free_b / 8) {
+            b->dev_rec = (b->stride || dev_reserve(c, &b->d_raddr, &b->raddr_cap, 0, b->addr.cap * 8) == BSDB_OK) &&
+                         (!b->approx || (dev_reserve(c, &b->d_rv8, &b->rv8_cap, 0, b->value8.cap * 8) == BSDB_OK &&
+                                         dev_reserve(c, &b->d_rvl, &b->rvl_cap, 0, b->vlen.cap) == BSDB_OK));
+            if (!b->dev_rec) builder_drop_dev_records(b);
+        }
+    }
     if (rc) {
         builder_release(b);
         delete b;

@@ -42,28 +42,77 @@ namespace {
 
 constexpr uint32_t KV_PAGE = 4096;  // NativeFileIO.PAGE_SIZE
 
+// A growable array of plain values, never value-initialised (a partition's
+// parse output: written once, record by record).
+template <class T>
+struct PodBuf {
+    T *p = nullptr;
+    size_t n = 0, cap = 0;
+    PodBuf() = default;
+    PodBuf(const PodBuf &) = delete;
+    PodBuf &operator=(const PodBuf &) = delete;
+    ~PodBuf() { free(p); }
+    void reserve(size_t c) {
+        if (c <= cap) return;
+        T *q = (T *)realloc(p, c * sizeof(T));
+        if (!q) throw std::bad_alloc();
+        p = q;
+        cap = c;
+    }
+    T *room(size_t k) {  // space for k more
+        if (n + k > cap) reserve(std::max(n + k, cap + cap / 2 + 4096));
+        return p + n;
+    }
+    void release() {
+        free(p);
+        p = nullptr;
+        n = cap = 0;
+    }
+    size_t size() const { return n; }
+    T *data() const { return p; }
+    T *begin() const { return p; }
+    T *end() const { return p + n; }
+    T &operator[](size_t i) const { return p[i]; }
+};
+
 struct KvPart {
-    std::vector<uint8_t> blob;
-    std::vector<uint64_t> off{0};  // key offsets into blob, n + 1
-    std::vector<uint64_t> addr, value8;
-    std::vector<uint8_t> vlen;
+    PodBuf<uint8_t> blob;
+    PodBuf<uint64_t> off;  // key offsets into blob, n + 1
+    PodBuf<uint64_t> addr, value8;
+    PodBuf<uint8_t> vlen;
+    bool values = true;  // value8 / vlen wanted (index.approximate, bsdb_kv_scan)
     int rc = BSDB_OK;
+    KvPart() {
+        *off.room(1) = 0;
+        off.n = 1;
+    }
     void reserve(uint64_t records, uint64_t key_bytes) {
         blob.reserve(key_bytes);
         off.reserve(records + 1);
         addr.reserve(records);
-        value8.reserve(records);
-        vlen.reserve(records);
+        if (values) {
+            value8.reserve(records);
+            vlen.reserve(records);
+        }
     }
     void add(uint64_t a, const uint8_t *key, uint32_t kl, const uint8_t *val, uint32_t vl) {
-        blob.insert(blob.end(), key, key + kl);
-        off.push_back(blob.size());
-        addr.push_back(a);
+        memcpy(blob.room(kl), key, kl);
+        blob.n += kl;
+        off.room(1)[0] = blob.n;
+        off.n++;
+        addr.room(1)[0] = a;
+        addr.n++;
+        if (!values) return;
         uint64_t v = 0;
         const uint32_t h = vl < 8 ? vl : 8;
-        for (uint32_t i = 0; i < h; ++i) v |= (uint64_t)val[i] << (8 * i);
-        value8.push_back(v);
-        vlen.push_back((uint8_t)h);
+        if (h == 8)
+            memcpy(&v, val, 8);  // (little-endian: byte i at bits 8i, W:141)
+        else
+            for (uint32_t i = 0; i < h; ++i) v |= (uint64_t)val[i] << (8 * i);
+        value8.room(1)[0] = v;
+        value8.n++;
+        vlen.room(1)[0] = (uint8_t)h;
+        vlen.n++;
     }
 };
 
@@ -202,7 +251,7 @@ int bsdb_kv_scan(const char *kv_base, int partitions, int format, uint32_t block
             r->addr.insert(r->addr.end(), p.addr.begin(), p.addr.end());
             r->value8.insert(r->value8.end(), p.value8.begin(), p.value8.end());
             r->vlen.insert(r->vlen.end(), p.vlen.begin(), p.vlen.end());
-            std::vector<uint8_t>().swap(p.blob);  // (peak memory: one partition twice)
+            p.blob.release();  // (peak memory: one partition twice)
         }
         r->fixed_len = n && same ? fixed : 0;
         r->blob.resize(bytes + 16, 0);  // readable slack past the last key
@@ -269,19 +318,28 @@ int bsdb_kv_build_index(bsdb_ctx *c, const char *kv_base, int partitions, int fo
         if (stat(path.c_str(), &st) != 0) return BSDB_EFILE;
         file_bytes += (uint64_t)st.st_size;
     }
-    // records and key bytes per file byte, from the first 16 MiB of partition 0
+    // records and key bytes per file byte, from the start of EVERY partition
+    // (16 MiB in all, at least 64 KiB each): a first partition of shorter keys
+    // than the rest no longer under-sizes the device key area (a
+    // key area that still cannot grow makes the builder spill, not fail)
     double per_byte_keys = 0.0, per_byte_blob = 0.0;
     {
-        Mapped m;
-        KvPart sample;
-        const uint64_t limit = 16ull << 20;
-        int rc = map_file(std::string(kv_base) + ".0", m);
-        if (!rc) rc = format == 0 ? scan_compact(m, 0, sample, limit) : scan_blocked(m, 0, block_size, sample, limit);
-        if (rc) return rc;
-        const uint64_t seen = std::min<uint64_t>(m.size, limit);
+        const uint64_t each = std::max<uint64_t>(64ull << 10, (16ull << 20) / (uint64_t)partitions);
+        uint64_t seen = 0, keys = 0, blob = 0;
+        for (int p = 0; p < partitions; ++p) {
+            Mapped m;
+            KvPart sample;
+            sample.values = false;
+            int rc = map_file(std::string(kv_base) + "." + std::to_string(p), m);
+            if (!rc) rc = format == 0 ? scan_compact(m, (uint64_t)p, sample, each) : scan_blocked(m, (uint64_t)p, block_size, sample, each);
+            if (rc) return rc;
+            seen += std::min<uint64_t>(m.size, each);
+            keys += sample.addr.size();
+            blob += sample.blob.size();
+        }
         if (seen) {
-            per_byte_keys = (double)sample.addr.size() / (double)seen;
-            per_byte_blob = (double)sample.blob.size() / (double)seen;
+            per_byte_keys = (double)keys / (double)seen;
+            per_byte_blob = (double)blob / (double)seen;
         }
     }
     bsdb_builder *b = nullptr;
@@ -296,6 +354,7 @@ int bsdb_kv_build_index(bsdb_ctx *c, const char *kv_base, int partitions, int fo
     auto worker = [&] {
         for (int p; !err.load() && (p = next.fetch_add(1)) < partitions;) {
             KvPart part;
+            part.values = approximate != 0;  // (exact mode: no value bytes)
             const auto t0 = std::chrono::steady_clock::now();
             Mapped m;
             int r = map_file(std::string(kv_base) + "." + std::to_string(p), m);  // PKV:79-81

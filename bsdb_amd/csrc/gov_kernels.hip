@@ -38,6 +38,11 @@ constexpr int GS_PER_CU = 2;
 constexpr int GS_CMAX = 1664;    // keys per bucket solved in LDS (expected ~1500, sigma ~39)
 constexpr int GS_NVMAX = 1872;   // > vertex_offset span of GS_CMAX keys
 constexpr int GS_TINY = 12;      // brute-force buckets (only in sets of < ~1500 keys)
+#ifndef GOV_GJ_REG
+// the heavy system's Gauss-Jordan in registers (gauss_jordan_reg): needs the
+// VGPRs of two waves per SIMD (256-thread workgroups, two per CU)
+#define GOV_GJ_REG (GOV_THREADS <= 256)
+#endif
 #ifndef GOV_PICK_REPS
 // FVS: pairs of heavy hinges taken per stuck cascade (with the in x out pick
 // key, C2 at 6 / 8 / 12 / 16 / 20 / 24 / 28: 522 / 536 / 553 / 558 / 566–569 /
@@ -1206,6 +1211,35 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
         auto X = [&](uint32_t rr, uint32_t w, uint32_t q) -> uint64_t & { return scr[(size_t)(2 * w + q) * Lds::CMAX + rr]; };
         uint8_t *colval = L.b0;  // (Tarjan's arrays are dead here)
 
+        // The shared tail of both Gauss-Jordan forms below: each column's
+        // value from its pivot row, and the consistency of the rows without one.
+        auto gj_tail = [&](uint32_t n, auto &&X) -> bool {
+            int16_t *piv = L.a0;
+            uint8_t *used = L.b1;
+            // column cc's pivot row reads cf * x + (free columns, all 0) = rhs
+            // with cf in {1, 2} (every other pivot column eliminated), so
+            // x = cf * rhs mod 3; a row without a pivot is all zero and must
+            // read rhs = 0
+            const uint64_t rbit = 1ULL << (n & 63);
+            for (uint32_t cc = tid; cc < n; cc += GS_THREADS) {
+                const int pr = piv[cc];
+                if (pr < 0) {
+                    colval[cc] = 0;
+                    continue;
+                }
+                const uint64_t cbit = 1ULL << (cc & 63);
+                const uint32_t rhs = (X(pr, n >> 6, 0) & rbit) ? 1 : (X(pr, n >> 6, 1) & rbit) ? 2 : 0;
+                const uint32_t cf = (X(pr, cc >> 6, 1) & cbit) ? 2 : 1;
+                colval[cc] = (uint8_t)(cf * rhs % 3);
+            }
+            bool bad = false;
+            for (uint32_t rr = tid; rr < n; rr += GS_THREADS)
+                if (!used[rr] && ((X(rr, n >> 6, 0) | X(rr, n >> 6, 1)) & rbit)) bad = true;
+            const bool ok = !__syncthreads_or(bad);
+            if (!ok && tid == 0) L.flag = 0;
+            __syncthreads();
+            return ok;
+        };
         // Gauss-Jordan on rows 0..n-1 of X (n equations, n unknowns, the
         // right-hand side in column n), without row swaps: column cc's pivot
         // is the first unused row with a nonzero there, piv[cc] remembers it
@@ -1296,29 +1330,119 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
                     pc.add(GP_GJ_BARRIER, clock64() - tb);
                 }
             }
-            // column cc's pivot row reads cf * x + (free columns, all 0) = rhs
-            // with cf in {1, 2} (every other pivot column eliminated), so
-            // x = cf * rhs mod 3; a row without a pivot is all zero and must
-            // read rhs = 0
-            const uint64_t rbit = 1ULL << (n & 63);
-            for (uint32_t cc = tid; cc < n; cc += GS_THREADS) {
-                const int pr = piv[cc];
-                if (pr < 0) {
-                    colval[cc] = 0;
+            return gj_tail(n, X);
+        };
+        // The heavy system's Gauss-Jordan with each row in its own thread's
+        // registers (n <= GS_THREADS rows of H words a plane; the solver's
+        // 256-thread form has the VGPRs for it, GOV_GJ_REG): per column,
+        // every wave's lowest candidate row for the next pivot publishes its
+        // index and words in the wave's slot (double-buffered by column
+        // parity); after the column's one barrier every thread reads the
+        // waves' bids, takes the lowest row -- the pivot the LDS form's
+        // atomicMin picks -- reads its words from that wave's slot and
+        // eliminates in registers: two LDS round trips a column instead of the
+        // LDS form's chain of ~6.  Same pivots, same reduced
+        // rows (written back at the end), same tail.
+        auto gauss_jordan_reg = [&](uint32_t n, auto hw, auto &&X, uint64_t *slots) -> bool {
+            constexpr uint32_t H = decltype(hw)::value;
+            constexpr uint32_t NW = GS_THREADS / 64, SW = 2 * H + 1;  // a slot: the row index, then its words
+            int16_t *piv = L.a0;
+            uint8_t *used_m = L.b1;
+            const uint32_t rr = tid, lane = tid & 63, wv = tid >> 6;
+            const bool mine = rr < n;
+            uint64_t r1[H], r2[H];
+#pragma unroll
+            for (uint32_t w = 0; w < H; ++w) {
+                r1[w] = mine ? X(rr, w, 0) : 0;
+                r2[w] = mine ? X(rr, w, 1) : 0;
+            }
+            bool used = false;
+            uint32_t nfree = 0;
+            auto publish = [&](uint32_t c, uint32_t par) {  // the wave's lowest candidate for column c
+                bool cand = false;
+                if (mine && !used && c < n) {
+                    uint64_t t = 0;
+#pragma unroll
+                    for (uint32_t w = 0; w < H; ++w)
+                        if (w == (c >> 6)) t = r1[w] | r2[w];
+                    cand = ((t >> (c & 63)) & 1ULL) != 0;
+                }
+                const uint64_t bal = __builtin_amdgcn_ballot_w64(cand);
+                uint64_t *sl = slots + (size_t)(par * NW + wv) * SW;
+                if (!bal) {
+                    if (lane == 0) sl[0] = ~0ULL;
+                } else if (lane == (uint32_t)__builtin_ctzll(bal)) {
+                    sl[0] = rr;
+#pragma unroll
+                    for (uint32_t w = 0; w < H; ++w) {
+                        sl[1 + 2 * w] = r1[w];
+                        sl[2 + 2 * w] = r2[w];
+                    }
+                }
+            };
+            __syncthreads();  // (every row read before the slots, which may share its words, are written)
+            publish(0, 0);
+            __syncthreads();
+            for (uint32_t cc = 0; cc < n; ++cc) {
+                const uint32_t par = cc & 1;
+                uint64_t best = ~0ULL;
+                uint32_t bw = 0;
+#pragma unroll
+                for (uint32_t w = 0; w < NW; ++w) {
+                    const uint64_t b = slots[(size_t)(par * NW + w) * SW];
+                    if (b < best) {
+                        best = b;
+                        bw = w;
+                    }
+                }
+                if (best == ~0ULL) {  // a free column (uniform): x_cc = 0
+                    if (tid == 0) piv[cc] = -1;
+                    ++nfree;
+                    publish(cc + 1, par ^ 1u);
+                    __syncthreads();
                     continue;
                 }
-                const uint64_t cbit = 1ULL << (cc & 63);
-                const uint32_t rhs = (X(pr, n >> 6, 0) & rbit) ? 1 : (X(pr, n >> 6, 1) & rbit) ? 2 : 0;
-                const uint32_t cf = (X(pr, cc >> 6, 1) & cbit) ? 2 : 1;
-                colval[cc] = (uint8_t)(cf * rhs % 3);
+                const uint64_t *ps = slots + (size_t)(par * NW + bw) * SW;
+                uint64_t q1[H], q2[H];
+#pragma unroll
+                for (uint32_t w = 0; w < H; ++w) {
+                    q1[w] = ps[1 + 2 * w];
+                    q2[w] = ps[2 + 2 * w];
+                }
+                const uint32_t wc = cc >> 6;
+                const uint64_t bit = 1ULL << (cc & 63);
+                uint64_t pq2 = 0, f1 = 0, f2 = 0;
+#pragma unroll
+                for (uint32_t w = 0; w < H; ++w)
+                    if (w == wc) {
+                        pq2 = q2[w];
+                        f1 = r1[w] & bit;
+                        f2 = r2[w] & bit;
+                    }
+                const bool two = (pq2 & bit) != 0;  // pivot coefficient 2: its row normalised = planes swapped
+                if (tid == 0) piv[cc] = (int16_t)best;
+                if (rr == (uint32_t)best) {
+                    used = true;
+                } else if (mine && (f1 | f2)) {
+                    const bool sw = (f1 != 0) != two;  // subtract cf * (normalised pivot row)
+#pragma unroll
+                    for (uint32_t w = 0; w < H; ++w)
+                        if (w >= wc) gf3_add(r1[w], r2[w], sw ? q2[w] : q1[w], sw ? q1[w] : q2[w]);
+                }
+                publish(cc + 1, par ^ 1u);
+                __syncthreads();
             }
-            bool bad = false;
-            for (uint32_t rr = tid; rr < n; rr += GS_THREADS)
-                if (!used[rr] && ((X(rr, n >> 6, 0) | X(rr, n >> 6, 1)) & rbit)) bad = true;
-            const bool ok = !__syncthreads_or(bad);
-            if (!ok && tid == 0) L.flag = 0;
+            if (mine) {
+#pragma unroll
+                for (uint32_t w = 0; w < H; ++w) {
+                    X(rr, w, 0) = r1[w];
+                    X(rr, w, 1) = r2[w];
+                }
+                used_m[rr] = used ? 1 : 0;
+            }
+            if (tid == 0) L.nfree = nfree;
             __syncthreads();
-            return ok;
+            return gj_tail(n, X);
         };
         // Block equation of member i: cf*x_hinge + sum of its other vertices
         // = h (mod 3), h = the hinge's position in the edge, cf = its count.
@@ -1795,7 +1919,25 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
                 }
                 __syncthreads();
                 // (rows in X: words < 12 CMAX, below the forms)
-                const bool hok = hs_lds ? gauss_jordan(nH, HSL) : gauss_jordan(nH, X);
+                // the register form when the heavy rows are in LDS, one per
+                // thread, with room past them for the wave slots
+                constexpr uint32_t NWV = GS_THREADS / 64;
+                const bool reg = GOV_GJ_REG && hs_lds && nH <= (uint32_t)GS_THREADS &&
+                                 (size_t)2 * HW * nH + (size_t)2 * NWV * (2 * HW + 1) <= Lds::HS_WORDS;
+                bool hok;
+                if (reg) {
+                    uint64_t *slots = hsb + (size_t)2 * HW * nH;
+                    switch (HW) {
+                        case 1: hok = gauss_jordan_reg(nH, std::integral_constant<uint32_t, 1>{}, HSL, slots); break;
+                        case 2: hok = gauss_jordan_reg(nH, std::integral_constant<uint32_t, 2>{}, HSL, slots); break;
+                        case 3: hok = gauss_jordan_reg(nH, std::integral_constant<uint32_t, 3>{}, HSL, slots); break;
+                        case 4: hok = gauss_jordan_reg(nH, std::integral_constant<uint32_t, 4>{}, HSL, slots); break;
+                        case 5: hok = gauss_jordan_reg(nH, std::integral_constant<uint32_t, 5>{}, HSL, slots); break;
+                        default: hok = gauss_jordan_reg(nH, std::integral_constant<uint32_t, FW>{}, HSL, slots); break;
+                    }
+                } else {
+                    hok = hs_lds ? gauss_jordan(nH, HSL) : gauss_jordan(nH, X);
+                }
                 pc.lap(GP_FVS_GJ);
                 if (!hok) {
                     pc.add(GP_N_FAIL_INCONS, 1);

@@ -16,12 +16,13 @@ def main():
     ap.add_argument("--c4", action="store_true")
     ap.add_argument("--kv", action="store_true")
     ap.add_argument("--n", type=int, default=13_193_787_549)
+    ap.add_argument("--reps", type=int, default=1, help="kv leg repetitions in this process")
     args = ap.parse_args()
     import bench
     from bsdb_amd import Context
     ctx = Context(0)
     out = {}
-    if args.kv:
+    for _ in range(args.reps if args.kv else 0):
         out["e2e_c2_kv_to_disk"] = bench.e2e_c2_kv_to_disk(ctx, 100_000_000, 4)
         print(json.dumps(out["e2e_c2_kv_to_disk"]), flush=True)
     if args.c4:
