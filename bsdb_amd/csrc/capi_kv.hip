@@ -343,10 +343,13 @@ int bsdb_kv_build_index(bsdb_ctx *c, const char *kv_base, int partitions, int fo
         }
     }
     bsdb_builder *b = nullptr;
+    const double t_sampled = since();
     int rc = builder_open(c, 0, (uint64_t)(per_byte_keys * (double)file_bytes * 1.02) + 1024,
                           (uint64_t)(per_byte_blob * (double)file_bytes * 1.02) + 65536, approximate, 0, 0, &b);
     if (rc) return rc;
     std::unique_ptr<bsdb_builder, int (*)(bsdb_builder *)> guard(b, bsdb_builder_free);
+    const double t_opened = since();
+    std::vector<double> tl((size_t)partitions * 3, 0.0);  // per partition: scan start, scan end, add end
     // (partitions in flight = threads: the host memory bound)
     const int T = std::max(1, std::min(threads > 0 ? threads : usable_cpus(), partitions));
     std::atomic<int> next{0};
@@ -368,6 +371,8 @@ int bsdb_kv_build_index(bsdb_ctx *c, const char *kv_base, int partitions, int fo
                 }
             }
             scan_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
+            tl[3 * (size_t)p] = std::chrono::duration<double>(t0 - t_start).count();
+            tl[3 * (size_t)p + 1] = since();
             const uint64_t k = part.addr.size();
             uint32_t uni = 0;
             if (!r) r = var_batch_lengths(part.off.data(), k, &uni);
@@ -382,6 +387,7 @@ int bsdb_kv_build_index(bsdb_ctx *c, const char *kv_base, int partitions, int fo
                 a.uni = uni;
                 r = builder_add(b, a, part.addr.data(), part.value8.data(), part.vlen.data());
                 add_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t1).count();
+                tl[3 * (size_t)p + 2] = since();
             }
             if (r) {
                 int expect = BSDB_OK;
@@ -395,6 +401,12 @@ int bsdb_kv_build_index(bsdb_ctx *c, const char *kv_base, int partitions, int fo
     for (auto &t : th) t.join();
     if ((rc = err.load())) return rc;
     const double t_scanned = since();
+    if (prof) {
+        fprintf(stderr, "[bsdb kv] sampled %.3f s, builder open %.3f s, %d threads; partitions (scan start, scan end, add end):",
+                t_sampled, t_opened, T);
+        for (int p = 0; p < partitions; ++p) fprintf(stderr, " %d:(%.3f %.3f %.3f)", p, tl[3 * p], tl[3 * p + 1], tl[3 * p + 2]);
+        fprintf(stderr, "\n");
+    }
     rc = bsdb_builder_finish(b, width, 0, index_path, index_a_path, out, nullptr);
     if (prof)
         fprintf(stderr, "[bsdb kv] %llu records: scan+add %.3f s (thread scan %.3f s, thread adds %.3f s), finish %.3f s\n",

@@ -4,7 +4,7 @@
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 OUT=gpurun_out/${TAG:-round}; mkdir -p $OUT
-timeout -k 10 700 python -u -m pytest tests -m gpu -x -v --timeout 600 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 || { tail -n 40 $OUT/pytest_gpu.log; exit 1; }
+timeout -k 10 800 python -u -m pytest tests -m gpu -x -v --timeout 700 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 || { tail -n 40 $OUT/pytest_gpu.log; exit 1; }
 tail -n 2 $OUT/pytest_gpu.log
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { tail -n 20 $OUT/smoke.log; exit 4; }
 tail -n 1 $OUT/smoke.log
