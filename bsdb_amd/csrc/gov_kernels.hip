@@ -43,6 +43,9 @@ constexpr int GS_TINY = 12;      // brute-force buckets (only in sets of < ~1500
 // VGPRs of two waves per SIMD (256-thread workgroups, two per CU)
 #define GOV_GJ_REG (GOV_THREADS <= 256)
 #endif
+#ifndef GOV_GJ_REG_HW
+#define GOV_GJ_REG_HW 6  // the widest heavy rows (64-bit words a plane) the register form takes
+#endif
 #ifndef GOV_PICK_REPS
 // FVS: pairs of heavy hinges taken per stuck cascade (with the in x out pick
 // key, C2 at 6 / 8 / 12 / 16 / 20 / 24 / 28: 522 / 536 / 553 / 558 / 566–569 /
@@ -1922,7 +1925,7 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
                 // the register form when the heavy rows are in LDS, one per
                 // thread, with room past them for the wave slots
                 constexpr uint32_t NWV = GS_THREADS / 64;
-                const bool reg = GOV_GJ_REG && hs_lds && nH <= (uint32_t)GS_THREADS &&
+                const bool reg = GOV_GJ_REG && hs_lds && nH <= (uint32_t)GS_THREADS && HW <= GOV_GJ_REG_HW &&
                                  (size_t)2 * HW * nH + (size_t)2 * NWV * (2 * HW + 1) <= Lds::HS_WORDS;
                 bool hok;
                 if (reg) {
@@ -1931,9 +1934,9 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
                         case 1: hok = gauss_jordan_reg(nH, std::integral_constant<uint32_t, 1>{}, HSL, slots); break;
                         case 2: hok = gauss_jordan_reg(nH, std::integral_constant<uint32_t, 2>{}, HSL, slots); break;
                         case 3: hok = gauss_jordan_reg(nH, std::integral_constant<uint32_t, 3>{}, HSL, slots); break;
-                        case 4: hok = gauss_jordan_reg(nH, std::integral_constant<uint32_t, 4>{}, HSL, slots); break;
-                        case 5: hok = gauss_jordan_reg(nH, std::integral_constant<uint32_t, 5>{}, HSL, slots); break;
-                        default: hok = gauss_jordan_reg(nH, std::integral_constant<uint32_t, FW>{}, HSL, slots); break;
+                        case 4: hok = gauss_jordan_reg(nH, std::integral_constant<uint32_t, GOV_GJ_REG_HW < 4 ? 1 : 4>{}, HSL, slots); break;
+                        case 5: hok = gauss_jordan_reg(nH, std::integral_constant<uint32_t, GOV_GJ_REG_HW < 5 ? 1 : 5>{}, HSL, slots); break;
+                        default: hok = gauss_jordan_reg(nH, std::integral_constant<uint32_t, GOV_GJ_REG_HW < 6 ? 1 : FW>{}, HSL, slots); break;
                     }
                 } else {
                     hok = hs_lds ? gauss_jordan(nH, HSL) : gauss_jordan(nH, X);

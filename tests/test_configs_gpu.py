@@ -306,6 +306,46 @@ def test_c2_passes_build_equals_oracle_field_for_field(ctx, capfd):
 
 
 @pytest.mark.timeout(900)
+def test_c5_varlen_passes_build_equals_oracle_on_1e8_keys(ctx):
+    """The same pin for C5's shape: the first 1e8 C5 keys (8-64 B Zipf,
+    device-generated = the oracle's recipe), hash.checksum.bits = 16, through
+    the variable-length bucket-range pass path (2 passes): E, values and the
+    16-bit checksums field for field against the oracle's build, and every
+    index slot against the W:129-145 restatement."""
+    n, width, passes, base, stride = 100_000_000, 16, 2, 0x2000, 64
+    hb, ho = O.gen_keys_var(0, n)
+
+    def oracle():
+        sig = O.hash_var(hb, ho)
+        rc, E, vals, sb, _ = O.gov_build_mt(sig, width, THREADS)
+        ranks = O.lookup_batch_mt(sig, n, E, vals, width, sb, True, THREADS) if rc == 0 else None
+        return rc, E, vals, sb, ranks
+
+    th, box = in_background(oracle)
+    blob, off = ctx.gen_keys_var(0, n)
+    d_index = torch.zeros(n, dtype=torch.int64, device="cuda")
+    E, vals, sb, used = ctx.mph_build_index_passes(blob, 0, n, width, passes, offsets=off, addr_base=base,
+                                                   addr_stride=stride, index=d_index)
+    torch.cuda.synchronize()
+    assert used == passes
+    head = blob[: int(ho[1000])].cpu().numpy()
+    hE, hv, hs, hidx = u64(E), u64(vals), u64(sb), u64(d_index)
+    del blob, off, E, vals, sb, d_index
+    torch.cuda.empty_cache()
+    np.testing.assert_array_equal(head, hb[: int(ho[1000])])   # (the device generator is the oracle's recipe)
+    th.join()
+    rc, oE, ov, osb, ranks = box["r"]
+    assert rc == 0
+    np.testing.assert_array_equal(hE, oE)
+    np.testing.assert_array_equal(hv, ov)
+    np.testing.assert_array_equal(hs[: osb.size], osb)
+    exp = np.zeros(n, np.uint64)
+    exp[ranks] = (np.uint64(base) + np.uint64(stride) * np.arange(n, dtype=np.uint64)).byteswap()
+    np.testing.assert_array_equal(hidx, exp)
+    solver_report("c5_varlen_passes_1e8", n, hE)
+
+
+@pytest.mark.timeout(900)
 def test_c3_approx_host_passes_equals_oracle_on_a_2e8_slice(ctx, tmp_path):
     """VERDICT r4 item 1, C3's mode: index.approximate = true from host
     buffers through the streaming builder's bucket-range passes (4 passes),
