@@ -15,3 +15,6 @@ tail -n 1 $OUT/bench.json | cut -c1-400
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/prof -o bench --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu --no-full-build > $OUT/prof_bench.json 2> $OUT/prof_bench.err || { tail -n 20 $OUT/prof_bench.err; exit 3; }
 find $OUT/prof -name "*kernel_stats.csv" -exec cp {} $OUT/kernel_stats.csv \;
 head -n 12 $OUT/kernel_stats.csv | cut -c1-160
+[ -n "$NOKV" ] && exit 0
+BSDB_BUILDER_PROFILE=1 timeout -k 10 300 python -u tools/e2e_legs.py --kv --reps 2 > $OUT/kv.json 2> $OUT/kv.err || { tail -n 20 $OUT/kv.err; exit 5; }
+grep "bsdb kv\|adds:" $OUT/kv.err
