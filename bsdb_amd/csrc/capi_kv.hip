@@ -356,16 +356,17 @@ int bsdb_kv_build_index(bsdb_ctx *c, const char *kv_base, int partitions, int fo
     if (rc) return rc;
     std::unique_ptr<bsdb_builder, int (*)(bsdb_builder *)> guard(b, bsdb_builder_free);
     const double t_opened = since();
-    std::vector<double> tl((size_t)partitions * 3, 0.0);  // per partition: scan start, scan end, add end
+    std::vector<double> tl((size_t)partitions * 4, 0.0);  // per partition: scan start, scan end, add end, released
     // (partitions in flight = threads: the host memory bound)
     const int T = std::max(1, std::min(threads > 0 ? threads : usable_cpus(), partitions));
     std::atomic<int> next{0};
     std::atomic<int> err{BSDB_OK};
     auto worker = [&] {
         for (int p; !err.load() && (p = next.fetch_add(1)) < partitions;) {
+          {
+            const auto t0 = std::chrono::steady_clock::now();
             KvPart part;
             part.values = approximate != 0;  // (exact mode: no value bytes)
-            const auto t0 = std::chrono::steady_clock::now();
             Mapped m;
             int r = map_file(std::string(kv_base) + "." + std::to_string(p), m);  // PKV:79-81
             if (!r) {
@@ -378,8 +379,8 @@ int bsdb_kv_build_index(bsdb_ctx *c, const char *kv_base, int partitions, int fo
                 }
             }
             scan_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
-            tl[3 * (size_t)p] = std::chrono::duration<double>(t0 - t_start).count();
-            tl[3 * (size_t)p + 1] = since();
+            tl[4 * (size_t)p] = std::chrono::duration<double>(t0 - t_start).count();
+            tl[4 * (size_t)p + 1] = since();
             const uint64_t k = part.addr.size();
             uint32_t uni = 0;
             if (!r) r = var_batch_lengths(part.off.data(), k, &uni);
@@ -394,12 +395,14 @@ int bsdb_kv_build_index(bsdb_ctx *c, const char *kv_base, int partitions, int fo
                 a.uni = uni;
                 r = builder_add(b, a, part.addr.data(), part.value8.data(), part.vlen.data());
                 add_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t1).count();
-                tl[3 * (size_t)p + 2] = since();
+                tl[4 * (size_t)p + 2] = since();
             }
             if (r) {
                 int expect = BSDB_OK;
                 err.compare_exchange_strong(expect, r);
             }
+          }  // (the partition's mapping and parse arrays released)
+          tl[4 * (size_t)p + 3] = since();
         }
     };
     std::vector<std::thread> th;
@@ -409,9 +412,10 @@ int bsdb_kv_build_index(bsdb_ctx *c, const char *kv_base, int partitions, int fo
     if ((rc = err.load())) return rc;
     const double t_scanned = since();
     if (prof) {
-        fprintf(stderr, "[bsdb kv] sampled %.3f s, builder open %.3f s, %d threads; partitions (scan start, scan end, add end):",
+        fprintf(stderr, "[bsdb kv] sampled %.3f s, builder open %.3f s, %d threads; partitions (scan start, scan end, add end, released):",
                 t_sampled, t_opened, T);
-        for (int p = 0; p < partitions; ++p) fprintf(stderr, " %d:(%.3f %.3f %.3f)", p, tl[3 * p], tl[3 * p + 1], tl[3 * p + 2]);
+        for (int p = 0; p < partitions; ++p)
+            fprintf(stderr, " %d:(%.3f %.3f %.3f %.3f)", p, tl[4 * p], tl[4 * p + 1], tl[4 * p + 2], tl[4 * p + 3]);
         fprintf(stderr, "\n");
     }
     rc = bsdb_builder_finish(b, width, 0, index_path, index_a_path, out, nullptr);
