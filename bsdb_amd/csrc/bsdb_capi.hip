@@ -28,6 +28,8 @@
 #include <shared_mutex>
 #include <string>
 #include <thread>
+#include <condition_variable>
+#include <deque>
 #include <vector>
 
 #include "../../include/bsdb_mi355x.h"

@@ -597,8 +597,19 @@ int add_copy_device(bsdb_builder *b, const AddBatch &a, uint64_t n0, uint64_t kb
     // one add alone: the runtime's pageable copy (56 GB/s for C4's 4 GiB
     // batches); several at once: each through pinned pieces
     const bool bounce = b->copying.fetch_add(1) > 0;
+    // (BSDB_ADD_COPY=register, measurement: the source pinned in place for
+    // its copy instead of the pinned pieces)
+    static const bool reg_copy = getenv("BSDB_ADD_COPY") && !strcmp(getenv("BSDB_ADD_COPY"), "register");
     auto h2d = [&](void *dst, const void *src, size_t len) -> hipError_t {
         if (!len || e != hipSuccess) return e;
+        if (bounce && reg_copy) {
+            hipError_t r = hipHostRegister(const_cast<void *>(src), len, hipHostRegisterDefault);
+            if (r != hipSuccess) return h2d_bounce(s, dst, src, len) ? hipErrorUnknown : hipSuccess;
+            r = hipMemcpyAsync(dst, src, len, hipMemcpyHostToDevice, s);
+            if (r == hipSuccess) r = hipStreamSynchronize(s);
+            const hipError_t u = hipHostUnregister(const_cast<void *>(src));
+            return r != hipSuccess ? r : u;
+        }
         if (bounce) return h2d_bounce(s, dst, src, len) ? hipErrorUnknown : hipSuccess;
         return hipMemcpyAsync(dst, src, len, hipMemcpyHostToDevice, s);
     };

@@ -356,7 +356,45 @@ int bsdb_kv_build_index(bsdb_ctx *c, const char *kv_base, int partitions, int fo
     if (rc) return rc;
     std::unique_ptr<bsdb_builder, int (*)(bsdb_builder *)> guard(b, bsdb_builder_free);
     const double t_opened = since();
-    std::vector<double> tl((size_t)partitions * 4, 0.0);  // per partition: scan start, scan end, add end, released
+    std::vector<double> tl((size_t)partitions * 4, 0.0);  // per partition: scan start, scan end, add end, handed off
+    // A partition's file mapping (~600 MB at C2) and parse arrays (~400 MB)
+    // are released by one background thread while the other partitions and
+    // the finish run: released by the scanning thread they took 50-180 ms
+    // after its add (munmap, serialised by the address-space lock;
+    // profiles/r5/kv/kv_release_timeline.err).  Joined before returning.
+    struct KvWork {
+        Mapped m;
+        KvPart part;
+    };
+    std::mutex reap_mu;
+    std::condition_variable reap_cv;
+    std::deque<std::unique_ptr<KvWork>> reap_q;
+    bool reap_end = false;
+    std::thread reaper([&] {
+        for (;;) {
+            std::unique_ptr<KvWork> w;
+            {
+                std::unique_lock<std::mutex> g(reap_mu);
+                reap_cv.wait(g, [&] { return reap_end || !reap_q.empty(); });
+                if (reap_q.empty()) return;
+                w = std::move(reap_q.front());
+                reap_q.pop_front();
+            }
+            w.reset();
+        }
+    });
+    auto reaper_join = [&] {
+        {
+            std::lock_guard<std::mutex> g(reap_mu);
+            reap_end = true;
+        }
+        reap_cv.notify_one();
+        if (reaper.joinable()) reaper.join();
+    };
+    struct ReaperGuard {
+        std::function<void()> f;
+        ~ReaperGuard() { f(); }
+    } reaper_guard{reaper_join};
     // (partitions in flight = threads: the host memory bound)
     const int T = std::max(1, std::min(threads > 0 ? threads : usable_cpus(), partitions));
     std::atomic<int> next{0};
@@ -365,9 +403,15 @@ int bsdb_kv_build_index(bsdb_ctx *c, const char *kv_base, int partitions, int fo
         for (int p; !err.load() && (p = next.fetch_add(1)) < partitions;) {
           {
             const auto t0 = std::chrono::steady_clock::now();
-            KvPart part;
+            std::unique_ptr<KvWork> work(new (std::nothrow) KvWork());
+            if (!work) {
+                int expect = BSDB_OK;
+                err.compare_exchange_strong(expect, BSDB_ENOMEM);
+                break;
+            }
+            KvPart &part = work->part;
+            Mapped &m = work->m;
             part.values = approximate != 0;  // (exact mode: no value bytes)
-            Mapped m;
             int r = map_file(std::string(kv_base) + "." + std::to_string(p), m);  // PKV:79-81
             if (!r) {
                 try {
@@ -401,7 +445,12 @@ int bsdb_kv_build_index(bsdb_ctx *c, const char *kv_base, int partitions, int fo
                 int expect = BSDB_OK;
                 err.compare_exchange_strong(expect, r);
             }
-          }  // (the partition's mapping and parse arrays released)
+            {
+                std::lock_guard<std::mutex> g(reap_mu);
+                reap_q.push_back(std::move(work));  // (released by the reaper)
+            }
+            reap_cv.notify_one();
+          }
           tl[4 * (size_t)p + 3] = since();
         }
     };
@@ -419,9 +468,13 @@ int bsdb_kv_build_index(bsdb_ctx *c, const char *kv_base, int partitions, int fo
         fprintf(stderr, "\n");
     }
     rc = bsdb_builder_finish(b, width, 0, index_path, index_a_path, out, nullptr);
+    const double t_finished = since();
+    reaper_join();
     if (prof)
-        fprintf(stderr, "[bsdb kv] %llu records: scan+add %.3f s (thread scan %.3f s, thread adds %.3f s), finish %.3f s\n",
-                (unsigned long long)b->n, t_scanned, scan_ns.load() / 1e9, add_ns.load() / 1e9, since() - t_scanned);
+        fprintf(stderr, "[bsdb kv] %llu records: scan+add %.3f s (thread scan %.3f s, thread adds %.3f s), finish %.3f s, "
+                        "partitions released %.3f s after\n",
+                (unsigned long long)b->n, t_scanned, scan_ns.load() / 1e9, add_ns.load() / 1e9, t_finished - t_scanned,
+                since() - t_finished);
     return rc;
 }
 

@@ -635,7 +635,11 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
     pc.start();
     pc.add(GP_N_SEEDS, 1);
     const bool tiny = cnt <= GS_TINY;
-    if (tid == 0) L.flag = 0;
+    if (tid == 0) {
+        L.flag = 0;
+        L.pivot = 0;  // (core edges and core vertices after the peel, below)
+        L.nscc = 0;
+    }
     for (uint32_t v = tid; v < nv; v += GS_THREADS) {
         L.deg[v] = 0;
         L.xe[v] = 0;
@@ -702,6 +706,33 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
     }
     const int rounds = r;
     pc.lap(GP_PEEL);
+    // An orientation gives every core edge its own hinge among the core's
+    // vertices, so a core with more edges than vertices has none: the seed
+    // fails here (GOV:425-432, sux4j's unorientable), as the augmenting paths
+    // below would find after the greedy and every BFS.  Measured on the
+    // oracle's edges (3e5 keys' buckets, every seed up to the solving one),
+    // this count catches every unorientable attempt of a random set, and they
+    // are ~18 % of attempts.  Same outcome, so the same seeds and output.
+    {
+        uint32_t ce = 0, cv = 0;
+        for (uint32_t k = tid; k < cnt; k += GS_THREADS) ce += L.round_of[k] < 0 ? 1u : 0u;
+        for (uint32_t v = tid; v < nv; v += GS_THREADS) cv += L.deg[v] != 0u ? 1u : 0u;
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) {
+            ce += (uint32_t)__shfl_xor((int)ce, d, 64);
+            cv += (uint32_t)__shfl_xor((int)cv, d, 64);
+        }
+        if ((tid & 63) == 0) {
+            atomicAdd(&L.pivot, ce);
+            atomicAdd(&L.nscc, cv);
+        }
+        __syncthreads();
+        const bool over = L.pivot > L.nscc;  // (uniform; both words are next written after the BFS's barrier)
+        if (over) {
+            pc.add(GP_N_FAIL_ORIENT, 1);
+            return false;
+        }
+    }
 
     // ---- 2. orientation of the core: greedy (wave 0), then BFS augmenting paths (wave 0).
     // A vertex is seen by BFS number `epoch` when seen[v] == epoch (the peel
