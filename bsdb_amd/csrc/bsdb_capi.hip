@@ -293,7 +293,9 @@ struct Populator {
         if (!base || !bytes || getenv("BSDB_NO_PREFAULT")) return;
         th = std::thread([this, base, bytes] {
             const auto t0 = std::chrono::steady_clock::now();
-            constexpr uint64_t STEP = 64ull << 20;
+            // (16 MiB steps: each holds the address-space lock, which other
+            // threads' mmap/munmap and thread creation wait for)
+            constexpr uint64_t STEP = 16ull << 20;
             constexpr int MADV_POPULATE_WRITE_ = 23;
             bool madv = true;
             for (uint64_t o = 0; o < bytes && !stop.load(std::memory_order_relaxed); o += STEP) {

@@ -351,11 +351,21 @@ int bsdb_kv_build_index(bsdb_ctx *c, const char *kv_base, int partitions, int fo
     }
     bsdb_builder *b = nullptr;
     const double t_sampled = since();
-    int rc = builder_open(c, 0, (uint64_t)(per_byte_keys * (double)file_bytes * 1.02) + 1024,
-                          (uint64_t)(per_byte_blob * (double)file_bytes * 1.02) + 65536, approximate, 0, 0, &b);
-    if (rc) return rc;
-    std::unique_ptr<bsdb_builder, int (*)(bsdb_builder *)> guard(b, bsdb_builder_free);
-    const double t_opened = since();
+    int rc = BSDB_OK;
+    std::unique_ptr<bsdb_builder, int (*)(bsdb_builder *)> guard(nullptr, bsdb_builder_free);
+    double t_opened = 0;
+    // The builder opens on this thread after the scan threads have started:
+    // its record arrays' populator holds the address-space lock in steps,
+    // and thread stacks created behind it started the scans ~45 ms late.  A
+    // scan thread waits for the open only at its first add.
+    std::mutex open_mu;
+    std::condition_variable open_cv;
+    int open_state = 1;  // 1 pending, 0 open, < 0 the open's error
+    auto wait_open = [&]() -> int {
+        std::unique_lock<std::mutex> g(open_mu);
+        open_cv.wait(g, [&] { return open_state != 1; });
+        return open_state;
+    };
     std::vector<double> tl((size_t)partitions * 4, 0.0);  // per partition: scan start, scan end, add end, handed off
     // A partition's file mapping (~600 MB at C2) and parse arrays (~400 MB)
     // are released by one background thread while the other partitions and
@@ -428,6 +438,7 @@ int bsdb_kv_build_index(bsdb_ctx *c, const char *kv_base, int partitions, int fo
             const uint64_t k = part.addr.size();
             uint32_t uni = 0;
             if (!r) r = var_batch_lengths(part.off.data(), k, &uni);
+            if (!r) r = wait_open();
             if (!r) {
                 // (adds from the scan threads run concurrently: the builder
                 // reserves each one's ranges under its lock and copies outside it)
@@ -456,8 +467,18 @@ int bsdb_kv_build_index(bsdb_ctx *c, const char *kv_base, int partitions, int fo
     };
     std::vector<std::thread> th;
     for (int t = 1; t < T; ++t) th.emplace_back(worker);
-    worker();
+    rc = builder_open(c, 0, (uint64_t)(per_byte_keys * (double)file_bytes * 1.02) + 1024,
+                      (uint64_t)(per_byte_blob * (double)file_bytes * 1.02) + 65536, approximate, 0, 0, &b);
+    guard.reset(rc ? nullptr : b);
+    t_opened = since();
+    {
+        std::lock_guard<std::mutex> g(open_mu);
+        open_state = rc ? rc : 0;
+    }
+    open_cv.notify_all();
+    if (!rc) worker();
     for (auto &t : th) t.join();
+    if (rc) return rc;
     if ((rc = err.load())) return rc;
     const double t_scanned = since();
     if (prof) {
