@@ -60,6 +60,9 @@ struct HostVec {
                     : mmap(nullptr, nc * sizeof(T), PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE,
                            -1, 0);
         if (q == MAP_FAILED) return false;
+        // 2 MiB pages where the kernel offers them: the populator and the
+        // release walk 512x fewer pages (a 1e8-key build's addresses: 800 MB)
+        if (!p) (void)madvise(q, nc * sizeof(T), MADV_HUGEPAGE);
         p = (T *)q;
         cap = nc;
         return true;
@@ -131,6 +134,9 @@ struct bsdb_builder {
         pop_addr.finish();
         pop_v8.finish();
     }
+    // called by the finish once its files and device arrays are allocated
+    // (the kv.db build holds its partitions' release until then)
+    std::function<void()> on_opened;
     ~bsdb_builder() { stop_prefault(); }
 };
 
@@ -748,6 +754,7 @@ int builder_finish_locked(bsdb_builder *b, uint32_t width, uint32_t passes, cons
     void *sp_in = nullptr, *sp_out = nullptr;  // spill mode: a pass's uploaded segments, its compacted keys
     size_t sp_in_bytes = 0, sp_out_bytes = 0;
     bsdb_mph *p = nullptr;
+    std::thread host_rel;  // the host record arrays' release, once the device copies took over
     // BSDB_BUILDER_PROFILE=1: the finish's phases on stderr
     const bool prof = getenv("BSDB_BUILDER_PROFILE") != nullptr;
     const auto t_start = std::chrono::steady_clock::now();
@@ -757,7 +764,10 @@ int builder_finish_locked(bsdb_builder *b, uint32_t width, uint32_t passes, cons
                     std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count());
     };
     auto done = [&](int rc) {
+        if (b->on_opened) b->on_opened();  // (every exit releases the caller's hold)
+        b->on_opened = nullptr;
         (void)hipStreamSynchronize(c->stream);
+        if (host_rel.joinable()) host_rel.join();
         for (void *q : {d_addr, d_v8, d_vl, slot_a[0], slot_a[1], sp_in, sp_out}) (void)hipFree(q);
         pop_o.finish();
         pop_a.finish();
@@ -783,12 +793,17 @@ int builder_finish_locked(bsdb_builder *b, uint32_t width, uint32_t passes, cons
     if (index_path && ((rc = open_out(index_path, n * 8, &fo)) ||
                        (index_a_path && (rc = open_out(index_a_path, b->approx ? n * 8 : 0, &fao)))))
         return done(rc);
+    mark("index file created");
+    // (the device arrays before the populators start: an allocation maps
+    // into the address space, which each populate step holds)
+    if ((rc = mph_alloc(c, n, width, &p))) return done(rc);
     pop_o.start(fo.map, fo.bytes, fo.fd, 0);
     pop_a.start(fao.map, fao.bytes, fao.fd, 0);
     fo.pop = &pop_o;
     fao.pop = &pop_a;
-    if ((rc = mph_alloc(c, n, width, &p))) return done(rc);
     mark("files opened");
+    if (b->on_opened) b->on_opened();
+    b->on_opened = nullptr;
     if (prof)
         fprintf(stderr, "[bsdb builder] adds: device copies %.3f s, record copies %.3f s (thread totals)%s\n",
                 b->add_copy_ns.load() / 1e9, b->add_rec_ns.load() / 1e9, b->dev_rec ? ", records on the device" : "");
@@ -827,6 +842,14 @@ int builder_finish_locked(bsdb_builder *b, uint32_t width, uint32_t passes, cons
             b->raddr_cap = b->rv8_cap = b->rvl_cap = 0;
             b->dev_rec = false;
             dev_addr = (const uint64_t *)d_addr;
+            // the host copies are dead: released beside the passes (a 1e8-key
+            // build's 800 MB took ~45 ms after them)
+            host_rel = std::thread([b] {
+                b->stop_prefault();
+                b->addr.release();
+                b->value8.release();
+                b->vlen.release();
+            });
         } else if (!host_gather) {
             const int dev = c->device;
             int up_rc = BSDB_OK;
@@ -941,12 +964,16 @@ int builder_finish_locked(bsdb_builder *b, uint32_t width, uint32_t passes, cons
 }
 
 void builder_release(bsdb_builder *b) {
+    const auto t0 = std::chrono::steady_clock::now();
     b->stop_prefault();
     (void)hipSetDevice(b->c->device);
     (void)hipFree(b->d_keys);
     (void)hipFree(b->d_off);
     (void)hipFree(b->d_stage);
     builder_drop_dev_records(b);
+    if (getenv("BSDB_BUILDER_PROFILE"))
+        fprintf(stderr, "[bsdb builder] release: prefault stopped, device freed in %.3f s\n",
+                std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
     b->d_keys = nullptr;
     b->d_off = nullptr;
     b->d_stage = nullptr;
@@ -1153,7 +1180,11 @@ int bsdb_builder_finish(bsdb_builder *b, uint32_t width, uint32_t passes, const 
         Ordered ord(c, c->stream);
         rc = builder_finish_locked(b, width, passes, index_path, index_a_path, out, passes_used);
         b->finished = true;
+        const auto t_rel = std::chrono::steady_clock::now();
         builder_release(b);  // the keys leave HBM: the MPHF stays
+        if (getenv("BSDB_BUILDER_PROFILE"))
+            fprintf(stderr, "[bsdb builder] builder released in %.3f s\n",
+                    std::chrono::duration<double>(std::chrono::steady_clock::now() - t_rel).count());
     }
     return rc;
 }

@@ -42,6 +42,21 @@ namespace {
 
 constexpr uint32_t KV_PAGE = 4096;  // NativeFileIO.PAGE_SIZE
 
+// munmap in 32 MiB steps: each munmap holds the address-space lock, which
+// another thread's mmap (the finish opening the index file) waits for; a
+// partition's ~1 GB released at once held it for tens of ms at a time.
+// A releasing thread may be held between steps (the kv.db reaper, while the
+// finish allocates: its device allocations waited up to 0.12 s behind it).
+thread_local const std::atomic<bool> *t_unmap_hold = nullptr;
+void unmap_in_steps(void *p, size_t bytes) {
+    constexpr size_t STEP = 32ull << 20;
+    for (size_t o = 0; o < bytes; o += STEP) {
+        while (t_unmap_hold && t_unmap_hold->load(std::memory_order_acquire))
+            std::this_thread::sleep_for(std::chrono::microseconds(200));
+        munmap((uint8_t *)p + o, std::min(STEP, bytes - o));
+    }
+}
+
 // A growable array of plain values, never value-initialised (a partition's
 // parse output: written once, record by record).  An anonymous mapping in
 // 2 MiB pages where the kernel offers them (MADV_HUGEPAGE): a partition's
@@ -71,7 +86,7 @@ struct PodBuf {
         return p + n;
     }
     void release() {
-        if (p) munmap(p, bytes_of(cap));
+        if (p) unmap_in_steps(p, bytes_of(cap));
         p = nullptr;
         n = cap = 0;
     }
@@ -127,7 +142,69 @@ struct Mapped {
     const uint8_t *p = nullptr;
     size_t size = 0;
     ~Mapped() {
-        if (p && size) munmap((void *)p, size);
+        if (p && size) unmap_in_steps((void *)p, (size + 4095) & ~(size_t)4095);
+    }
+    const uint8_t *at(uint64_t pos, uint64_t) const { return p + pos; }  // (the scanners check the bounds)
+};
+
+// A kv.db file read through a 4 MiB window (pread) instead of mapped whole:
+// the scan parses the same bytes, but no 600 MB file mapping is faulted in
+// and torn down per partition.  Those munmaps (page-cache pages, 4 KiB each)
+// took 100+ ms a partition under the address-space lock, which the finish's
+// device allocations and populators wait for (profiles/r5/kv/).
+struct FileWindow {
+    static constexpr uint64_t CHUNK = 4ull << 20;
+    int fd = -1;
+    uint64_t size = 0;
+    uint8_t *buf = nullptr;
+    uint64_t cap = 0, wb = 0, wl = 0;  // buffer bytes; the window [wb, wb + wl) of the file
+    FileWindow() = default;
+    FileWindow(const FileWindow &) = delete;
+    FileWindow &operator=(const FileWindow &) = delete;
+    ~FileWindow() {
+        if (fd >= 0) close(fd);
+        if (buf) munmap(buf, cap);
+    }
+    int open_file(const std::string &path) {
+        fd = open(path.c_str(), O_RDONLY);
+        if (fd < 0) return BSDB_EFILE;
+        struct stat st;
+        if (fstat(fd, &st) != 0) return BSDB_EFILE;
+        size = (uint64_t)st.st_size;
+        (void)posix_fadvise(fd, 0, 0, POSIX_FADV_SEQUENTIAL);
+        return BSDB_OK;
+    }
+    // the file's bytes [pos, pos + len), or nullptr past its end / on a read error
+    const uint8_t *at(uint64_t pos, uint64_t len) {
+        if (pos >= wb && pos + len <= wb + wl) return buf + (pos - wb);
+        if (pos + len > size) return nullptr;
+        const uint64_t want = std::min(std::max(CHUNK, len), size - pos);
+        if (want > cap) {
+            if (buf) munmap(buf, cap);
+            const uint64_t nc = (want + (2ull << 20) - 1) & ~((2ull << 20) - 1);
+            void *q = mmap(nullptr, nc, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+            if (q == MAP_FAILED) {
+                buf = nullptr;
+                cap = wl = 0;
+                return nullptr;
+            }
+            (void)madvise(q, nc, MADV_HUGEPAGE);
+            buf = (uint8_t *)q;
+            cap = nc;
+        }
+        uint64_t got = 0;
+        while (got < want) {
+            const ssize_t r = pread(fd, buf + got, want - got, (off_t)(pos + got));
+            if (r < 0 && errno == EINTR) continue;
+            if (r <= 0) {
+                wl = 0;
+                return nullptr;
+            }
+            got += (uint64_t)r;
+        }
+        wb = pos;
+        wl = got;
+        return buf;
     }
 };
 
@@ -155,50 +232,89 @@ int map_file(const std::string &path, Mapped &m) {
 }
 
 // SCK:55-70.  Records starting at or past `limit` are not read (a sample).
-int scan_compact(const Mapped &m, uint64_t part, KvPart &out, uint64_t limit = UINT64_MAX) {
+// Src: a whole mapping (Mapped) or a read window (FileWindow).
+template <class Src>
+int scan_compact(Src &m, uint64_t part, KvPart &out, uint64_t limit = UINT64_MAX) {
     uint64_t pos = 0;
     while (pos < m.size && pos < limit) {
-        const uint32_t kl = m.p[pos];
+        const uint8_t *h = m.at(pos, std::min<uint64_t>(3, m.size - pos));
+        if (!h) return BSDB_EFILE;
+        const uint32_t kl = h[0];
         if (kl == 0) break;
         if (pos + 3 > m.size) return BSDB_EFILE;
-        const uint32_t vl = ((uint32_t)m.p[pos + 1] << 8) | m.p[pos + 2];
+        const uint32_t vl = ((uint32_t)h[1] << 8) | h[2];
         if (pos + 3 + kl + vl > m.size) return BSDB_EFILE;
-        out.add(part << 56 | pos, m.p + pos + 3, kl, m.p + pos + 3 + kl, vl);
+        const uint8_t *r = m.at(pos, 3 + (uint64_t)kl + vl);
+        if (!r) return BSDB_EFILE;
+        out.add(part << 56 | pos, r + 3, kl, r + 3 + kl, vl);
         pos += 3 + (uint64_t)kl + vl;
     }
     return BSDB_OK;
 }
 
 // BKV:84-121
-int scan_blocked(const Mapped &m, uint64_t part, uint32_t block, KvPart &out, uint64_t limit = UINT64_MAX) {
+template <class Src>
+int scan_blocked(Src &m, uint64_t part, uint32_t block, KvPart &out, uint64_t limit = UINT64_MAX) {
     uint64_t position = 0;
     while (position < m.size && position < limit) {
         const uint64_t end = std::min<uint64_t>(m.size, position + block);  // readBlockAt: up to one block
         uint64_t next = block;
         uint64_t o = position;
         while (o < end) {
-            const uint32_t kl = m.p[o];
+            const uint8_t *h = m.at(o, 1);
+            if (!h) return BSDB_EFILE;
+            const uint32_t kl = h[0];
             if (kl == 0) break;
             if (o + 3 + kl > end) return BSDB_EFILE;
-            const uint32_t vl = ((uint32_t)m.p[o + 1] << 8) | m.p[o + 2];
+            if (!(h = m.at(o, 3))) return BSDB_EFILE;
+            const uint32_t vl = ((uint32_t)h[1] << 8) | h[2];
             const uint32_t rec_off = (uint32_t)(o - position);
-            if (o + 3 + kl + vl <= end) {
-                out.add(part << 56 | (uint64_t)(block / KV_PAGE) << 48 | (position / KV_PAGE) << 16 | rec_off,
-                        m.p + o + 3, kl, m.p + o + 3 + kl, vl);
-                o += 3 + (uint64_t)kl + vl;
+            const uint64_t rec = 3 + (uint64_t)kl + vl;
+            if (o + rec <= end) {
+                const uint8_t *r = m.at(o, rec);
+                if (!r) return BSDB_EFILE;
+                out.add(part << 56 | (uint64_t)(block / KV_PAGE) << 48 | (position / KV_PAGE) << 16 | rec_off, r + 3,
+                        kl, r + 3 + kl, vl);
+                o += rec;
             } else {
                 // a large record alone in a page-aligned block (BKV:104-109)
-                const uint64_t rec = 3 + (uint64_t)kl + vl;
                 next = (rec + KV_PAGE - 1) / KV_PAGE * KV_PAGE;
-                if (position + rec > m.size) return BSDB_EFILE;
-                out.add(part << 56 | (next / KV_PAGE) << 48 | (position / KV_PAGE) << 16 | rec_off, m.p + o + 3, kl,
-                        m.p + o + 3 + kl, vl);
+                if (position + rec > m.size || o + rec > m.size) return BSDB_EFILE;
+                const uint8_t *r = m.at(o, rec);
+                if (!r) return BSDB_EFILE;
+                out.add(part << 56 | (next / KV_PAGE) << 48 | (position / KV_PAGE) << 16 | rec_off, r + 3, kl,
+                        r + 3 + kl, vl);
                 break;
             }
         }
         position += next;
     }
     return BSDB_OK;
+}
+
+// one partition's file, mapped whole (BSDB_KV_READ=window: through the
+// read window, measured slower: thread scan 2.3-2.9 s against 1.2-1.7 s for
+// C2's 8 partitions, profiles/r5/kv/callH_*)
+// (on_size: called with the file's size before the scan, e.g. to reserve)
+int scan_file(const std::string &path, int format, uint64_t part, uint32_t block, KvPart &out,
+              uint64_t limit = UINT64_MAX, uint64_t *size = nullptr,
+              const std::function<void(uint64_t)> &on_size = nullptr, Mapped *keep = nullptr) {
+    static const bool use_mmap = !getenv("BSDB_KV_READ") || strcmp(getenv("BSDB_KV_READ"), "window") != 0;
+    if (use_mmap) {
+        Mapped local;
+        Mapped &m = keep ? *keep : local;  // (keep: the caller releases the mapping)
+        int rc = map_file(path, m);
+        if (size) *size = m.size;
+        if (!rc && on_size) on_size(m.size);
+        if (!rc) rc = format == 0 ? scan_compact(m, part, out, limit) : scan_blocked(m, part, block, out, limit);
+        return rc;
+    }
+    FileWindow w;
+    int rc = w.open_file(path);
+    if (size) *size = w.size;
+    if (!rc && on_size) on_size(w.size);
+    if (!rc) rc = format == 0 ? scan_compact(w, part, out, limit) : scan_blocked(w, part, block, out, limit);
+    return rc;
 }
 
 }  // namespace
@@ -216,11 +332,8 @@ int bsdb_kv_scan(const char *kv_base, int partitions, int format, uint32_t block
     std::atomic<int> next{0};
     auto worker = [&] {
         for (int p; (p = next.fetch_add(1)) < partitions;) {
-            Mapped m;
             const std::string path = std::string(kv_base) + "." + std::to_string(p);  // PKV:79-81
-            int rc = map_file(path, m);
-            if (!rc) rc = format == 0 ? scan_compact(m, (uint64_t)p, parts[p]) : scan_blocked(m, (uint64_t)p, block_size, parts[p]);
-            parts[p].rc = rc;
+            parts[p].rc = scan_file(path, format, (uint64_t)p, block_size, parts[p]);
         }
     };
     std::vector<std::thread> th;
@@ -334,13 +447,13 @@ int bsdb_kv_build_index(bsdb_ctx *c, const char *kv_base, int partitions, int fo
         const uint64_t each = std::max<uint64_t>(64ull << 10, (16ull << 20) / (uint64_t)partitions);
         uint64_t seen = 0, keys = 0, blob = 0;
         for (int p = 0; p < partitions; ++p) {
-            Mapped m;
             KvPart sample;
             sample.values = false;
-            int rc = map_file(std::string(kv_base) + "." + std::to_string(p), m);
-            if (!rc) rc = format == 0 ? scan_compact(m, (uint64_t)p, sample, each) : scan_blocked(m, (uint64_t)p, block_size, sample, each);
+            uint64_t size = 0;
+            const int rc = scan_file(std::string(kv_base) + "." + std::to_string(p), format, (uint64_t)p, block_size,
+                                     sample, each, &size);
             if (rc) return rc;
-            seen += std::min<uint64_t>(m.size, each);
+            seen += std::min<uint64_t>(size, each);
             keys += sample.addr.size();
             blob += sample.blob.size();
         }
@@ -368,19 +481,22 @@ int bsdb_kv_build_index(bsdb_ctx *c, const char *kv_base, int partitions, int fo
     };
     std::vector<double> tl((size_t)partitions * 4, 0.0);  // per partition: scan start, scan end, add end, handed off
     // A partition's file mapping (~600 MB at C2) and parse arrays (~400 MB)
-    // are released by one background thread while the other partitions and
-    // the finish run: released by the scanning thread they took 50-180 ms
-    // after its add (munmap, serialised by the address-space lock;
-    // profiles/r5/kv/kv_release_timeline.err).  Joined before returning.
+    // are released by one background thread while
+    // the other partitions and the finish run: released by the scanning
+    // thread they took 50-180 ms after its add (munmap, serialised by the
+    // address-space lock; profiles/r5/kv/kv_release_timeline.err).  Joined
+    // before returning.
     struct KvWork {
-        Mapped m;
+        Mapped m;  // (the read-window form: none)
         KvPart part;
     };
     std::mutex reap_mu;
     std::condition_variable reap_cv;
     std::deque<std::unique_ptr<KvWork>> reap_q;
     bool reap_end = false;
+    std::atomic<bool> reap_hold{false};  // set from the finish's start until its files are open
     std::thread reaper([&] {
+        t_unmap_hold = &reap_hold;
         for (;;) {
             std::unique_ptr<KvWork> w;
             {
@@ -394,6 +510,7 @@ int bsdb_kv_build_index(bsdb_ctx *c, const char *kv_base, int partitions, int fo
         }
     });
     auto reaper_join = [&] {
+        reap_hold.store(false, std::memory_order_release);
         {
             std::lock_guard<std::mutex> g(reap_mu);
             reap_end = true;
@@ -420,17 +537,16 @@ int bsdb_kv_build_index(bsdb_ctx *c, const char *kv_base, int partitions, int fo
                 break;
             }
             KvPart &part = work->part;
-            Mapped &m = work->m;
             part.values = approximate != 0;  // (exact mode: no value bytes)
-            int r = map_file(std::string(kv_base) + "." + std::to_string(p), m);  // PKV:79-81
-            if (!r) {
-                try {
-                    part.reserve((uint64_t)(per_byte_keys * (double)m.size * 1.05) + 64,
-                                 (uint64_t)(per_byte_blob * (double)m.size * 1.05) + 4096);
-                    r = format == 0 ? scan_compact(m, (uint64_t)p, part) : scan_blocked(m, (uint64_t)p, block_size, part);
-                } catch (const std::bad_alloc &) {
-                    r = BSDB_ENOMEM;
-                }
+            int r;
+            try {
+                r = scan_file(std::string(kv_base) + "." + std::to_string(p), format, (uint64_t)p, block_size, part,  // PKV:79-81
+                              UINT64_MAX, nullptr, [&](uint64_t size) {
+                                  part.reserve((uint64_t)(per_byte_keys * (double)size * 1.05) + 64,
+                                               (uint64_t)(per_byte_blob * (double)size * 1.05) + 4096);
+                              }, &work->m);
+            } catch (const std::bad_alloc &) {
+                r = BSDB_ENOMEM;
             }
             scan_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
             tl[4 * (size_t)p] = std::chrono::duration<double>(t0 - t_start).count();
@@ -488,7 +604,12 @@ int bsdb_kv_build_index(bsdb_ctx *c, const char *kv_base, int partitions, int fo
             fprintf(stderr, " %d:(%.3f %.3f %.3f %.3f)", p, tl[4 * p], tl[4 * p + 1], tl[4 * p + 2], tl[4 * p + 3]);
         fprintf(stderr, "\n");
     }
+    reap_hold.store(true, std::memory_order_release);
+    // (BSDB_KV_REAP_HOLD=finish, measurement: held for the whole finish)
+    static const bool hold_all = getenv("BSDB_KV_REAP_HOLD") && !strcmp(getenv("BSDB_KV_REAP_HOLD"), "finish");
+    if (!hold_all) b->on_opened = [&] { reap_hold.store(false, std::memory_order_release); };
     rc = bsdb_builder_finish(b, width, 0, index_path, index_a_path, out, nullptr);
+    reap_hold.store(false, std::memory_order_release);
     const double t_finished = since();
     reaper_join();
     if (prof)

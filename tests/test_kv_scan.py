@@ -6,6 +6,8 @@ BlockedKVWriter's layouts); the scan must return them in partition order
 addresses the reference's partitionForEach hands to buildIndex
 (SimpleCompactKVWriter.java:55-70, BlockedKVWriter.java:84-136)."""
 import os
+import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -86,6 +88,31 @@ def test_blocked_layout_with_large_records(tmp_path, block):
     # a record's address names its block (pages, position) and offset (BlockedKVWriter.java:124-136)
     a = s["addr"]
     assert set(((a >> np.uint64(48)) & np.uint64(0xFF)).tolist()) >= {block // 4096, 2, 3}
+
+
+@pytest.mark.parametrize("read", ["mapped", "window"])
+def test_files_longer_than_the_read_window(tmp_path, read):
+    """Files longer than the 4 MiB read window (capi_kv.hip FileWindow, the
+    BSDB_KV_READ=window form; mapped whole by default): records straddling
+    the window's end, in both layouts.  The library reads the knob once, so
+    the window form runs in a child process."""
+    if read == "window" and os.environ.get("BSDB_KV_READ") != "window":
+        env = dict(os.environ, BSDB_KV_READ="window")
+        r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-p", "no:cacheprovider",
+                            f"{__file__}::test_files_longer_than_the_read_window[window]"],
+                           env=env, capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+        return
+    kb, ko, vb, vo = records(60_000, 5)  # ~11 MB in one partition: two refills
+    base = str(tmp_path / "kv.db")
+    addr = kvfiles.write_compact(base, 1, kb, ko, vb, vo)
+    assert os.path.getsize(base + ".0") > 2 * (4 << 20)
+    check(kv_scan(base, 1, 0), kb, ko, vb, vo, addr, 1)
+    kb, ko, vb, vo = records(30_000, 6, big_every=97)
+    base = str(tmp_path / "kvb.db")
+    addr = kvfiles.write_blocked(base, 1, kb, ko, vb, vo, 8192)
+    assert os.path.getsize(base + ".0") > (4 << 20)
+    check(kv_scan(base, 1, 1, 8192), kb, ko, vb, vo, addr, 1)
 
 
 def test_bad_inputs(tmp_path):
