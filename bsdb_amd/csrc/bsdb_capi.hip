@@ -1375,11 +1375,14 @@ static int gov_build_impl(bsdb_ctx *c, const GovSrc &src, uint64_t n_global, uin
     }
     const uint32_t big_cap = (uint32_t)(n_local / (GS_CMAX + 1) + 1);
     if ((rc = grow(&c->g_big, &c->g_big_bytes, (size_t)big_cap * 4))) return rc;
-    // BSDB_GOV_ONE_PER_CU=1 (measurement only): one solver workgroup per CU
-    // (grid and LDS padding), to price the second one
-    const bool one_per_cu = getenv("BSDB_GOV_ONE_PER_CU") != nullptr;
+    // BSDB_GOV_ONE_PER_CU=1 / BSDB_GOV_PER_CU=k (measurement only): k < GS_PER_CU
+    // solver workgroups per CU (grid and LDS padding), to price the others
+    int per_cu = GS_PER_CU;
+    if (getenv("BSDB_GOV_ONE_PER_CU")) per_cu = 1;
+    if (getenv("BSDB_GOV_PER_CU")) per_cu = std::max(1, std::min(GS_PER_CU, atoi(getenv("BSDB_GOV_PER_CU"))));
+    const size_t lds_pad = per_cu < GS_PER_CU ? (160 * 1024 / (per_cu + 1) + 1024 - sizeof(SolveLds)) & ~(size_t)1023 : 0;
     const uint32_t solve_grid = (uint32_t)std::max<uint64_t>(
-        1, std::min<uint64_t>(nb, (uint64_t)c->num_cus * (one_per_cu ? 1 : GS_PER_CU)));
+        1, std::min<uint64_t>(nb, (uint64_t)c->num_cus * per_cu));
     if ((rc = grow(&c->g_scratch, &c->g_scratch_bytes, (size_t)solve_grid * solve_scratch_words<SolveLds>() * 8)))
         return rc;
     uint64_t *sorted = (uint64_t *)c->g_sorted;
@@ -1485,19 +1488,20 @@ static int gov_build_impl(bsdb_ctx *c, const GovSrc &src, uint64_t n_global, uin
     }
     // (the phase counters are compiled only into k_gov_solve<true>)
     const void *solve_fn = gprof ? (const void *)k_gov_solve<true> : (const void *)k_gov_solve<false>;
-    if (one_per_cu) HIP_OK(hipFuncSetAttribute(solve_fn, hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024));
+    if (lds_pad) HIP_OK(hipFuncSetAttribute(solve_fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_pad));
     if (gprof)
-        k_gov_solve<true><<<solve_grid, GS_THREADS, one_per_cu ? 64 * 1024 : 0, s>>>(sa);  // A8
+        k_gov_solve<true><<<solve_grid, GS_THREADS, lds_pad, s>>>(sa);  // A8
     else
-        k_gov_solve<false><<<solve_grid, GS_THREADS, one_per_cu ? 64 * 1024 : 0, s>>>(sa);
+        k_gov_solve<false><<<solve_grid, GS_THREADS, lds_pad, s>>>(sa);
     if (nbig) HIP_OK(hipStreamWaitEvent(s, c->big_ev[1], 0));
     if (gprof) {
         std::vector<uint64_t> h((size_t)solve_grid * GP_N);
         HIP_OK(hipMemcpyAsync(h.data(), d_prof, h.size() * 8, hipMemcpyDeviceToHost, s));
         HIP_OK(hipStreamSynchronize(s));
-        int per_cu = 0;
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_gov_solve<true>, GS_THREADS, 0);
-        fprintf(stderr, "[gov-profile] solver workgroups per CU: %d (LDS %zu B each)\n", per_cu, sizeof(SolveLds));
+        int occ = 0;
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_gov_solve<true>, GS_THREADS, lds_pad);
+        fprintf(stderr, "[gov-profile] solver workgroups per CU: %d (LDS %zu B each + %zu padding), grid %u\n", occ,
+                sizeof(SolveLds), lds_pad, solve_grid);
         print_gov_profile(h, solve_grid, m);
     }
     const MphView v{d_E, d_values, nullptr, n_global, mult, width};

@@ -34,9 +34,17 @@ constexpr int GS_THREADS = GOV_THREADS;
 // Two solver workgroups per CU (LDS <= 80 KiB each): one's single-wave
 // phases (greedy, BFS, FVS selection) overlap the other's.  4.2 sigma above
 // the mean bucket; larger buckets (~1e-5 of them) take the global-slab path.
-constexpr int GS_PER_CU = 2;
-constexpr int GS_CMAX = 1664;    // keys per bucket solved in LDS (expected ~1500, sigma ~39)
-constexpr int GS_NVMAX = 1872;   // > vertex_offset span of GS_CMAX keys
+#ifndef GOV_PER_CU
+#define GOV_PER_CU 2
+#endif
+#ifndef GOV_CMAX
+#define GOV_CMAX 1664
+#endif
+// (GOV_PER_CU / GOV_CMAX other than 2 / 1664: measurement builds only,
+// tools/build_variant.sh, with BSDB_PROBE_BUCKET_SIZE)
+constexpr int GS_PER_CU = GOV_PER_CU;
+constexpr int GS_CMAX = GOV_CMAX;    // keys per bucket solved in LDS (expected ~1500, sigma ~39)
+constexpr int GS_NVMAX = GS_CMAX + GS_CMAX / 8;   // > vertex_offset span of GS_CMAX keys (1872)
 constexpr int GS_TINY = 12;      // brute-force buckets (only in sets of < ~1500 keys)
 #ifndef GOV_GJ_REG
 // the heavy system's Gauss-Jordan in registers (gauss_jordan_reg): needs the
@@ -559,10 +567,14 @@ static_assert(SolveLds::NVMAX == GS_NVMAX && SolveLds::WMAX == GS_WMAX, "LDS lay
 static_assert(sizeof(SolveLds) + 64 <= 160 * 1024 / GS_PER_CU, "GS_PER_CU solver workgroups per CU");
 // per-workgroup global scratch of the dense phase (bit-sliced rows, forms)
 template <class Lds>
-constexpr size_t solve_scratch_words() { return (size_t)2 * Lds::CMAX * Lds::WMAX; }
 // FVS null vectors (bytes) at word 30 CMAX of the scratch, past the forms
-// (words [16, 28) CMAX) and the reverse dependency CSR ([28, 29.5) CMAX)
-static_assert(30 * 8 + NB_MAX <= 8 * 2 * GS_WMAX, "FVS null-vector basis fits the dense scratch");
+// (words [16, 28) CMAX) and the reverse dependency CSR ([28, 29.5) CMAX):
+// within the dense rows' words at production sizes
+constexpr size_t solve_scratch_words() {
+    const size_t dense = (size_t)2 * Lds::CMAX * Lds::WMAX, fvs = ((size_t)30 * 8 + NB_MAX) * Lds::CMAX / 8;
+    return dense > fvs ? dense : fvs;
+}
+static_assert(GS_CMAX != 1664 || 30 * 8 + NB_MAX <= 8 * 2 * GS_WMAX, "FVS null-vector basis fits the dense scratch");
 
 __device__ __forceinline__ void gf3_add(uint64_t &x1, uint64_t &x2, uint64_t y1, uint64_t y2) {
     const uint64_t a1 = x1, a2 = x2;

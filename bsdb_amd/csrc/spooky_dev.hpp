@@ -12,7 +12,13 @@ namespace bsdb {
 
 constexpr uint64_t SC = 0x9e3779b97f4a7c13ULL;  // spooky.c:39
 constexpr uint64_t OFFSET_MASK = ~0ULL >> 8;    // GOV:157
+#ifndef BSDB_PROBE_BUCKET_SIZE
 constexpr uint32_t BUCKET_SIZE = 1500;          // GOV:281
+#else
+// (measurement builds only, tools/build_variant.sh: a different mean bucket
+// to price the solver's LDS footprint; never the product library)
+constexpr uint32_t BUCKET_SIZE = BSDB_PROBE_BUCKET_SIZE;
+#endif
 
 // 64-bit rotate by a constant as two v_alignbit_b32 (the generic shift/or form
 // costs 2 v_lshl*_b64 + 2 v_or_b32).

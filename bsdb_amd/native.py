@@ -295,7 +295,7 @@ class Context:
     def gov_build(self, sig, width: int, stream=None):
         import torch
         n = sig.shape[0]
-        m = n // 1500 + 1
+        m = num_buckets(n)
         E = torch.empty(m + 1, dtype=torch.int64, device=sig.device)
         values = torch.empty(int(lib().bsdb_values_words(n)), dtype=torch.int64, device=sig.device)
         sigbits = torch.empty((n * width + 63) // 64 + 1, dtype=torch.int64, device=sig.device) if width else None
@@ -308,7 +308,7 @@ class Context:
         """F2: (E, values, sigbits, rank) -- rank[i] = getLong of sig[i], from the solve."""
         import torch
         n = sig.shape[0]
-        m = n // 1500 + 1
+        m = num_buckets(n)
         E = torch.empty(m + 1, dtype=torch.int64, device=sig.device)
         values = torch.empty(int(lib().bsdb_values_words(n)), dtype=torch.int64, device=sig.device)
         sigbits = torch.empty((n * width + 63) // 64 + 1, dtype=torch.int64, device=sig.device) if width else None
@@ -337,7 +337,7 @@ class Context:
         import torch
         import numpy as np
         dev = keys.device
-        m = n // 1500 + 1
+        m = num_buckets(n)
         E = torch.empty(m + 1, dtype=torch.int64, device=dev)
         values = torch.empty(int(lib().bsdb_values_words(n)), dtype=torch.int64, device=dev)
         sigbits = torch.empty((n * width + 63) // 64 + 1, dtype=torch.int64, device=dev) if width else None
@@ -861,7 +861,7 @@ class Multi:
         import numpy as np
         keys_np = np.ascontiguousarray(keys_np, np.uint8)
         n = keys_np.size // key_len
-        E = np.zeros(n // 1500 + 2, np.uint64)
+        E = np.zeros(num_buckets(n) + 1, np.uint64)
         _check("bsdb_multi_histogram_fixed", lib().bsdb_multi_histogram_fixed(
             self._h, keys_np.ctypes.data, key_len, n, seed & (2**64 - 1), E.ctypes.data))
         return E
@@ -869,14 +869,14 @@ class Multi:
     def histogram_var(self, blob_np, off_np, seed: int = 0):
         import numpy as np
         blob_np, off_np, n = Context._var_host_args(blob_np, off_np)
-        E = np.zeros(n // 1500 + 2, np.uint64)
+        E = np.zeros(num_buckets(n) + 1, np.uint64)
         _check("bsdb_multi_histogram_var", lib().bsdb_multi_histogram_var(
             self._h, blob_np.ctypes.data, off_np.ctypes.data, n, seed & (2**64 - 1), E.ctypes.data))
         return E
 
     def _build_outputs(self, n: int, width: int):
         import numpy as np
-        E = np.zeros(n // 1500 + 2, np.uint64)
+        E = np.zeros(num_buckets(n) + 1, np.uint64)
         vals = np.zeros(int(lib().bsdb_values_words(n)), np.uint64)
         sb = np.zeros((n * width + 63) // 64 + 1, np.uint64) if width else None
         return E, vals, sb

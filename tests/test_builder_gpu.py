@@ -233,6 +233,45 @@ def test_empty_builder(ctx, tmp_path):
     b.close(); m.close()
 
 
+_WRITE_FAIL_CHILD = r"""
+import resource, signal, sys
+import numpy as np
+sys.path.insert(0, sys.argv[1])
+import oracle as O
+from bsdb_amd.native import BsdbError, Context
+signal.signal(signal.SIGXFSZ, signal.SIG_IGN)  # (a write past the limit then fails with EFBIG)
+ctx = Context(0)
+n = 200_000
+keys = O.gen_keys13(0, n)
+addr = np.arange(n, dtype=np.uint64)
+resource.setrlimit(resource.RLIMIT_FSIZE, (1 << 16, resource.getrlimit(resource.RLIMIT_FSIZE)[1]))
+for path in sys.argv[2:]:
+    b = ctx.builder(13)
+    b.add_fixed(keys, 13, addr)
+    try:
+        b.finish(4, path, None)
+        print("ok", path)
+    except BsdbError as e:
+        print("code", e.code, path)
+    b.close()
+"""
+
+
+def test_index_write_failures_return_efile(tmp_path):
+    """an index file the file system cannot hold is an error code,
+    not a SIGBUS from a mapped store: a regular file past RLIMIT_FSIZE (its
+    size reservation fails, 1.6 MB > 64 KiB) and /dev/full (written with
+    pwrite: ENOSPC).  In a child process, which must survive both."""
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", _WRITE_FAIL_CHILD, repo, str(tmp_path / "i.db"), "/dev/full"],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    lines = [l.split() for l in r.stdout.splitlines() if l.startswith(("ok", "code"))]
+    assert lines == [["code", "-9", str(tmp_path / "i.db")], ["code", "-9", "/dev/full"]], r.stdout
+
+
 def test_index_open_out_of_memory_returns(ctx, tmp_path):
     """bsdb_index_open whose second pass buffer (index_a) cannot be
     allocated must return ENOMEM, not deadlock on the context lock."""
