@@ -236,7 +236,7 @@ def test_empty_builder(ctx, tmp_path):
 _WRITE_FAIL_CHILD = r"""
 import resource, signal, sys
 import numpy as np
-sys.path.insert(0, sys.argv[1])
+sys.path[:0] = [sys.argv[1], sys.argv[1] + "/oracle"]
 import oracle as O
 from bsdb_amd.native import BsdbError, Context
 signal.signal(signal.SIGXFSZ, signal.SIG_IGN)  # (a write past the limit then fails with EFBIG)
