@@ -104,6 +104,17 @@ struct KvPart {
     PodBuf<uint8_t> vlen;
     bool values = true;  // value8 / vlen wanted (index.approximate, bsdb_kv_scan)
     int rc = BSDB_OK;
+    // streamed parse (the kv.db build): every `chunk` records the scanner
+    // calls flush(), which adds them to the builder and resets the arrays
+    uint64_t chunk = UINT64_MAX;
+    std::function<int()> flush;
+    void reset_records() {
+        blob.n = 0;
+        off.n = 1;  // (off[0] == 0: offsets restart with the blob)
+        addr.n = 0;
+        value8.n = 0;
+        vlen.n = 0;
+    }
     KvPart() {
         *off.room(1) = 0;
         off.n = 1;
@@ -248,6 +259,10 @@ int scan_compact(Src &m, uint64_t part, KvPart &out, uint64_t limit = UINT64_MAX
         if (!r) return BSDB_EFILE;
         out.add(part << 56 | pos, r + 3, kl, r + 3 + kl, vl);
         pos += 3 + (uint64_t)kl + vl;
+        if (out.addr.n >= out.chunk) {
+            const int f = out.flush();
+            if (f) return f;
+        }
     }
     return BSDB_OK;
 }
@@ -276,6 +291,10 @@ int scan_blocked(Src &m, uint64_t part, uint32_t block, KvPart &out, uint64_t li
                 out.add(part << 56 | (uint64_t)(block / KV_PAGE) << 48 | (position / KV_PAGE) << 16 | rec_off, r + 3,
                         kl, r + 3 + kl, vl);
                 o += rec;
+                if (out.addr.n >= out.chunk) {
+                    const int f = out.flush();
+                    if (f) return f;
+                }
             } else {
                 // a large record alone in a page-aligned block (BKV:104-109)
                 next = (rec + KV_PAGE - 1) / KV_PAGE * KV_PAGE;
@@ -284,6 +303,10 @@ int scan_blocked(Src &m, uint64_t part, uint32_t block, KvPart &out, uint64_t li
                 if (!r) return BSDB_EFILE;
                 out.add(part << 56 | (next / KV_PAGE) << 48 | (position / KV_PAGE) << 16 | rec_off, r + 3, kl,
                         r + 3 + kl, vl);
+                if (out.addr.n >= out.chunk) {
+                    const int f = out.flush();
+                    if (f) return f;
+                }
                 break;
             }
         }
@@ -480,6 +503,9 @@ int bsdb_kv_build_index(bsdb_ctx *c, const char *kv_base, int partitions, int fo
         return open_state;
     };
     std::vector<double> tl((size_t)partitions * 4, 0.0);  // per partition: scan start, scan end, add end, handed off
+    // records per streamed add (BSDB_KV_CHUNK; 0: the whole partition in one add)
+    uint64_t kv_chunk = 1ull << 21;
+    if (const char *e = getenv("BSDB_KV_CHUNK")) kv_chunk = strtoull(e, nullptr, 10) ? strtoull(e, nullptr, 10) : UINT64_MAX;
     // A partition's file mapping (~600 MB at C2) and parse arrays (~400 MB)
     // are released by one background thread while
     // the other partitions and the finish run: released by the scanning
@@ -538,36 +564,49 @@ int bsdb_kv_build_index(bsdb_ctx *c, const char *kv_base, int partitions, int fo
             }
             KvPart &part = work->part;
             part.values = approximate != 0;  // (exact mode: no value bytes)
-            int r;
-            try {
-                r = scan_file(std::string(kv_base) + "." + std::to_string(p), format, (uint64_t)p, block_size, part,  // PKV:79-81
-                              UINT64_MAX, nullptr, [&](uint64_t size) {
-                                  part.reserve((uint64_t)(per_byte_keys * (double)size * 1.05) + 64,
-                                               (uint64_t)(per_byte_blob * (double)size * 1.05) + 4096);
-                              }, &work->m);
-            } catch (const std::bad_alloc &) {
-                r = BSDB_ENOMEM;
-            }
-            scan_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
-            tl[4 * (size_t)p] = std::chrono::duration<double>(t0 - t_start).count();
-            tl[4 * (size_t)p + 1] = since();
-            const uint64_t k = part.addr.size();
-            uint32_t uni = 0;
-            if (!r) r = var_batch_lengths(part.off.data(), k, &uni);
-            if (!r) r = wait_open();
-            if (!r) {
-                // (adds from the scan threads run concurrently: the builder
-                // reserves each one's ranges under its lock and copies outside it)
+            // The partition's records go to the builder in chunks as they are
+            // parsed (adds from the scan threads run concurrently: the builder
+            // reserves each one's ranges under its lock and copies outside
+            // it): the copies overlap the other threads' parsing, read a
+            // cache-warm chunk, and the parse arrays stay small.
+            uint64_t thread_add_ns = 0;
+            part.chunk = kv_chunk;
+            part.flush = [&]() -> int {
+                const uint64_t k = part.addr.size();
+                if (!k) return BSDB_OK;
+                uint32_t uni = 0;
+                int f = var_batch_lengths(part.off.data(), k, &uni);
+                if (!f) f = wait_open();
+                if (f) return f;
                 const auto t1 = std::chrono::steady_clock::now();
                 AddBatch a;
                 a.keys = part.blob.data();
                 a.off = part.off.data();
                 a.count = k;
                 a.uni = uni;
-                r = builder_add(b, a, part.addr.data(), part.value8.data(), part.vlen.data());
-                add_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t1).count();
-                tl[4 * (size_t)p + 2] = since();
+                f = builder_add(b, a, part.addr.data(), part.value8.data(), part.vlen.data());
+                thread_add_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t1).count();
+                part.reset_records();
+                return f;
+            };
+            int r;
+            try {
+                r = scan_file(std::string(kv_base) + "." + std::to_string(p), format, (uint64_t)p, block_size, part,  // PKV:79-81
+                              UINT64_MAX, nullptr, [&](uint64_t size) {
+                                  const uint64_t recs = (uint64_t)(per_byte_keys * (double)size * 1.05) + 64;
+                                  const uint64_t want = kv_chunk == UINT64_MAX ? recs : std::min<uint64_t>(recs, kv_chunk + 64);
+                                  part.reserve(want, (uint64_t)(per_byte_blob / std::max(per_byte_keys, 1e-12) *
+                                                                (double)want * 1.05) + 4096);
+                              }, &work->m);
+                tl[4 * (size_t)p + 1] = since();
+                if (!r) r = part.flush();  // the rest
+            } catch (const std::bad_alloc &) {
+                r = BSDB_ENOMEM;
             }
+            tl[4 * (size_t)p] = std::chrono::duration<double>(t0 - t_start).count();
+            tl[4 * (size_t)p + 2] = since();
+            add_ns += thread_add_ns;
+            scan_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count() - thread_add_ns;
             if (r) {
                 int expect = BSDB_OK;
                 err.compare_exchange_strong(expect, r);
