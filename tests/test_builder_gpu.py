@@ -338,13 +338,18 @@ def test_c3_size_host_passes_equal_one_shot():
         ctx.close()
 
 
+@pytest.mark.parametrize("chunk", [None, "997", "0"])
 @pytest.mark.parametrize("fmt,var,approx,partitions", [(0, False, False, 4), (0, True, True, 7), (1, True, True, 3),
                                                        (0, False, True, 1)])
-def test_kv_streamed_build_equals_in_memory_scan(ctx, tmp_path, fmt, var, approx, partitions):
+def test_kv_streamed_build_equals_in_memory_scan(ctx, tmp_path, monkeypatch, fmt, var, approx, partitions, chunk):
     """F3 in bounded host memory: bsdb_kv_build_index hands
-    each kv.db partition to the builder as soon as it is parsed; its files and
-    MPHF equal those of the in-memory scan (bsdb_kv_scan) fed to the one-call
+    each kv.db partition to the builder while it is parsed, in chunks of
+    BSDB_KV_CHUNK records (default 2 M: one chunk a partition here; 997: many,
+    cut anywhere in a partition; 0: one add a partition); its files and MPHF
+    equal those of the in-memory scan (bsdb_kv_scan) fed to the one-call
     build."""
+    if chunk is not None:
+        monkeypatch.setenv("BSDB_KV_CHUNK", chunk)
     from bsdb_amd import kvfiles
     from bsdb_amd.native import kv_scan
     n = 60_000 if fmt == 1 else 250_000
