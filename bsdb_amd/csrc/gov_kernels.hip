@@ -54,6 +54,18 @@ constexpr int GS_TINY = 12;      // brute-force buckets (only in sets of < ~1500
 #ifndef GOV_GJ_REG_HW
 #define GOV_GJ_REG_HW 6  // the widest heavy rows (64-bit words a plane) the register form takes
 #endif
+#ifndef GOV_GJ_PANEL
+// the heavy system's Gauss-Jordan by 64-column panels (gauss_jordan_panel):
+// bit-identical, off in production (-21 % heavy-GJ cycles in
+// the profiling instance, C2 +2 % in the production one)
+#define GOV_GJ_PANEL 0
+#endif
+// LDS words of the panel form's scratch for n unknowns: the waves' pivot
+// slots (two column parities, 5 words each), two multiplier planes a row, a
+// pivot's trailing words (both planes) for each of a panel's 64 columns
+__host__ __device__ constexpr size_t gj_panel_words(uint32_t n) {
+    return (size_t)2 * (GOV_THREADS / 64) * 5 + (size_t)2 * n + (size_t)2 * 64 * ((n + 1 + 63) / 64);
+}
 #ifndef GOV_PICK_REPS
 // FVS: pairs of heavy hinges taken per stuck cascade (with the in x out pick
 // key, C2 at 6 / 8 / 12 / 16 / 20 / 24 / 28: 522 / 536 / 553 / 558 / 566–569 /
@@ -575,6 +587,10 @@ constexpr size_t solve_scratch_words() {
     return dense > fvs ? dense : fvs;
 }
 static_assert(GS_CMAX != 1664 || 30 * 8 + NB_MAX <= 8 * 2 * GS_WMAX, "FVS null-vector basis fits the dense scratch");
+
+__device__ __forceinline__ uint64_t shfl_xor64(uint64_t x, int d) {
+    return ((uint64_t)(uint32_t)__shfl_xor((int)(x >> 32), d, 64) << 32) | (uint32_t)__shfl_xor((int)(uint32_t)x, d, 64);
+}
 
 __device__ __forceinline__ void gf3_add(uint64_t &x1, uint64_t &x2, uint64_t y1, uint64_t y2) {
     const uint64_t a1 = x1, a2 = x2;
@@ -1490,6 +1506,137 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
             __syncthreads();
             return gj_tail(n, X);
         };
+        // The heavy system's Gauss-Jordan by 64-column panels (GOV_GJ_PANEL).
+        // Per panel (one word of every row), a row per thread holds in
+        // registers its panel word and its multiplier word M over the
+        // panel's pivots (row now = row at the panel's start + sum_j M[j]
+        // pivot row j at the panel's start), and the panel's columns are
+        // taken in order as gauss_jordan takes them: the lowest unused row
+        // with a nonzero is the pivot (each wave's lowest candidate publishes
+        // its index and words in a slot, double-buffered by column parity:
+        // one barrier and two LDS round trips a column, as the register form
+        // but with 4 words a row at any width), every other row with a nonzero
+        // subtracts the normalised pivot row's panel word and adds s (e_c +
+        // M[p]) to its M.  Then every row's trailing words take sum_j M[j] Q_j
+        // (Q_j: pivot row j's trailing words at the panel's start).  Same
+        // pivots, the same linear combinations of the rows: the same reduced
+        // rows, the same tail.  pw: LDS scratch of gj_panel_words(n) words.
+        auto gauss_jordan_panel = [&](uint32_t n, auto &&X, uint64_t *pw) -> bool {
+            constexpr uint32_t NW = GS_THREADS / 64, SW = 5;  // a slot: the row index, its panel word, its M
+            const uint32_t W = (n + 1 + 63) / 64;            // words a plane, the right-hand side (column n) included
+            int16_t *piv = L.a0;
+            uint8_t *used_m = L.b1;
+            uint64_t *slots = pw, *ma = pw + 2 * NW * SW, *mb = ma + n, *Q = mb + n;  // Q[(j * W + t) * 2 + q]
+            const uint32_t rr = tid, lane = tid & 63, wv = tid >> 6;
+            const bool mine = rr < n;
+            bool used = false;
+            uint32_t nfree = 0;
+            for (uint32_t wc = 0; 64 * wc < n; ++wc) {
+                const uint32_t TW = W - wc - 1, cn = min(64u, n - 64 * wc);
+                uint64_t r1 = mine ? X(rr, wc, 0) : 0, r2 = mine ? X(rr, wc, 1) : 0, m1 = 0, m2 = 0;
+                auto publish = [&](uint32_t cl, uint32_t par) {  // the wave's lowest candidate for panel column cl
+                    const bool cand = mine && !used && cl < cn && (((r1 | r2) >> cl) & 1ULL);
+                    const uint64_t bal = __builtin_amdgcn_ballot_w64(cand);
+                    uint64_t *sl = slots + (size_t)(par * NW + wv) * SW;
+                    if (!bal) {
+                        if (lane == 0) sl[0] = ~0ULL;
+                    } else if (lane == (uint32_t)__builtin_ctzll(bal)) {
+                        sl[0] = rr;
+                        sl[1] = r1;
+                        sl[2] = r2;
+                        sl[3] = m1;
+                        sl[4] = m2;
+                    }
+                };
+                __syncthreads();  // (the previous panel's slot readers are done)
+                publish(0, 0);
+                __syncthreads();
+                for (uint32_t cl = 0; cl < cn; ++cl) {
+                    const uint32_t par = cl & 1, c = 64 * wc + cl;
+                    const uint64_t bit = 1ULL << cl;
+                    uint64_t best = ~0ULL;
+                    uint32_t bw = 0;
+#pragma unroll
+                    for (uint32_t w = 0; w < NW; ++w) {
+                        const uint64_t b = slots[(size_t)(par * NW + w) * SW];
+                        if (b < best) {
+                            best = b;
+                            bw = w;
+                        }
+                    }
+                    if (best == ~0ULL) {  // a free column (uniform): x_c = 0
+                        if (tid == 0) piv[c] = -1;
+                        ++nfree;
+                        publish(cl + 1, par ^ 1u);
+                        __syncthreads();
+                        continue;
+                    }
+                    const uint64_t *ps = slots + (size_t)(par * NW + bw) * SW;
+                    const uint64_t q1 = ps[1], q2 = ps[2], d1 = ps[3] | bit, d2 = ps[4];  // d = e_c + M[p] (M[p][c] = 0)
+                    const bool two = (q2 & bit) != 0;  // pivot coefficient 2: its row normalised = planes swapped
+                    if (tid == 0) piv[c] = (int16_t)best;
+                    if (rr == (uint32_t)best) {
+                        used = true;
+                    } else if (mine) {
+                        const uint64_t f1 = r1 & bit, f2 = r2 & bit;
+                        if (f1 | f2) {
+                            const bool sw = (f1 != 0) != two;  // subtract cf * (normalised pivot row)
+                            gf3_add(r1, r2, sw ? q2 : q1, sw ? q1 : q2);
+                            gf3_add(m1, m2, sw ? d2 : d1, sw ? d1 : d2);
+                        }
+                    }
+                    publish(cl + 1, par ^ 1u);
+                    __syncthreads();
+                }
+                if (mine) {
+                    X(rr, wc, 0) = r1;
+                    X(rr, wc, 1) = r2;
+                    ma[rr] = m1;
+                    mb[rr] = m2;
+                }
+                if (TW) {
+                    // Q_j: pivot row j's trailing words at the panel's start
+                    // (the rows are updated in place below)
+                    for (uint32_t ix = tid; ix < cn * TW; ix += GS_THREADS) {
+                        const uint32_t j = ix / TW, t = ix - j * TW;
+                        const int pr = piv[64 * wc + j];
+                        if (pr >= 0) {
+                            Q[((size_t)j * W + t) * 2] = X((uint32_t)pr, wc + 1 + t, 0);
+                            Q[((size_t)j * W + t) * 2 + 1] = X((uint32_t)pr, wc + 1 + t, 1);
+                        }
+                    }
+                    __syncthreads();
+                    if (mine && (m1 | m2)) {
+                        // row += sum_j M[j] Q_j (the panel's columns 4 at a
+                        // time, every lane the same Q words: broadcast reads)
+                        const uint32_t ncol = 64 - (uint32_t)__builtin_clzll(m1 | m2);
+                        for (uint32_t t = 0; t < TW; ++t) {
+                            uint64_t t1 = X(rr, wc + 1 + t, 0), t2 = X(rr, wc + 1 + t, 1);
+                            for (uint32_t c0 = 0; c0 < ncol; c0 += 4) {
+                                uint64_t a1[4], a2[4];
+#pragma unroll
+                                for (uint32_t k = 0; k < 4; ++k) {
+                                    const uint64_t *qj = Q + ((size_t)(c0 + k) * W + t) * 2;
+                                    a1[k] = qj[0];
+                                    a2[k] = qj[1];
+                                }
+#pragma unroll
+                                for (uint32_t k = 0; k < 4; ++k) {
+                                    if ((m1 >> (c0 + k)) & 1u) gf3_add(t1, t2, a1[k], a2[k]);
+                                    if ((m2 >> (c0 + k)) & 1u) gf3_add(t1, t2, a2[k], a1[k]);
+                                }
+                            }
+                            X(rr, wc + 1 + t, 0) = t1;
+                            X(rr, wc + 1 + t, 1) = t2;
+                        }
+                    }
+                }
+            }
+            if (mine) used_m[rr] = used ? 1 : 0;
+            if (tid == 0) L.nfree = nfree;
+            __syncthreads();
+            return gj_tail(n, X);
+        };
         // Block equation of member i: cf*x_hinge + sum of its other vertices
         // = h (mod 3), h = the hinge's position in the edge, cf = its count.
         // Large blocks: heavy variables chosen so that the others follow in
@@ -1930,6 +2077,11 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
                 // the heavy members' equations: cf*x_j + forms = h, in LDS
                 // (the forms' selection arrays are dead now) when they fit
                 const bool hs_lds = (size_t)2 * HW * nH <= Lds::HS_WORDS;
+                // the panel form: its scratch in LDS past the rows (rows in
+                // the global scratch: the whole region)
+                const size_t pscr = gj_panel_words(nH);
+                const bool panel = GOV_GJ_PANEL && nH <= (uint32_t)GS_THREADS && hs_lds &&
+                                   (size_t)2 * HW * nH + pscr <= Lds::HS_WORDS;
                 uint64_t *const hsb = L.hs();
                 auto HSL = [&](uint32_t rr, uint32_t w, uint32_t q) -> uint64_t & { return hsb[(2 * w + q) * nH + rr]; };
                 for (uint32_t i = tid; i < sz; i += GS_THREADS) {
@@ -1981,6 +2133,8 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
                         case 5: hok = gauss_jordan_reg(nH, std::integral_constant<uint32_t, GOV_GJ_REG_HW < 5 ? 1 : 5>{}, HSL, slots); break;
                         default: hok = gauss_jordan_reg(nH, std::integral_constant<uint32_t, GOV_GJ_REG_HW < 6 ? 1 : FW>{}, HSL, slots); break;
                     }
+                } else if (panel) {
+                    hok = gauss_jordan_panel(nH, HSL, hsb + (size_t)2 * HW * nH);
                 } else {
                     hok = hs_lds ? gauss_jordan(nH, HSL) : gauss_jordan(nH, X);
                 }
