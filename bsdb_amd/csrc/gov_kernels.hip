@@ -55,16 +55,15 @@ constexpr int GS_TINY = 12;      // brute-force buckets (only in sets of < ~1500
 #define GOV_GJ_REG_HW 6  // the widest heavy rows (64-bit words a plane) the register form takes
 #endif
 #ifndef GOV_GJ_PANEL
-// the heavy system's Gauss-Jordan by 64-column panels (gauss_jordan_panel):
-// bit-identical, off in production (-21 % heavy-GJ cycles in
-// the profiling instance, C2 +2 % in the production one)
-#define GOV_GJ_PANEL 0
+// the heavy system's Gauss-Jordan by 64-column panels, pivots found by the
+// leader wave (gauss_jordan_panel): bit-identical; C2 solve -8.6 %
+#define GOV_GJ_PANEL 1
 #endif
 // LDS words of the panel form's scratch for n unknowns: the waves' pivot
-// slots (two column parities, 5 words each), two multiplier planes a row, a
+// slots (5 words each), a panel's recorded pivots (4 words a column), a
 // pivot's trailing words (both planes) for each of a panel's 64 columns
 __host__ __device__ constexpr size_t gj_panel_words(uint32_t n) {
-    return (size_t)2 * (GOV_THREADS / 64) * 5 + (size_t)2 * n + (size_t)2 * 64 * ((n + 1 + 63) / 64);
+    return (size_t)(GOV_THREADS / 64) * 5 + (size_t)4 * 64 + (size_t)2 * 64 * ((n + 1 + 63) / 64);
 }
 #ifndef GOV_PICK_REPS
 // FVS: pairs of heavy hinges taken per stuck cascade (with the in x out pick
@@ -1510,14 +1509,17 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
         // Per panel (one word of every row), a row per thread holds in
         // registers its panel word and its multiplier word M over the
         // panel's pivots (row now = row at the panel's start + sum_j M[j]
-        // pivot row j at the panel's start), and the panel's columns are
-        // taken in order as gauss_jordan takes them: the lowest unused row
-        // with a nonzero is the pivot (each wave's lowest candidate publishes
-        // its index and words in a slot, double-buffered by column parity:
-        // one barrier and two LDS round trips a column, as the register form
-        // but with 4 words a row at any width), every other row with a nonzero
-        // subtracts the normalised pivot row's panel word and adds s (e_c +
-        // M[p]) to its M.  Then every row's trailing words take sum_j M[j] Q_j
+        // pivot row j at the panel's start); eliminating column c with pivot
+        // p adds s (p's panel word) to a row's panel word and s (e_c + M[p])
+        // to its M.  The columns are taken in order with gauss_jordan's pivots
+        // (the lowest unused row with a nonzero), found without a barrier per
+        // column: the LEADER, the lowest wave with an unused row, holds the
+        // lowest unused rows, so while it has a candidate the pivot is its
+        // own -- it runs through the panel's columns alone (ballot, readlane)
+        // and records each pivot's words; then the other waves take the
+        // recorded eliminations in order, and a column the leader has no
+        // candidate for is settled by every wave's lowest candidate (slots).
+        // After the panel every row's trailing words take sum_j M[j] Q_j
         // (Q_j: pivot row j's trailing words at the panel's start).  Same
         // pivots, the same linear combinations of the rows: the same reduced
         // rows, the same tail.  pw: LDS scratch of gj_panel_words(n) words.
@@ -1526,77 +1528,143 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
             const uint32_t W = (n + 1 + 63) / 64;            // words a plane, the right-hand side (column n) included
             int16_t *piv = L.a0;
             uint8_t *used_m = L.b1;
-            uint64_t *slots = pw, *ma = pw + 2 * NW * SW, *mb = ma + n, *Q = mb + n;  // Q[(j * W + t) * 2 + q]
+            uint32_t *flags = L.hbin;                         // [w]: wave w has an unused row; [16]: the leader's block end
+            uint64_t *slots = pw, *pinfo = pw + NW * SW;      // pinfo[4 cl ..]: pivot panel word, e_c + M[p]
+            uint64_t *Q = pinfo + 4 * 64;                     // Q[(j * W + t) * 2 + q]
             const uint32_t rr = tid, lane = tid & 63, wv = tid >> 6;
             const bool mine = rr < n;
             bool used = false;
             uint32_t nfree = 0;
+            // blocks of this call are numbered 1, 2, ...: a progress word left
+            // by an earlier call or block never reads as the current block's
+            // (the reset is ordered before any use by the first block's barrier)
+            uint32_t seq = 0;
+            if (tid == 0) flags[16] = 0xFFFFFFFFu;
             for (uint32_t wc = 0; 64 * wc < n; ++wc) {
                 const uint32_t TW = W - wc - 1, cn = min(64u, n - 64 * wc);
                 uint64_t r1 = mine ? X(rr, wc, 0) : 0, r2 = mine ? X(rr, wc, 1) : 0, m1 = 0, m2 = 0;
-                auto publish = [&](uint32_t cl, uint32_t par) {  // the wave's lowest candidate for panel column cl
-                    const bool cand = mine && !used && cl < cn && (((r1 | r2) >> cl) & 1ULL);
-                    const uint64_t bal = __builtin_amdgcn_ballot_w64(cand);
-                    uint64_t *sl = slots + (size_t)(par * NW + wv) * SW;
-                    if (!bal) {
-                        if (lane == 0) sl[0] = ~0ULL;
-                    } else if (lane == (uint32_t)__builtin_ctzll(bal)) {
-                        sl[0] = rr;
-                        sl[1] = r1;
-                        sl[2] = r2;
-                        sl[3] = m1;
-                        sl[4] = m2;
-                    }
-                };
-                __syncthreads();  // (the previous panel's slot readers are done)
-                publish(0, 0);
-                __syncthreads();
-                for (uint32_t cl = 0; cl < cn; ++cl) {
-                    const uint32_t par = cl & 1, c = 64 * wc + cl;
-                    const uint64_t bit = 1ULL << cl;
-                    uint64_t best = ~0ULL;
-                    uint32_t bw = 0;
-#pragma unroll
-                    for (uint32_t w = 0; w < NW; ++w) {
-                        const uint64_t b = slots[(size_t)(par * NW + w) * SW];
-                        if (b < best) {
-                            best = b;
-                            bw = w;
-                        }
-                    }
-                    if (best == ~0ULL) {  // a free column (uniform): x_c = 0
-                        if (tid == 0) piv[c] = -1;
-                        ++nfree;
-                        publish(cl + 1, par ^ 1u);
-                        __syncthreads();
-                        continue;
-                    }
-                    const uint64_t *ps = slots + (size_t)(par * NW + bw) * SW;
-                    const uint64_t q1 = ps[1], q2 = ps[2], d1 = ps[3] | bit, d2 = ps[4];  // d = e_c + M[p] (M[p][c] = 0)
-                    const bool two = (q2 & bit) != 0;  // pivot coefficient 2: its row normalised = planes swapped
-                    if (tid == 0) piv[c] = (int16_t)best;
-                    if (rr == (uint32_t)best) {
+                auto apply = [&](uint64_t bit, uint64_t q1, uint64_t q2, uint64_t d1, uint64_t d2, uint32_t p) {
+                    if (rr == p) {
                         used = true;
                     } else if (mine) {
                         const uint64_t f1 = r1 & bit, f2 = r2 & bit;
                         if (f1 | f2) {
-                            const bool sw = (f1 != 0) != two;  // subtract cf * (normalised pivot row)
+                            const bool sw = (f1 != 0) != ((q2 & bit) != 0);  // subtract cf * (normalised pivot row)
                             gf3_add(r1, r2, sw ? q2 : q1, sw ? q1 : q2);
                             gf3_add(m1, m2, sw ? d2 : d1, sw ? d1 : d2);
                         }
                     }
-                    publish(cl + 1, par ^ 1u);
+                };
+                uint32_t cl = 0;
+                while (cl < cn) {  // (uniform)
+                    const uint64_t un = __builtin_amdgcn_ballot_w64(mine && !used);
+                    if (lane == 0) flags[wv] = un != 0;
                     __syncthreads();
+                    uint32_t lead = NW;
+                    for (uint32_t w = 0; w < NW; ++w)
+                        if (flags[w]) {
+                            lead = w;
+                            break;
+                        }
+                    // The leader's progress word: (block sequence << 16) |
+                    // columns recorded | 0x8000 once the block has ended.  The
+                    // other waves take each recorded column as soon as it is
+                    // published, beside the leader (no barrier between).
+                    ++seq;  // (< 0xFFFF: a block takes at least one column)
+                    uint32_t ce = cl;
+                    if (wv == lead) {
+                        for (; ce < cn; ++ce) {
+                            const uint64_t bit = 1ULL << ce;
+                            const uint64_t bal = __builtin_amdgcn_ballot_w64(mine && !used && ((r1 | r2) & bit));
+                            if (!bal) break;
+                            const uint32_t pl = (uint32_t)__builtin_ctzll(bal), p = 64 * wv + pl;
+                            const uint64_t q1 = readlane64(r1, (int)pl), q2 = readlane64(r2, (int)pl);
+                            const uint64_t d1 = readlane64(m1, (int)pl) | bit, d2 = readlane64(m2, (int)pl);  // M[p][c] = 0
+                            if (lane == 0) {
+                                pinfo[4 * ce] = q1;
+                                pinfo[4 * ce + 1] = q2;
+                                pinfo[4 * ce + 2] = d1;
+                                pinfo[4 * ce + 3] = d2;
+                                piv[64 * wc + ce] = (int16_t)p;
+                                __hip_atomic_store(&flags[16], seq << 16 | (ce + 1), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                            }
+                            apply(bit, q1, q2, d1, d2, p);
+                        }
+                        if (lane == 0) __hip_atomic_store(&flags[16], seq << 16 | 0x8000u | ce, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    } else if (lead < NW) {
+                        uint32_t c2 = cl;
+                        for (;;) {
+                            const uint32_t v = __hip_atomic_load(&flags[16], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                            const bool mine_seq = (v >> 16) == seq;
+                            const uint32_t lim = mine_seq ? (v & 0x7FFFu) : cl;
+                            for (; c2 + 4 <= lim; c2 += 4) {  // (the recorded pivots 4 at a time: loads issued together)
+                                // (a pivot row is the leader's, never this wave's)
+                                uint64_t pv4[16];
+#pragma unroll
+                                for (uint32_t k = 0; k < 16; ++k) pv4[k] = pinfo[4 * c2 + k];
+#pragma unroll
+                                for (uint32_t k = 0; k < 4; ++k)
+                                    apply(1ULL << (c2 + k), pv4[4 * k], pv4[4 * k + 1], pv4[4 * k + 2], pv4[4 * k + 3],
+                                          0xFFFFFFFFu);
+                            }
+                            if (mine_seq && (v & 0x8000u)) {
+                                for (; c2 < lim; ++c2) {
+                                    const uint64_t *pi = pinfo + 4 * c2;
+                                    apply(1ULL << c2, pi[0], pi[1], pi[2], pi[3], 0xFFFFFFFFu);
+                                }
+                                ce = lim;
+                                break;
+                            }
+                            if (c2 + 4 > lim) __builtin_amdgcn_s_sleep(1);
+                        }
+                    }
+                    // (every wave has ce; uniform)
+                    cl = ce;
+                    if (cl < cn) {
+                        // column cl: no candidate in the leader -- every
+                        // wave's lowest candidate (or a free column)
+                        const uint64_t bit = 1ULL << cl;
+                        const uint64_t bal = __builtin_amdgcn_ballot_w64(mine && !used && ((r1 | r2) & bit));
+                        uint64_t *sl = slots + (size_t)wv * SW;
+                        if (!bal) {
+                            if (lane == 0) sl[0] = ~0ULL;
+                        } else if (lane == (uint32_t)__builtin_ctzll(bal)) {
+                            sl[0] = rr;
+                            sl[1] = r1;
+                            sl[2] = r2;
+                            sl[3] = m1;
+                            sl[4] = m2;
+                        }
+                        __syncthreads();
+                        uint64_t best = ~0ULL;
+                        uint32_t bw = 0;
+                        for (uint32_t w = 0; w < NW; ++w) {
+                            const uint64_t b = slots[(size_t)w * SW];
+                            if (b < best) {
+                                best = b;
+                                bw = w;
+                            }
+                        }
+                        const uint32_t c = 64 * wc + cl;
+                        if (best == ~0ULL) {  // a free column (uniform): x_c = 0
+                            if (tid == 0) piv[c] = -1;
+                            ++nfree;
+                        } else {
+                            const uint64_t *ps = slots + (size_t)bw * SW;
+                            if (tid == 0) piv[c] = (int16_t)best;
+                            apply(bit, ps[1], ps[2], ps[3] | bit, ps[4], (uint32_t)best);
+                        }
+                        ++cl;
+                    }
                 }
                 if (mine) {
                     X(rr, wc, 0) = r1;
                     X(rr, wc, 1) = r2;
-                    ma[rr] = m1;
-                    mb[rr] = m2;
                 }
                 if (TW) {
                     // Q_j: pivot row j's trailing words at the panel's start
                     // (the rows are updated in place below)
+                    __syncthreads();
                     for (uint32_t ix = tid; ix < cn * TW; ix += GS_THREADS) {
                         const uint32_t j = ix / TW, t = ix - j * TW;
                         const int pr = piv[64 * wc + j];
@@ -1631,6 +1699,7 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
                         }
                     }
                 }
+                __syncthreads();
             }
             if (mine) used_m[rr] = used ? 1 : 0;
             if (tid == 0) L.nfree = nfree;
