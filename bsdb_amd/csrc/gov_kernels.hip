@@ -587,10 +587,6 @@ constexpr size_t solve_scratch_words() {
 }
 static_assert(GS_CMAX != 1664 || 30 * 8 + NB_MAX <= 8 * 2 * GS_WMAX, "FVS null-vector basis fits the dense scratch");
 
-__device__ __forceinline__ uint64_t shfl_xor64(uint64_t x, int d) {
-    return ((uint64_t)(uint32_t)__shfl_xor((int)(x >> 32), d, 64) << 32) | (uint32_t)__shfl_xor((int)(uint32_t)x, d, 64);
-}
-
 __device__ __forceinline__ void gf3_add(uint64_t &x1, uint64_t &x2, uint64_t y1, uint64_t y2) {
     const uint64_t a1 = x1, a2 = x2;
     x1 = (a1 & ~y1 & ~y2) | (~a1 & ~a2 & y1) | (a2 & y2);
