@@ -54,6 +54,12 @@ constexpr int GS_TINY = 12;      // brute-force buckets (only in sets of < ~1500
 #ifndef GOV_GJ_REG_HW
 #define GOV_GJ_REG_HW 6  // the widest heavy rows (64-bit words a plane) the register form takes
 #endif
+#ifndef GOV_GJ_FOLLOW
+#define GOV_GJ_FOLLOW 1  // panel form: recorded pivots a following wave takes at once (2, 4, 8: slower)
+#endif
+#ifndef GOV_GJ_SLEEP
+#define GOV_GJ_SLEEP 1   // panel form: s_sleep of a following wave that waits for the leader
+#endif
 #ifndef GOV_GJ_PANEL
 // the heavy system's Gauss-Jordan by 64-column panels, pivots found by the
 // leader wave (gauss_jordan_panel): bit-identical; C2 solve -8.6 %
@@ -1593,13 +1599,14 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
                             const uint32_t v = __hip_atomic_load(&flags[16], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
                             const bool mine_seq = (v >> 16) == seq;
                             const uint32_t lim = mine_seq ? (v & 0x7FFFu) : cl;
-                            for (; c2 + 4 <= lim; c2 += 4) {  // (the recorded pivots 4 at a time: loads issued together)
+                            constexpr uint32_t FU = GOV_GJ_FOLLOW;
+                            for (; c2 + FU <= lim; c2 += FU) {  // (the recorded pivots FU at a time: loads issued together)
                                 // (a pivot row is the leader's, never this wave's)
-                                uint64_t pv4[16];
+                                uint64_t pv4[4 * FU];
 #pragma unroll
-                                for (uint32_t k = 0; k < 16; ++k) pv4[k] = pinfo[4 * c2 + k];
+                                for (uint32_t k = 0; k < 4 * FU; ++k) pv4[k] = pinfo[4 * c2 + k];
 #pragma unroll
-                                for (uint32_t k = 0; k < 4; ++k)
+                                for (uint32_t k = 0; k < FU; ++k)
                                     apply(1ULL << (c2 + k), pv4[4 * k], pv4[4 * k + 1], pv4[4 * k + 2], pv4[4 * k + 3],
                                           0xFFFFFFFFu);
                             }
@@ -1611,7 +1618,7 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
                                 ce = lim;
                                 break;
                             }
-                            if (c2 + 4 > lim) __builtin_amdgcn_s_sleep(1);
+                            if (GOV_GJ_SLEEP && c2 + FU > lim) __builtin_amdgcn_s_sleep(GOV_GJ_SLEEP);
                         }
                     }
                     // (every wave has ce; uniform)
