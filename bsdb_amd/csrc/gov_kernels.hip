@@ -57,6 +57,9 @@ constexpr int GS_TINY = 12;      // brute-force buckets (only in sets of < ~1500
 #ifndef GOV_GJ_FOLLOW
 #define GOV_GJ_FOLLOW 1  // panel form: recorded pivots a following wave takes at once (2, 4, 8: slower)
 #endif
+#ifndef GOV_GJ_B2
+#define GOV_GJ_B2 4  // panel form: a panel's columns a row's trailing update takes at once (a power of two)
+#endif
 #ifndef GOV_GJ_SLEEP
 #define GOV_GJ_SLEEP 1   // panel form: s_sleep of a following wave that waits for the leader
 #endif
@@ -1683,16 +1686,17 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
                         const uint32_t ncol = 64 - (uint32_t)__builtin_clzll(m1 | m2);
                         for (uint32_t t = 0; t < TW; ++t) {
                             uint64_t t1 = X(rr, wc + 1 + t, 0), t2 = X(rr, wc + 1 + t, 1);
-                            for (uint32_t c0 = 0; c0 < ncol; c0 += 4) {
-                                uint64_t a1[4], a2[4];
+                            constexpr uint32_t BU = GOV_GJ_B2;
+                            for (uint32_t c0 = 0; c0 < ncol; c0 += BU) {
+                                uint64_t a1[BU], a2[BU];
 #pragma unroll
-                                for (uint32_t k = 0; k < 4; ++k) {
+                                for (uint32_t k = 0; k < BU; ++k) {
                                     const uint64_t *qj = Q + ((size_t)(c0 + k) * W + t) * 2;
                                     a1[k] = qj[0];
                                     a2[k] = qj[1];
                                 }
 #pragma unroll
-                                for (uint32_t k = 0; k < 4; ++k) {
+                                for (uint32_t k = 0; k < BU; ++k) {
                                     if ((m1 >> (c0 + k)) & 1u) gf3_add(t1, t2, a1[k], a2[k]);
                                     if ((m2 >> (c0 + k)) & 1u) gf3_add(t1, t2, a2[k], a1[k]);
                                 }
