@@ -65,7 +65,7 @@ constexpr int GS_TINY = 12;      // brute-force buckets (only in sets of < ~1500
 #endif
 #ifndef GOV_GJ_PANEL
 // the heavy system's Gauss-Jordan by 64-column panels, pivots found by the
-// leader wave (gauss_jordan_panel): bit-identical; C2 solve -8.6 %
+// leader wave (gauss_jordan_panel): bit-identical; C2 solve -10 %
 #define GOV_GJ_PANEL 1
 #endif
 // LDS words of the panel form's scratch for n unknowns: the waves' pivot
