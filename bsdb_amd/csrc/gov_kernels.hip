@@ -2156,8 +2156,11 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
                 // the panel form: its scratch in LDS past the rows (rows in
                 // the global scratch: the whole region)
                 const size_t pscr = gj_panel_words(nH);
-                const bool panel = GOV_GJ_PANEL && nH <= (uint32_t)GS_THREADS && hs_lds &&
-                                   (size_t)2 * HW * nH + pscr <= Lds::HS_WORDS;
+                // (LDS state only: the following waves poll the leader's
+                // progress word, which a global slab -- SolveBig -- would put
+                // behind the vector L1)
+                const bool panel = GOV_GJ_PANEL && !std::is_same<Lds, SolveBig>::value && nH <= (uint32_t)GS_THREADS &&
+                                   hs_lds && (size_t)2 * HW * nH + pscr <= Lds::HS_WORDS;
                 uint64_t *const hsb = L.hs();
                 auto HSL = [&](uint32_t rr, uint32_t w, uint32_t q) -> uint64_t & { return hsb[(2 * w + q) * nH + rr]; };
                 for (uint32_t i = tid; i < sz; i += GS_THREADS) {
