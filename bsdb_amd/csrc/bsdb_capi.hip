@@ -18,6 +18,7 @@
 #include <cerrno>
 #include <functional>
 #include <chrono>
+#include <condition_variable>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -344,11 +345,50 @@ int copy_on_own_stream(int dev, void *dst, const void *src, size_t bytes, hipMem
 // that run on several host threads at once (the builder's concurrent adds):
 // the runtime's own pageable path serialised them (8 kv.db partitions' adds
 // at ~1 GB/s each, profiles/r5/kv/), each thread's bounce copies on its own.
+// At most BOUNCE_SLOTS copies bounce at once (BSDB_BOUNCE_SLOTS, default 16:
+// <= 1 GiB of page-locked pieces however many threads add); a copy
+// that cannot have its pieces (hipHostMalloc refused) takes the runtime's
+// pageable path instead of failing the add.
+struct BounceSlots {
+    std::mutex mu;
+    std::condition_variable cv;
+    int free_slots;
+    BounceSlots() {
+        const char *e = getenv("BSDB_BOUNCE_SLOTS");
+        const int v = e ? atoi(e) : 16;
+        free_slots = v > 0 ? v : 1;
+    }
+    void acquire() {
+        std::unique_lock<std::mutex> g(mu);
+        cv.wait(g, [this] { return free_slots > 0; });
+        --free_slots;
+    }
+    void release() {
+        {
+            std::lock_guard<std::mutex> g(mu);
+            ++free_slots;
+        }
+        cv.notify_one();
+    }
+};
+static BounceSlots &bounce_slots() {
+    static BounceSlots *b = new BounceSlots();
+    return *b;
+}
 int h2d_bounce(hipStream_t s, void *dst, const void *src, size_t bytes) {
     if (bytes == 0) return BSDB_OK;
+    bounce_slots().acquire();
     void *pin[2] = {pinned_pool().take(), pinned_pool().take()};
+    if (!pin[0] || !pin[1]) {  // no page-locked memory to be had: the runtime's pageable copy
+        pinned_pool().give(pin[0]);
+        pinned_pool().give(pin[1]);
+        bounce_slots().release();
+        hipError_t e = hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        return e == hipSuccess ? BSDB_OK : hip_fail(e, "H2D copy (pageable fallback)", __LINE__);
+    }
     hipEvent_t ev[2] = {nullptr, nullptr};
-    int rc = pin[0] && pin[1] ? BSDB_OK : BSDB_ENOMEM;
+    int rc = BSDB_OK;
     for (int i = 0; i < 2 && !rc; ++i)
         if (hipEventCreateWithFlags(&ev[i], hipEventDisableTiming) != hipSuccess) rc = BSDB_EIO;
     bool pending[2] = {false, false};
@@ -368,6 +408,7 @@ int h2d_bounce(hipStream_t s, void *dst, const void *src, size_t bytes) {
         pinned_pool().give(pin[i]);
         if (ev[i]) (void)hipEventDestroy(ev[i]);
     }
+    bounce_slots().release();
     return rc;
 }
 

@@ -92,6 +92,10 @@ struct bsdb_builder {
     HostVec<uint8_t> vlen;
     bool borrowed_records = false;  // one-call forms: the caller's record arrays cover every key
     int failed = BSDB_OK;  // an add that failed part-way leaves the builder unusable
+    // an add's copy that failed, recorded before the add releases grow_mu (the
+    // add takes mu for `failed` only afterwards, when a finish may hold it):
+    // finish reads it once it holds grow_mu exclusively
+    std::atomic<int> copy_failed{BSDB_OK};
     bool finished = false;
     // Adds may come from several threads (put() threads, the kv.db scan
     // threads).  mu is held only to RESERVE an add's ranges (its keys' index
@@ -701,6 +705,10 @@ int builder_add(bsdb_builder *b, const AddBatch &a, const uint64_t *h_addr, cons
     add_copy_records(b, n0, a.count, h_addr, h_value8, h_vlen);
     b->add_copy_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(t1 - t0).count();
     b->add_rec_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t1).count();
+    if (rc) {
+        int expect = BSDB_OK;
+        b->copy_failed.compare_exchange_strong(expect, rc);
+    }
     copying.unlock();
     if (rc) {
         std::lock_guard<std::mutex> gb(b->mu);
@@ -1100,7 +1108,9 @@ static int host_passes_build(bsdb_ctx *c, const uint8_t *h_keys, uint32_t key_le
         std::lock_guard<std::mutex> gb(b->mu);
         std::unique_lock<std::shared_mutex> settled(b->grow_mu);
         std::lock_guard<std::mutex> g(c->mu);
-        if (hipSetDevice(c->device) != hipSuccess) {
+        if (b->copy_failed.load()) {
+            rc = b->failed = b->copy_failed.load();
+        } else if (hipSetDevice(c->device) != hipSuccess) {
             rc = BSDB_EIO;
         } else {
             Ordered ord(c, c->stream);
@@ -1175,6 +1185,7 @@ int bsdb_builder_finish(bsdb_builder *b, uint32_t width, uint32_t passes, const 
     int rc;
     {
         std::unique_lock<std::shared_mutex> settled(b->grow_mu);  // every add's copies are done
+        if (const int cf = b->copy_failed.load()) return b->failed = cf;  // a copy failed after the check above
         std::lock_guard<std::mutex> g(c->mu);
         HIP_OK(hipSetDevice(c->device));
         Ordered ord(c, c->stream);

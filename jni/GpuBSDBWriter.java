@@ -4,8 +4,10 @@
 // and the same output files (kv.db.<p>, config.properties, hash.db, index.db,
 // index_a.db), with the key hash, bucket histogram, GOV solve, signing and the
 // index scatter on the GPU through GpuBuild (jni/GpuBuild.java, the C ABI of
-// include/bsdb_mi355x.h).  Builder (src/main/java/tech/bsdb/tools/Builder.java:86)
-// and ParquetBuilder construct it in place of BSDBWriter; nothing else changes.
+// include/bsdb_mi355x.h).  The reference's BSDBWriter delegates every public
+// method to it when the JVM runs with -Dbsdb.build.gpu=true (jni/BSDBWriter-gpu.patch,
+// off by default), so its callers -- Builder.java:86, ParquetBuilder.java:90,
+// BSDBWriterTest.java:34 -- construct BSDBWriter unchanged.
 //
 // What replaces what:
 //   put     W:75-89 appends to the KV writer, then keys.add(key) hashes the key
@@ -48,6 +50,7 @@ import java.io.File;
 import java.io.IOException;
 import java.nio.ByteBuffer;
 import java.nio.ByteOrder;
+import java.util.ArrayDeque;
 import java.util.ArrayList;
 import java.util.List;
 import java.util.Objects;
@@ -107,7 +110,7 @@ public class GpuBSDBWriter {
         // takes the formula form (stride 1) and keeps no record arrays
         builder = nativeFormat < 0 ? GpuBuild.builderOpen(ctx, 0, BATCH_KEYS, BATCH_BYTES, false, 0, 1) : 0;
         keyBatch = ThreadLocal.withInitial(() -> {
-            final Batch b = new Batch(false);
+            final Batch b = new Batch(false, false);
             synchronized (batches) {
                 batches.add(b);
             }
@@ -188,29 +191,35 @@ public class GpuBSDBWriter {
     }
 
     // W:112-155: passSize = min(n, ps/8) slots a pass, one kvWriter.forEach per
-    // pass; the records go to the device in batches (getLong + scatter there)
+    // pass; the records go to the device in batches (getLong + scatter there).
+    // kvWriter.forEach starts a new thread pool on every call (Common.java:287),
+    // so a batch belongs to a pass: the pass's threads take batches from a pool,
+    // and every batch goes back to it after the pass's final flush.  The pool
+    // holds at most one pass's worth of scan threads' batches.
     private void passLoop() throws IOException, InterruptedException {
         final long[] passes = new long[1];
         final long ix = GpuBuild.indexOpen(gpuMph, approximateMode, passCacheSize, indexFile().getPath(),
                 approximateIndexFile().getPath(), passes);
+        final ArrayDeque<Batch> pool = new ArrayDeque<>();
         try {
-            final List<Batch> all = new ArrayList<>();
-            final ThreadLocal<Batch> records = ThreadLocal.withInitial(() -> {
-                final Batch b = new Batch(true);
-                synchronized (all) {
-                    all.add(b);
-                }
-                return b;
-            });
             for (long p = 0; p < passes[0]; p++) {
                 GpuBuild.indexBeginPass(ix, p);
+                final List<Batch> inPass = new ArrayList<>();
+                final ThreadLocal<Batch> records = ThreadLocal.withInitial(() -> {
+                    synchronized (pool) {
+                        final Batch b = pool.isEmpty() ? new Batch(true, approximateMode) : pool.pop();
+                        inPass.add(b);
+                        return b;
+                    }
+                });
                 kvWriter.forEach((addr, key, value) -> {   // scan threads (PartitionedKVWriter.java:50-70)
                     final Batch b = records.get();
                     if (!b.fits(key, value)) b.flushRecords(ix, this);
                     b.add(addr, key, value);
                 });
-                synchronized (all) {
-                    for (Batch b : all) b.flushRecords(ix, this);
+                synchronized (pool) {
+                    for (Batch b : inPass) b.flushRecords(ix, this);
+                    pool.addAll(inPass);                      // the next pass's threads reuse them
                 }
                 GpuBuild.indexEndPass(ix);                    // the pass's <= 128 MiB writes (W:166-179)
             }
@@ -234,10 +243,11 @@ public class GpuBSDBWriter {
         final ByteBuffer addr, value8, vlen;
         int count;
 
-        Batch(boolean records) {
+        /** records: a pass loop's batch (addresses); approximate: index_a.db value bytes too (W:140-142). */
+        Batch(boolean records, boolean approximate) {
             addr = records ? direct(8L * BATCH_KEYS) : null;
-            value8 = records ? direct(8L * BATCH_KEYS) : null;
-            vlen = records ? direct(BATCH_KEYS) : null;
+            value8 = records && approximate ? direct(8L * BATCH_KEYS) : null;
+            vlen = records && approximate ? direct(BATCH_KEYS) : null;
             offs.putLong(0, 0L);
         }
 
@@ -248,8 +258,8 @@ public class GpuBSDBWriter {
         void add(long a, byte[] key, byte[] value) {
             blob.put(key);
             offs.putLong(8 * (count + 1), blob.position());
-            if (addr != null) {
-                addr.putLong(8 * count, a);
+            if (addr != null) addr.putLong(8 * count, a);
+            if (value8 != null) {
                 // index_a.db slot: the value's first min(len, 8) bytes (W:140-142); a
                 // blocked writer's large record hands null (BlockedKVWriter.java:105-109)
                 long v = 0;
@@ -285,8 +295,8 @@ public class GpuBSDBWriter {
             return ByteBuffer.allocateDirect((int) bytes).order(ByteOrder.nativeOrder());
         }
 
-        private static long address(ByteBuffer b) {
-            return ((DirectBuffer) b).address();
+        private static long address(ByteBuffer b) {  // null: no buffer (the C ABI takes NULL)
+            return b == null ? 0L : ((DirectBuffer) b).address();
         }
     }
 }

@@ -188,6 +188,7 @@ JNIEXPORT jlongArray JF(mphInfo)(JNIEnv *env, jclass c, jlong mph) {
     if (rc) { fail(env, rc); return NULL; }
     jlong v[5] = {(jlong)n, (jlong)m, (jlong)w, (jlong)vw, (jlong)sw};
     jlongArray a = (*env)->NewLongArray(env, 5);
+    if (!a) return NULL;  /* OutOfMemoryError pending */
     (*env)->SetLongArrayRegion(env, a, 0, 5, v);
     return a;
 }
@@ -201,6 +202,7 @@ JNIEXPORT jlongArray JF(mphSizes)(JNIEnv *env, jclass c, jlong n, jint w) {
     if (rc) { fail(env, rc); return NULL; }
     jlong v[4] = {(jlong)m, (jlong)vw, (jlong)vb, (jlong)sw};
     jlongArray a = (*env)->NewLongArray(env, 4);
+    if (!a) return NULL;  /* OutOfMemoryError pending */
     (*env)->SetLongArrayRegion(env, a, 0, 4, v);
     return a;
 }

@@ -210,3 +210,170 @@ def test_shim_type_checks_against_the_header():
                         "-I", os.path.join(ROOT, "tests", "jni_stub"), "-I", os.path.join(ROOT, "include"), SHIM],
                        capture_output=True, text=True)
     assert r.returncode == 0, r.stderr
+
+
+# ---- the reference's BSDBWriter delegating to GpuBSDBWriter ----
+PATCH = os.path.join(ROOT, "jni", "BSDBWriter-gpu.patch")
+REF_ROOT = "/root/reference"
+W_REL = os.path.join("src", "main", "java", "tech", "bsdb", "write", "BSDBWriter.java")
+# the reference's public API of BSDBWriter (W:39,67,71,75,91,99,107): name -> parameter names
+W_METHODS = {"sample": ["key", "value"], "onSampleFinished": [], "put": ["key", "value"], "build": [],
+             "buildHash": [], "buildIndex": ["hashFunction"]}
+W_CTOR_PARAMS = [("File", "basePath"), ("File", "tmpDir"), ("int", "checksumBits"), ("long", "passCacheSize"),
+                 ("boolean", "compact"), ("boolean", "compress"), ("int", "compressBLockSize"),
+                 ("int", "sharedDictSize"), ("boolean", "approximateMode")]
+# (file, line) of every construction of BSDBWriter in the reference
+W_CALLERS = [("src/main/java/tech/bsdb/tools/Builder.java", 86),
+             ("src/main/java/tech/bsdb/tools/ParquetBuilder.java", 90),
+             ("src/test/java/tech/bsdb/write/BSDBWriterTest.java", 34)]
+needs_ref = pytest.mark.skipif(not os.path.isfile(os.path.join(REF_ROOT, W_REL)) or shutil.which("patch") is None,
+                               reason="the reference tree (this container only) and patch(1)")
+
+
+def _patched_writer(tmp_path) -> str:
+    """The reference's BSDBWriter.java with jni/BSDBWriter-gpu.patch applied
+    (in a scratch copy: the reference stays read-only)."""
+    dst = tmp_path / W_REL
+    dst.parent.mkdir(parents=True)
+    shutil.copyfile(os.path.join(REF_ROOT, W_REL), dst)
+    r = subprocess.run(["patch", "-p1", "--forward", "--batch", "--no-backup-if-mismatch", "-i", PATCH],
+                       cwd=tmp_path, capture_output=True, text=True)
+    assert r.returncode == 0 and "FAILED" not in r.stdout and "fuzz" not in r.stdout, r.stdout + r.stderr
+    return dst.read_text()
+
+
+def _method_body(src: str, head: str) -> str:
+    """The body of the member whose declaration matches regex `head` (braces balanced)."""
+    m = re.search(head + r"[^{;]*\{", src)
+    assert m, head
+    depth, j = 1, m.end()
+    while depth:
+        depth += {"{": 1, "}": -1}.get(src[j], 0)
+        j += 1
+    return src[m.end(): j - 1]
+
+
+def test_patch_adds_only_delegation():
+    """The patch (no reference needed) removes nothing but the two field
+    initialisers it guards, and every line it adds is the switch, the
+    delegate field, or a `gpu` guard / delegation."""
+    txt = open(PATCH).read()
+    assert txt.startswith("--- a/" + W_REL.replace(os.sep, "/")) and ("+++ b/" + W_REL.replace(os.sep, "/")) in txt
+    body = [ln for ln in txt.splitlines() if not ln.startswith(("---", "+++", "@@"))]
+    removed = [ln[1:].strip() for ln in body if ln.startswith("-")]
+    added = [ln[1:].strip() for ln in body if ln.startswith("+")]
+    assert len(removed) == 2 and removed[0].startswith("this.kvWriter =") and removed[1].startswith("this.keys =")
+    for ln in added:
+        ok = (ln in ("", "}", "return;") or ln.startswith(("/**", "if (gpu != null)", "gpu.", "this.gpu = GPU_BUILD ?"))
+              or ln in ("static final boolean GPU_BUILD = Boolean.getBoolean(\"bsdb.build.gpu\");",
+                        "private final GpuBSDBWriter gpu;")
+              or re.fullmatch(r"this\.(kvWriter|keys) = gpu != null \? null : .+;", ln))
+        assert ok, ln
+
+
+@needs_ref
+def test_patched_writer_delegates_every_public_method(tmp_path):
+    """Applied to the reference's own file: the switch is off unless
+    -Dbsdb.build.gpu=true, the constructor hands GpuBSDBWriter its own
+    arguments in order, and each public method's first statement hands its
+    arguments to the same-named GpuBSDBWriter method."""
+    src = _strip_comments(_patched_writer(tmp_path))
+    flat = re.sub(r"\s+", " ", src)
+    assert 'static final boolean GPU_BUILD = Boolean.getBoolean("bsdb.build.gpu");' in flat
+    ctor = re.sub(r"\s+", " ", _method_body(src, r"public\s+BSDBWriter\s*\("))
+    want = "this.gpu = GPU_BUILD ? new GpuBSDBWriter(" + ", ".join(n for _, n in W_CTOR_PARAMS) + ") : null;"
+    assert want in ctor
+    # the reference's own construction still runs when the switch is off, and
+    # every final field is assigned before the GPU path returns
+    pre = ctor[: ctor.index("if (gpu != null) return;")]
+    for f in ("this.basePath", "this.kvWriter", "this.keys", "this.checksumBits", "this.passCacheSize",
+              "this.approximateMode", "this.gpu"):
+        assert f + " =" in pre, f
+    for name, params in W_METHODS.items():
+        body = re.sub(r"\s+", " ", _method_body(src, r"public\s+[\w<>\[\]]+\s+" + name + r"\s*\(")).strip()
+        call = f"gpu.{name}({', '.join(params)})"
+        assert body.startswith("if (gpu != null)") and call in body[:120], (name, body[:160])
+
+
+@needs_ref
+def test_patched_writer_resolves_every_simple_name(tmp_path):
+    """The name check of the committed classes, on the patched reference file:
+    GpuBSDBWriter is the one new name, from the same package (jni/)."""
+    src = _strip_comments(_patched_writer(tmp_path))
+    body = re.sub(r"^(package|import)\s+[^;]+;", "", re.sub(r'"[^"\n]*"', '""', src), flags=re.M)
+    used = set(re.findall(r"\bnew\s+([A-Z]\w*)", body)) | set(re.findall(r"\b([A-Z]\w*)\s+gpu\b", body))
+    assert "GpuBSDBWriter" in used
+    gpu_src = open(os.path.join(ROOT, "jni", "GpuBSDBWriter.java")).read()
+    assert re.search(r"^package\s+tech\.bsdb\.write;", gpu_src, re.M) and "public class GpuBSDBWriter" in gpu_src
+
+
+def _java_type_of(arg: str, caller_src: str) -> str:
+    """Static type of a constructor argument in a caller: a literal, or the
+    declared type of a local / parameter / field of that name."""
+    a = arg.strip()
+    if a == "null":
+        return "null"
+    if a in ("true", "false"):
+        return "boolean"
+    if re.fullmatch(r"[\d\s*+()]+", a):
+        return "int"
+    m = re.search(r"\b(File|int|long|boolean|String)\s+" + re.escape(a) + r"\s*[=;,)]", caller_src)
+    assert m, f"no declaration of {a}"
+    return m.group(1)
+
+
+@needs_ref
+@pytest.mark.parametrize("caller,line", W_CALLERS)
+def test_reference_callers_construct_the_patched_writer_unchanged(caller, line, tmp_path):
+    """Builder.java:86, ParquetBuilder.java:90 and BSDBWriterTest.java:34 keep
+    `new BSDBWriter(...)`: their argument lists resolve against the patched
+    constructor (which is the reference's, unchanged) and so against
+    GpuBSDBWriter's (the same parameter types, test_writer_drop_in_keeps_the_reference_api)."""
+    src = _strip_comments(_patched_writer(tmp_path))
+    sig = re.search(r"public\s+BSDBWriter\s*\(([^)]*)\)", src).group(1)
+    params = [tuple(p.split()) for p in _split_args(sig)]
+    assert params == W_CTOR_PARAMS
+    path = os.path.join(REF_ROOT, caller)
+    lines = open(path).read().splitlines()
+    m = re.search(r"new\s+BSDBWriter\s*\((.*)\)\s*;", lines[line - 1])
+    assert m, lines[line - 1]
+    ctx_src = open(path).read()
+    if caller.endswith("BSDBWriterTest.java"):  # basePath is BaseTest's field, the test's parameters are below
+        ctx_src += open(os.path.join(REF_ROOT, "src/test/java/tech/bsdb/BaseTest.java")).read()
+    args = _split_args(m.group(1))
+    assert len(args) == len(params)
+    widen = {("int", "long")}
+    for a, (ptype, pname) in zip(args, params):
+        t = _java_type_of(a, ctx_src)
+        ok = t == ptype or (t, ptype) in widen or (t == "null" and ptype == "File")
+        assert ok, f"{caller}:{line}: argument {a!r} ({t}) for {ptype} {pname}"
+
+
+def test_writer_test_call_takes_a_path_govassembler_accepts():
+    """BSDBWriterTest.java:34 passes tmpDir = null and checksumBits = 0: the GPU
+    writer never dereferences tmpDir, and width 0 exports no checksum words
+    (sig = null), which GovAssembler.assemble accepts (GOV:510-511:
+    signatureMask 0, signatures null)."""
+    w = _strip_comments(open(os.path.join(ROOT, "jni", "GpuBSDBWriter.java")).read())
+    assert not re.search(r"\btmpDir\s*\.", w)
+    g = _strip_comments(open(os.path.join(ROOT, "jni", "GovAssembler.java")).read())
+    assert "final long[] sig = width == 0 ? null :" in re.sub(r"\s+", " ", g)
+    guard = re.search(r"if \((E\.length < 2[^{]*)\)\s*throw new IllegalArgumentException", re.sub(r"\s+", " ", g)).group(1)
+    assert "(width != 0 && sigWords == null)" in guard
+    assert re.search(r'if \(width == 0\) \{\s*set\(f, "signatureMask", 0L\);\s*set\(f, "signatures", null\);', g)
+    # the C side: bsdb_mph_sizes gives 0 checksum words at width 0
+    lib = ctypes.CDLL(LIB)
+    out = [ctypes.c_uint64() for _ in range(4)]
+    assert lib.bsdb_mph_sizes(ctypes.c_uint64(8290050), ctypes.c_uint32(0), *[ctypes.byref(o) for o in out]) == 0
+    assert out[3].value == 0
+
+
+def test_index_batches_are_pass_scoped():
+    """kvWriter.forEach starts new threads every pass (Common.java:287),
+    so the pass loop's per-thread batches come from a pool and go back to it
+    after each pass; value buffers exist only in approximate mode."""
+    w = re.sub(r"\s+", " ", _strip_comments(open(os.path.join(ROOT, "jni", "GpuBSDBWriter.java")).read()))
+    loop = w[w.index("private void passLoop()"):]
+    assert loop.index("for (long p = 0;") < loop.index("ThreadLocal.withInitial") < loop.index("kvWriter.forEach")
+    assert "pool.addAll(inPass);" in loop
+    assert "value8 = records && approximate ?" in w and "vlen = records && approximate ?" in w
