@@ -179,6 +179,73 @@ def c4_exact_passes(ctx, keys, n: int, width: int):
                     "(8 B x n, byte-reversed addr = 0x1000 + 48 i) in host memory"}
 
 
+def e4_ranks_full_build(ctx, world: int, rank: int, backend: str, width: int, reps: int, n_total: int):
+    """The N > 1 full build, one rank per GPU: each rank
+    holds its contiguous key shard of n_total keys in HBM (13 B each, the
+    headline's recipe) and the timed region is the product's whole build --
+    hash the shard, group (sig0, sig1, addr) by bucket-range owner, ONE
+    all-to-all, the range build (sort, solve, sign, ranks) into O(n/G) windows,
+    each rank's index.db slots placed from its ranks and copied to host
+    memory, every window sent to rank 0, which assembles E / values /
+    checksum words (distributed.sharded_full_build).  n_total defaults to C4's
+    per-GPU share at 8 GPUs times N (C4 itself at N = 8; weak scaling): C4's
+    whole key set on fewer GPUs exceeds one GPU's HBM without passes.  Returns
+    the max over ranks of each rep's wall time (barrier on both sides)."""
+    import time as _t
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    from bsdb_amd.distributed import DeviceBuild, sharded_full_build
+    lo, hi = shard(n_total, rank, world)
+    nloc = hi - lo
+    keys = ctx.gen_keys13(lo, nloc)
+    addr = torch.arange(lo, hi, dtype=torch.int64, device="cuda") * 48 + 0x1000  # SimpleCompact 48-B records
+    host_index = None
+    times, stage = [], None
+    red_dev = "cuda" if backend == "nccl" else "cpu"
+    for rep in range(reps + 1):  # rep 0 warms the workspace and the allocator
+        torch.cuda.synchronize()
+        dist.barrier()
+        t0 = _t.perf_counter()
+        sig = ctx.hash_fixed(keys[: 13 * nloc], 13)
+        torch.cuda.synchronize()
+        t1 = _t.perf_counter()
+        res = sharded_full_build(DeviceBuild(ctx), sig, addr, n_total, width)
+        del sig
+        torch.cuda.synchronize()
+        t2 = _t.perf_counter()
+        idx = res["index"]
+        if host_index is None or host_index.numel() < idx.numel():
+            host_index = torch.empty(idx.numel(), dtype=torch.int64)
+        host_index[: idx.numel()].copy_(idx)  # index.db slots of this rank's range, in host memory
+        t3 = _t.perf_counter()
+        dist.barrier()
+        t4 = _t.perf_counter()
+        local = torch.tensor([t4 - t0, t1 - t0, t2 - t1, t3 - t2], dtype=torch.float64, device=red_dev)
+        dist.all_reduce(local, op=dist.ReduceOp.MAX)
+        if rep:
+            times.append(local.tolist())
+        ok = rank != 0 or int(res["E"][-1].item()) & ((1 << 56) - 1) == n_total
+        flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=red_dev)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        sent = torch.tensor([res["bytes_sent"]], dtype=torch.float64, device=red_dev)
+        dist.all_reduce(sent, op=dist.ReduceOp.MAX)
+        del res, idx
+    del keys, addr, host_index
+    torch.cuda.empty_cache()
+    ctx.release_workspace()
+    best = min(times, key=lambda t: t[0])
+    return {"n_keys": n_total, "checksum_bits": width, "ranks": world, "keys_per_s": n_total / best[0],
+            "ms": best[0] * 1e3, "reps": reps,
+            "stage_ms_max_over_ranks": {"hash": best[1] * 1e3, "exchange_build_assemble": best[2] * 1e3,
+                                        "index_d2h": best[3] * 1e3},
+            "max_bytes_sent_per_rank": float(sent.item()), "check": {"E[m]==n": bool(flag.item())},
+            "scaling": "weak (C4/8 keys per GPU; C4 at N = 8)",
+            "path": "per rank: shard keys in HBM -> hash -> owner partition -> ONE all-to-all of (sig0, sig1, addr) "
+                    "-> bsdb_dev_gov_build_window (sort, solve, sign, ranks) -> index slots to host memory; "
+                    "windows to rank 0 (point to point), which ORs them into the GOV structure"}
+
+
 def _roomiest_dir(need_bytes: float):
     """The candidate directory with the most free space, or None when none has
     room for `need_bytes` (the figure then writes to /dev/null and says so)."""
@@ -419,6 +486,9 @@ def main():
     ap.add_argument("--no-full-build", action="store_true", help="skip the full-build figures")
     ap.add_argument("--e4-devices", type=int, default=1,
                     help="GPUs of the one-process E4 full-build figure (0 = skip it); never more than asked")
+    ap.add_argument("--e4-keys", type=int, default=0,
+                    help="N>1: keys of the E4 full-build leg over the ranks (0 = C4's per-GPU share x N)")
+    ap.add_argument("--e4-reps", type=int, default=1, help="N>1: timed reps of the E4 leg (after one warm rep)")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="collective backend (nccl = RCCL over xGMI; gloo only to rehearse N ranks on one GPU)")
     args = ap.parse_args()
@@ -619,6 +689,19 @@ def main():
         if not args.no_cpu:
             full["cpu_c1"] = full_build_cpu(1_000_000, 4, args.cpu_threads)
         log("full-build figures done")
+    if world > 1 and not args.no_full_build:
+        # the product's full build at N ranks (E4) beside the histogram stage;
+        # every rank joins, rank 0 reports (after the headline's keys are freed)
+        del keys
+        torch.cuda.empty_cache()
+        ctx.release_workspace()
+        n_e4 = args.e4_keys if args.e4_keys > 0 else -(-README_N * world // 8)
+        full = {}
+        try:
+            full["e4_ranks_full_build"] = e4_ranks_full_build(ctx, world, rank, args.backend, 4, args.e4_reps, n_e4)
+        except Exception as e:  # recorded, not faked; the headline line is printed regardless
+            full["e4_ranks_full_build"] = {"error": repr(e)[:300]}
+        log("E4 full build over the ranks done")
     if rank == 0:
         cpu = None
         if not args.no_cpu and world == 1:  # the CPU baseline is an N = 1 figure

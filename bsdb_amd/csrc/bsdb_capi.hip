@@ -1617,6 +1617,48 @@ int bsdb_dev_gov_build_range(bsdb_ctx *c, const uint64_t *d_sig, uint64_t n_loca
                           false);
 }
 
+// The value words and checksum words the range [e_lo, e_lo + n_local) of keys
+// writes (store_bucket: words [vo >> 5, (vo + nv + 31) >> 5) of its vertices,
+// the checksum fields of its ranks).
+int bsdb_gov_range_windows(uint64_t n_global, uint32_t width, uint64_t e_lo, uint64_t n_local, uint64_t *out4) {
+    if (!out4 || width > 64 || e_lo + n_local > n_global || n_global > (1ULL << 56)) return BSDB_EINVAL;
+    auto vo = [](uint64_t x) { return (x * 281) >> 8; };  // vertexOffset (GOV:315-317)
+    const uint64_t v_lo = vo(e_lo), v_hi = vo(e_lo + n_local);
+    out4[0] = v_lo >> 5;
+    out4[1] = ((v_hi + 31) >> 5) - out4[0];
+    out4[2] = width ? (e_lo * width) >> 6 : 0;
+    out4[3] = width ? ((((e_lo + n_local) * width) + 63) >> 6) - out4[2] : 0;
+    return BSDB_OK;
+}
+
+int bsdb_dev_gov_build_window(bsdb_ctx *c, const uint64_t *d_sig, uint64_t n_local, uint64_t n_global, uint64_t b_lo,
+                              uint64_t b_hi, uint64_t e_lo, uint32_t width, uint64_t *d_E_win, uint64_t *d_values_win,
+                              uint64_t values_w0, uint64_t values_words, uint64_t *d_sigbits_win, uint64_t sig_w0,
+                              uint64_t sig_words, int64_t *d_rank, void *stream) {
+    const uint64_t m = n_global / BUCKET_SIZE + 1;
+    uint64_t need[4];
+    if (!c || width > 64 || !d_E_win || !d_values_win || (n_local && !d_sig) || (width && !d_sigbits_win) ||
+        !aligned16(d_sig) || m > 0x7FFFFFFFULL || b_lo >= b_hi || b_hi > m || n_local > n_global ||
+        e_lo + n_local > n_global || bsdb_gov_range_windows(n_global, width, e_lo, n_local, need) != BSDB_OK)
+        return BSDB_EINVAL;
+    // the windows must hold every word the range writes
+    if (values_w0 > need[0] || values_w0 + values_words < need[0] + need[1] ||
+        (width && (sig_w0 > need[2] || sig_w0 + sig_words < need[2] + need[3])))
+        return BSDB_EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    HIP_OK(hipSetDevice(c->device));
+    hipStream_t s = pick(c, stream);
+    Ordered ord(c, s);
+    // the range build indexes the structure globally: its bases are moved so
+    // that every index it forms lands in the windows (no other word is touched)
+    auto shift = [](uint64_t *p, uint64_t first) {
+        return reinterpret_cast<uint64_t *>(reinterpret_cast<uintptr_t>(p) - (uintptr_t)first * 8);
+    };
+    return gov_build_impl(c, d_sig, n_local, n_global, b_lo, b_hi, e_lo, width, shift(d_E_win, b_lo),
+                          shift(d_values_win, values_w0), width ? shift(d_sigbits_win, sig_w0) : nullptr, d_rank, s,
+                          false);
+}
+
 int bsdb_dev_partition_owners(bsdb_ctx *c, const uint64_t *d_sig, const uint64_t *d_payload, uint64_t n, uint64_t m,
                               int nranks, uint64_t *d_out, uint64_t *d_payload_out, uint64_t *h_counts, void *stream) {
     if (!c || nranks < 1 || nranks > OWN_MAXR || m == 0 || m > 0x7FFFFFFFULL || !h_counts ||

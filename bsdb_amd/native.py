@@ -45,6 +45,9 @@ SIGNATURES = [
     ("bsdb_dev_gov_build", _i, [_vp, _vp, _u64, _u32, _vp, _vp, _vp, _vp]),
     ("bsdb_dev_gov_build_ranks", _i, [_vp, _vp, _u64, _u32, _vp, _vp, _vp, _vp, _vp]),
     ("bsdb_dev_gov_build_range", _i, [_vp, _vp, _u64, _u64, _u64, _u64, _u64, _u32, _vp, _vp, _vp, _vp, _vp]),
+    ("bsdb_gov_range_windows", _i, [_u64, _u32, _u64, _u64, _vp]),
+    ("bsdb_dev_gov_build_window", _i, [_vp, _vp, _u64, _u64, _u64, _u64, _u64, _u32, _vp, _vp, _u64, _u64, _vp, _u64,
+                                       _u64, _vp, _vp]),
     ("bsdb_dev_mph_build_index_passes_fixed", _i, [_vp, _vp, _u32, _u64, _u32, _u32, _vp, _u64, _u64, _vp, _vp,
                                                    _vp, _vp, _vp, C.POINTER(_u32), _vp]),
     ("bsdb_dev_mph_build_index_passes_var", _i, [_vp, _vp, _u64, _vp, _u64, _u32, _u32, _vp, _u64, _u64, _vp, _vp,
@@ -166,6 +169,14 @@ def mph_sizes(n: int, width: int) -> dict:
     m, vw, vb, sw = C.c_uint64(), C.c_uint64(), C.c_uint64(), C.c_uint64()
     _check("bsdb_mph_sizes", lib().bsdb_mph_sizes(n, width, C.byref(m), C.byref(vw), C.byref(vb), C.byref(sw)))
     return {"num_buckets": m.value, "values_words": vw.value, "value_bits": vb.value, "sig_words": sw.value}
+
+
+def range_windows(n_global: int, width: int, e_lo: int, n_local: int):
+    """bsdb_gov_range_windows: (values_w0, values_words, sig_w0, sig_words), the
+    words the keys [e_lo, e_lo + n_local) of a range build write (host only)."""
+    out = (C.c_uint64 * 4)()
+    _check("bsdb_gov_range_windows", lib().bsdb_gov_range_windows(n_global, width, e_lo, n_local, out))
+    return tuple(int(x) for x in out)
 
 
 def _ptr(t) -> int:
@@ -325,6 +336,18 @@ class Context:
         _check("bsdb_dev_gov_build_range", lib().bsdb_dev_gov_build_range(
             self._h, _ptr(sig), sig.shape[0], n_global, b_lo, b_hi, e_lo, width, _ptr(E), _ptr(values),
             _ptr(sigbits) if sigbits is not None else None, _ptr(rank) if rank is not None else None, _stream(stream)))
+
+    def gov_build_window(self, sig, n_global: int, b_lo: int, b_hi: int, e_lo: int, width: int, E_win, values_win,
+                         values_w0: int, sigbits_win=None, sig_w0: int = 0, rank=None, stream=None):
+        """E4 with O(n/G) memory: the range build into zeroed windows of the
+        structure (E[b_lo..b_hi], value words from values_w0, checksum words
+        from sig_w0; range_windows gives the words the range writes)."""
+        assert E_win.numel() >= b_hi - b_lo + 1
+        _check("bsdb_dev_gov_build_window", lib().bsdb_dev_gov_build_window(
+            self._h, _ptr(sig), sig.shape[0], n_global, b_lo, b_hi, e_lo, width, _ptr(E_win), _ptr(values_win),
+            values_w0, values_win.numel(), _ptr(sigbits_win) if sigbits_win is not None else None, sig_w0,
+            sigbits_win.numel() if sigbits_win is not None else 0, _ptr(rank) if rank is not None else None,
+            _stream(stream)))
 
     def mph_build_index_passes(self, keys, key_len: int, n: int, width: int, passes: int = 0, offsets=None,
                                addr=None, addr_base: int = 0, addr_stride: int = 0, index=None, stream=None):

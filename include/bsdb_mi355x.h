@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define BSDB_ABI_VERSION 5
+#define BSDB_ABI_VERSION 6
 
 /* Return codes (negative errno-style). */
 #define BSDB_OK          0
@@ -166,6 +166,22 @@ int bsdb_dev_gov_build_ranks(bsdb_ctx *ctx, const uint64_t *d_sig, uint64_t n, u
 int bsdb_dev_gov_build_range(bsdb_ctx *ctx, const uint64_t *d_sig, uint64_t n_local, uint64_t n_global,
                              uint64_t b_lo, uint64_t b_hi, uint64_t e_lo, uint32_t width, uint64_t *d_E,
                              uint64_t *d_values, uint64_t *d_sigbits, int64_t *d_rank, void *stream);
+/* E4 with O(n/G) memory per rank (ABI 6): the same range build into windows
+ * of the structure instead of full-size arrays.  d_E_win holds E[b_lo..b_hi]
+ * (b_hi - b_lo + 1 entries; E[b_hi] is zeroed again unless b_hi == m, as
+ * above); d_values_win the value words [values_w0, values_w0 + values_words);
+ * d_sigbits_win the checksum words [sig_w0, sig_w0 + sig_words) -- all zeroed
+ * by the caller, and covering the words the range writes, which
+ * bsdb_gov_range_windows gives as {values_w0, values_words, sig_w0, sig_words}
+ * (BSDB_EINVAL otherwise).  A word shared with the next or the previous range
+ * holds only this range's bits: the structure is the windows OR-ed at their
+ * positions (distributed.py's assembly on rank 0). */
+int bsdb_gov_range_windows(uint64_t n_global, uint32_t width, uint64_t e_lo, uint64_t n_local, uint64_t *out4);
+int bsdb_dev_gov_build_window(bsdb_ctx *ctx, const uint64_t *d_sig, uint64_t n_local, uint64_t n_global,
+                              uint64_t b_lo, uint64_t b_hi, uint64_t e_lo, uint32_t width, uint64_t *d_E_win,
+                              uint64_t *d_values_win, uint64_t values_w0, uint64_t values_words,
+                              uint64_t *d_sigbits_win, uint64_t sig_w0, uint64_t sig_words, int64_t *d_rank,
+                              void *stream);
 /* The whole build of a key set resident in this device's HBM (C4: 13.19e9 x
  * 13 B; C5: 4e9 var-len) by sequential bucket-range passes: pass p of P covers
  * buckets [p*m/P, (p+1)*m/P) (the reference's 256 spill segments are such

@@ -47,7 +47,7 @@ def test_host_only_calls(lib):
     lib.bsdb_num_buckets.argtypes = [C.c_uint64]
     assert lib.bsdb_num_buckets(13_193_787_549) == 8_795_859
     assert lib.bsdb_num_buckets(0) == 1
-    assert lib.bsdb_abi_version() == 5
+    assert lib.bsdb_abi_version() == 6
     hdr = open(os.path.join(ROOT, "include", "bsdb_mi355x.h")).read()
     assert f"#define BSDB_ABI_VERSION {lib.bsdb_abi_version()}" in hdr
 

@@ -9,7 +9,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from bsdb_amd.distributed import TILE, global_histogram, shard
+from bsdb_amd.distributed import TILE, global_histogram, range_windows, shard
 
 
 def test_shard_cover():
@@ -120,17 +120,31 @@ class OracleBuild:
         counts = [int((own == g).sum()) for g in range(world)]
         return sig[torch.from_numpy(order)], addr[torch.from_numpy(order)], counts
 
-    def build_range(self, sig, n_global, b_lo, b_hi, e_lo, width, E, values, sigbits):
-        sb = sigbits if sigbits is not None else torch.zeros(1, dtype=torch.int64)
-        rc = self.O.gov_build_range(sig.numpy().view(np.uint64), n_global, b_lo, b_hi, e_lo, width,
-                                    E.numpy().view(np.uint64), values.numpy().view(np.uint64),
-                                    sb.numpy().view(np.uint64), 2)
-        assert rc == 0
+    def build_window(self, sig, n_global, b_lo, b_hi, e_lo, width, E_win, values_win, values_w0, sig_win, sig_w0):
+        """The oracle's range build into full-size arrays (small test sets),
+        cut to the windows DeviceBuild fills; the full arrays stay for the
+        lookups of index_slice."""
+        m = n_global // 1500 + 1
+        E = np.zeros(m + 1, np.uint64)
+        vals = np.zeros((2 * (1 + ((n_global * 281) >> 8)) + 63) // 64, np.uint64)
+        sb = np.zeros((n_global * width + 63) // 64 + 1 if width else 1, np.uint64)
+        s = sig.numpy().view(np.uint64)
+        assert self.O.gov_build_range(s, n_global, b_lo, b_hi, e_lo, width, E, vals, sb, 2) == 0
+        # nothing outside the range's windows was written
+        v0, vn, s0, sn = range_windows(n_global, width, e_lo, s.size // 2)
+        assert not vals[:v0].any() and not vals[v0 + vn:].any()
+        if width:
+            assert not sb[:s0].any() and not sb[s0 + sn:].any()
+        E_win.numpy().view(np.uint64)[: b_hi - b_lo + 1] = E[b_lo: b_hi + 1]
+        values_win.numpy().view(np.uint64)[:vn] = vals[v0: v0 + vn]
+        if width:
+            sig_win.numpy().view(np.uint64)[:sn] = sb[s0: s0 + sn]
+        E[b_hi] = e_lo + s.size // 2  # (the lookups of index_slice need the range's end)
+        self._full = (s, n_global, E, vals, width, sb if width else None)
 
-    def index_slice(self, sig, addr, n_global, E, values, width, sigbits, e_lo, n_local):
-        sb = sigbits.numpy().view(np.uint64) if sigbits is not None else None
-        r = self.O.lookup_batch(sig.numpy().view(np.uint64), n_global, E.numpy().view(np.uint64),
-                                values.numpy().view(np.uint64), width, sb, True)
+    def index_slice(self, addr, e_lo, n_local):
+        s, n_global, E, vals, width, sb = self._full
+        r = self.O.lookup_batch(s, n_global, E, vals, width, sb, True)
         assert r.min() >= e_lo and r.max() < e_lo + n_local
         idx = np.zeros(n_local, ">u8")
         idx[r - e_lo] = addr.numpy().view(np.uint64)
@@ -199,10 +213,21 @@ def run_e4(world, n, width, tmp_path, use_gpu, pg="gloo"):
     exp = np.zeros(n, ">u8")
     exp[ranks] = np.arange(n, dtype=np.uint64) * 48 + 4096
     assert open(path, "rb").read() == exp.tobytes()
-    # every other rank keeps its own fields (the reduce leaves only rank 0 defined)
+    # every other rank keeps its windows: E[b_lo..b_hi), its value and checksum
+    # words (a boundary word holds only this rank's bits of it)
     for g in range(1, world):
         lo, hi = res[g]["b_lo"], res[g]["b_hi"]
-        np.testing.assert_array_equal(res[g]["E"].view(np.uint64)[lo:hi], E[lo:hi])
+        if lo >= hi:
+            continue
+        assert res[g]["E_b0"] == lo
+        np.testing.assert_array_equal(res[g]["E"].view(np.uint64)[: hi - lo], E[lo:hi])
+        v0, vn, s0, sn = range_windows(n, width, res[g]["e_lo"], res[g]["n_local"])
+        assert res[g]["values_w0"] == v0
+        w = res[g]["values"].view(np.uint64)[:vn]
+        np.testing.assert_array_equal(w[1:-1], vals[v0 + 1: v0 + vn - 1])
+        assert not (w & ~vals[v0: v0 + vn]).any()
+        # bytes this rank moved: its exchange payload plus its windows, O(n / G)
+        assert res[g]["bytes_sent"] <= 24 * (n // world + 8192) + 8 * (hi - lo + 1 + vn + sn) + 64
 
 
 @pytest.mark.parametrize("world", [2, 3])
@@ -236,3 +261,25 @@ def test_nccl_full_build_device_tensors(tmp_path):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     run_e4(1, 400_003, 4, tmp_path, use_gpu=True, pg="nccl")
+
+
+def test_range_windows_equal_the_abi():
+    """distributed.range_windows == bsdb_gov_range_windows (host arithmetic, no
+    device), and consecutive ranges' windows tile the structure's words with
+    at most one shared word at each boundary."""
+    from bsdb_amd.native import range_windows as abi_windows
+    for n, width, cuts in [(1_000_000, 4, [0, 1, 333_333, 999_999, 1_000_000]),
+                           (13_193_787_549, 4, [0, 1_649_223_443, 6_596_893_774, 13_193_787_549]),
+                           (4_000_000_000, 16, [0, 500_000_001, 4_000_000_000]), (2_000, 0, [0, 700, 2_000])]:
+        vw = (2 * (1 + ((n * 281) >> 8)) + 63) // 64
+        sw = (n * width + 63) // 64
+        prev = None
+        for a, b in zip(cuts, cuts[1:]):
+            w = range_windows(n, width, a, b - a)
+            assert w == abi_windows(n, width, a, b - a)
+            assert w[0] + w[1] <= vw and w[2] + w[3] <= max(sw, 1)
+            if prev is not None:
+                assert prev[0] + prev[1] - 1 <= w[0] <= prev[0] + prev[1]
+                if width:
+                    assert prev[2] + prev[3] - 1 <= w[2] <= prev[2] + prev[3]
+            prev = w
