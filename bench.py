@@ -33,6 +33,17 @@ HBM_PEAK_GBS = 8000.0         # MI355X_MICROARCH.md chip table: 8.0 TB/s HBM3E
 
 
 
+def _lib_sha256():
+    """sha256 of the HIP library this process loads (BSDB_LIB or the in-tree build)."""
+    import hashlib
+    path = os.environ.get("BSDB_LIB") or os.path.join(ROOT, "bsdb_amd", "libbsdb_mi355x.so")
+    h = hashlib.sha256()
+    with open(path, "rb") as f:
+        for b in iter(lambda: f.read(1 << 20), b""):
+            h.update(b)
+    return h.hexdigest()
+
+
 def _oracle():
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
@@ -316,21 +327,36 @@ def e2e_c4_host_passes(ctx, n: int, width: int, chunk: int = 1 << 28):
                                                   "box had room for 8n bytes")}
 
 
-def e2e_c2_kv_to_disk(ctx, n: int, width: int, partitions: int = 8):
-    """BASELINE C2 from the DATA FILES: n records of 13-byte keys and 32-byte
-    values in SimpleCompactKVWriter's layout (48-byte records, kv.db.<p>,
-    written before the clock) -> bsdb_kv_build_index (host threads parse the
-    partitions and stream them into the builder; bucket-range-pass build;
-    index.db) + hash.dump.  The reference's buildIndex reads the same files
-    (W:134, PartitionedKVWriter.java:50-70)."""
+def usable_cpus() -> int:
+    """CPUs this process may use: the affinity mask capped by the cgroup quota
+    (the GPU box's os.cpu_count() counts the whole machine)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(quota) // int(period)))
+    except (OSError, ValueError):
+        pass
+    return max(1, n)
+
+
+def e2e_kv_to_disk(ctx, n: int, width: int, partitions: int = 8, approximate: bool = False):
+    """BASELINE C2 / C3 from the DATA FILES: n records of 13-byte keys and
+    32-byte values in SimpleCompactKVWriter's layout (48-byte records,
+    kv.db.<p>, written before the clock) -> bsdb_kv_build_index (host threads
+    parse the partitions and stream them into the builder; bucket-range-pass
+    build; index.db, and index_a.db's value slots in approximate mode) +
+    hash.dump.  The reference's buildIndex reads the same files (W:134,
+    PartitionedKVWriter.java:50-70), which its writer splits into
+    2 x availableProcessors() partitions (PartitionedKVWriter.java:14)."""
     import shutil
     import tempfile
     import time as _t
-    import numpy as np
     import torch
-    d, _ = _roomiest_dir(48 * n + 8 * n)
+    need = 48 * n + 8 * n * (2 if approximate else 1)
+    d, _ = _roomiest_dir(need)
     if d is None:
-        return {"skipped": f"no directory with {56 * n / 1e9:.1f} GB free"}
+        return {"skipped": f"no directory with {need / 1e9:.1f} GB free"}
     tmp = tempfile.mkdtemp(prefix="bsdb_kv_", dir=d)
     try:
         base = os.path.join(tmp, "kv.db")
@@ -349,22 +375,24 @@ def e2e_c2_kv_to_disk(ctx, n: int, width: int, partitions: int = 8):
                     rec.cpu().numpy().tofile(f)
                     del rec
         torch.cuda.empty_cache()
-        ip = os.path.join(tmp, "index.db")
+        ip, ap = os.path.join(tmp, "index.db"), os.path.join(tmp, "index_a.db")
         t0 = _t.perf_counter()
-        mph = ctx.kv_build_index(base, partitions, width, ip, os.path.join(tmp, "index_a.db"))
+        mph = ctx.kv_build_index(base, partitions, width, ip, ap, approximate=approximate)
         mph.dump(os.path.join(tmp, "hash.dump"))
         dt = _t.perf_counter() - t0
-        size = os.path.getsize(ip)
+        size, asize = os.path.getsize(ip), os.path.getsize(ap)
         E, _, _ = mph.export()
         ok = int(E[-1]) & ((1 << 56) - 1) == n
         mph.close()
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
-    return {"n_keys": n, "checksum_bits": width, "partitions": partitions, "keys_per_s": n / dt, "ms": dt * 1e3,
-            "kv_db_bytes": 48 * n, "check": {"E[m]==n": ok, "index.db bytes == 8n": size == 8 * n},
-            "path": f"kv.db.<p> files ({48 * n / 1e9:.1f} GB, compact layout, in {d}) -> bsdb_kv_build_index "
-                    "(parallel partition scan streamed into the builder, bucket-range-pass build) -> index.db + "
-                    "index_a.db (empty) + hash.dump"}
+    return {"n_keys": n, "checksum_bits": width, "partitions": partitions, "approximate": approximate,
+            "keys_per_s": n / dt, "ms": dt * 1e3, "kv_db_bytes": 48 * n, "host_cpus": usable_cpus(),
+            "check": {"E[m]==n": ok, "index.db bytes == 8n": size == 8 * n,
+                      "index_a.db bytes": asize == (8 * n if approximate else 0)},
+            "path": f"kv.db.<p> files ({48 * n / 1e9:.1f} GB, compact layout, {partitions} partitions, in {d}) -> "
+                    "bsdb_kv_build_index (parallel partition scan streamed into the builder, bucket-range-pass "
+                    "build) -> index.db" + (" + index_a.db" if approximate else "") + " + hash.dump"}
 
 
 def single_pass_ab(ctx, keys, n: int, m: int, ref_counts, reps: int = 3):
@@ -630,13 +658,21 @@ def main():
         p1_avg_s = p1_ms / 1e3 / max(p1_launches, 1)
         keys_per_launch = p1_keys / max(p1_launches, 1)
         achieved = KEY_LEN * keys_per_launch / p1_avg_s / 1e9        # GB/s, algorithmic bytes
-        traffic = None
+        # PMC bytes per launch (profiles/pmc_pass1_latest.json), reported only
+        # for the library the counters were collected with and the same launch
+        # shape; otherwise null (a kernel change re-collects them)
+        traffic, traffic_src = None, None
         prof = os.path.join(ROOT, "profiles", "pmc_pass1_latest.json")
         if os.path.exists(prof):
             try:
                 pj = json.load(open(prof))
-                if abs(pj.get("keys_per_launch", 0) - keys_per_launch) < 1.0:
-                    traffic = pj.get("hbm_bytes_per_launch")  # PMC bytes / launch (profiles/)
+                same_lib = pj.get("library_sha256") == _lib_sha256()
+                same_shape = abs(pj.get("keys_per_launch", 0) - keys_per_launch) < 1.0
+                traffic_src = {"file": "profiles/pmc_pass1_latest.json", "round": pj.get("round"),
+                               "library_sha256": pj.get("library_sha256"), "same_library": same_lib,
+                               "same_launch_shape": same_shape}
+                if same_lib and same_shape:
+                    traffic = pj.get("hbm_bytes_per_launch")
             except Exception:
                 traffic = None
         log(f"timed {args.steps} steps: {dt * 1e3 / args.steps:.2f} ms/step")
@@ -677,10 +713,17 @@ def main():
             full["e2e_c2_host_to_disk"] = e2e_host_to_disk(ctx, 100_000_000, 4)
         except OSError as e:  # (no room for 0.8 GB in /tmp: the figure is skipped, not faked)
             full["e2e_c2_host_to_disk"] = {"skipped": str(e)}
-        try:
-            full["e2e_c2_kv_to_disk"] = e2e_c2_kv_to_disk(ctx, 100_000_000, 4)
-        except Exception as e:  # recorded, not faked
-            full["e2e_c2_kv_to_disk"] = {"error": repr(e)[:300]}
+        # from the data files: C2 with 8 partitions and with the reference
+        # writer's 2 x cores, C3 (approximate index) with 2 x cores
+        kv_parts = 2 * usable_cpus()
+        for key, kn, parts, approx in (("e2e_c2_kv_to_disk", 100_000_000, 8, False),
+                                       ("e2e_c2_kv_to_disk_2xcores", 100_000_000, kv_parts, False),
+                                       ("e2e_c3_kv_to_disk", 1_000_000_000, kv_parts, True)):
+            try:
+                full[key] = e2e_kv_to_disk(ctx, kn, 4, parts, approx)
+            except Exception as e:  # recorded, not faked
+                full[key] = {"error": repr(e)[:300]}
+            log(f"{key} done")
         if args.e4_devices > 0:
             try:
                 full["e4_c3_multi_device"] = e4_multi_device(ctx, 1_000_000_000, 4, args.e4_devices)
@@ -734,7 +777,7 @@ def main():
             "roofline": {
                 "bound": "hbm", "kernel": "k_pass1 (hash+bucket+partition)",
                 "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                "traffic": traffic,
+                "traffic": traffic, "traffic_source": traffic_src,
                 "bytes_per_key": KEY_LEN, "keys_per_launch": keys_per_launch,
                 "avg_launch_ms": p1_avg_s * 1e3, "launches": p1_launches,
             },

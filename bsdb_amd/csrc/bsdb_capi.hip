@@ -1288,7 +1288,9 @@ static void print_gov_profile(const std::vector<uint64_t> &h, uint32_t solve_gri
                                "bfs_flip", "n_bfs_iters", "n_flip_steps", "n_sel_batches", "n_sel_picks",
                                "sel_pick_cycles", "sel_prep_cycles", "n_singular_solved", "n_null_vectors", "n_speculative_lost",
                                "n_fvs_blocks", "n_form_levels", "n_heavy", "gj_columns", "gj_barrier_wait_cycles",
-                               "unused"};
+                               "unused", "tarjan_prep", "tarjan_sweeps", "tarjan_compact",
+                               "gj_leader_cycles", "gj_follower_cycles", "gj_slot_columns", "gj_leader_columns",
+                               "gj_trailing_cycles", "gj_panels"};
     std::vector<double> tot(GP_N, 0.0);
     for (uint32_t w = 0; w < solve_grid; ++w)
         for (int k = 0; k < GP_N; ++k) {
@@ -1297,7 +1299,7 @@ static void print_gov_profile(const std::vector<uint64_t> &h, uint32_t solve_gri
         }
     fprintf(stderr, "[gov-profile] m=%llu grid=%u", (unsigned long long)m, solve_grid);
     for (int k = 0; k < GP_N; ++k)
-        fprintf(stderr, " %s=%.4g", names[k], k == GP_N_DENSE_MAX ? tot[k] : tot[k] / ((k < GP_N_SEEDS || (k >= GP_FVS_SEL && k <= GP_FVS_GJ) || k == GP_FAILED_CYCLES || k == GP_BFS_FLIP || k == GP_SEL_PICK_CYCLES || k == GP_SEL_PREP_CYCLES) ? solve_grid : 1));
+        fprintf(stderr, " %s=%.4g", names[k], k == GP_N_DENSE_MAX ? tot[k] : tot[k] / ((k < GP_N_SEEDS || (k >= GP_FVS_SEL && k <= GP_FVS_GJ) || k == GP_FAILED_CYCLES || k == GP_BFS_FLIP || k == GP_SEL_PICK_CYCLES || k == GP_SEL_PREP_CYCLES || (k >= GP_TJ_PREP && k <= GP_TJ_COMPACT)) ? solve_grid : 1));
     fprintf(stderr, "  (cycles: mean per workgroup; counts: totals)\n");
 }
 

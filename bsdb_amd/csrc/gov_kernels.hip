@@ -69,10 +69,11 @@ constexpr int GS_TINY = 12;      // brute-force buckets (only in sets of < ~1500
 #define GOV_GJ_PANEL 1
 #endif
 // LDS words of the panel form's scratch for n unknowns: the waves' pivot
-// slots (5 words each), a panel's recorded pivots (4 words a column), a
-// pivot's trailing words (both planes) for each of a panel's 64 columns
+// slots (5 words each), a panel's recorded pivots (4 words a column), the
+// trailing update's table (9 entries of both planes for each of a panel's 32
+// column pairs)
 __host__ __device__ constexpr size_t gj_panel_words(uint32_t n) {
-    return (size_t)(GOV_THREADS / 64) * 5 + (size_t)4 * 64 + (size_t)2 * 64 * ((n + 1 + 63) / 64);
+    return (size_t)(GOV_THREADS / 64) * 5 + (size_t)4 * 64 + (size_t)2 * 32 * 9;  // slots, pinfo, the pair table
 }
 #ifndef GOV_PICK_REPS
 // FVS: pairs of heavy hinges taken per stuck cascade (with the in x out pick
@@ -537,7 +538,8 @@ enum GovProf { GP_EDGES, GP_PEEL, GP_GREEDY, GP_BFS, GP_TARJAN, GP_SINGLE, GP_DE
                GP_N_FAIL_DEGEN, GP_N_FAIL_ORIENT, GP_N_FAIL_INCONS, GP_FAILED_CYCLES, GP_BFS_FLIP, GP_N_BFS_ITERS,
                GP_N_FLIP_STEPS, GP_N_SEL_BATCHES, GP_N_SEL_PICKS, GP_SEL_PICK_CYCLES, GP_SEL_PREP_CYCLES,
                GP_N_SING_SOLVED, GP_N_NULL_VECS, GP_N_SPEC_LOST, GP_N_FVS_BLOCKS, GP_N_FORM_LEVELS, GP_N_HEAVY,
-               GP_GJ_COLUMNS, GP_GJ_BARRIER, GP_GJ_ROWS_WAVE7, GP_N };
+               GP_GJ_COLUMNS, GP_GJ_BARRIER, GP_GJ_ROWS_WAVE7, GP_TJ_PREP, GP_TJ_SWEEP, GP_TJ_COMPACT,
+               GP_GJ_LEAD, GP_GJ_FOLLOW, GP_GJ_SLOTCOLS, GP_GJ_LEADCOLS, GP_GJ_TRAIL, GP_GJ_PANELS, GP_N };
 
 // Solver state for buckets of up to CMAX_ keys: LDS for GS_CMAX, a global
 // slab per workgroup for GB_CMAX (same code; indices fit int16 either way).
@@ -602,6 +604,21 @@ __device__ __forceinline__ void gf3_add(uint64_t &x1, uint64_t &x2, uint64_t y1,
     x2 = (a2 & ~y1 & ~y2) | (~a1 & ~a2 & y2) | (a1 & y1);
 }
 
+// The single-wave phases (greedy and BFS orientation, the Tarjan walk, the
+// singletons, the FVS closure, the Gauss-Jordan leader) hold up their whole
+// workgroup: that wave takes the highest issue priority while it works, so
+// the co-resident waves of the CU's other solver workgroup (throughput work)
+// do not delay it at its SIMD.  GOV_PRIO=0 builds the form without.
+#ifndef GOV_PRIO
+#define GOV_PRIO 1
+#endif
+__device__ __forceinline__ void crit_on() {
+    if (GOV_PRIO) __builtin_amdgcn_s_setprio(3);
+}
+__device__ __forceinline__ void crit_off() {
+    if (GOV_PRIO) __builtin_amdgcn_s_setprio(0);
+}
+
 // Phase counters; P = false (production) compiles them away, so the
 // profiling pointer and clock hold no registers in the solver.
 template <bool P>
@@ -619,6 +636,11 @@ struct PhaseClock {
     }
     __device__ void add(int slot, uint64_t v) { if (on() && threadIdx.x == 0) acc[slot] += v; }
     __device__ void max(int slot, uint64_t v) { if (on() && threadIdx.x == 0 && v > acc[slot]) acc[slot] = v; }
+    // from lane 0 of any wave (the counters are summed atomically)
+    __device__ void add_any(int slot, uint64_t v) {
+        if (on() && (threadIdx.x & 63) == 0) atomicAdd((unsigned long long *)(acc + slot), (unsigned long long)v);
+    }
+    __device__ uint64_t now() const { return on() ? clock64() : 0; }
 };
 
 // In-place exclusive scan of a[0..n) by the whole workgroup, 3 * GS_THREADS
@@ -794,6 +816,7 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
     // later lanes clear the chosen vertex and take j's decrements.
     // Together, the sequential outcome.
     if (tid < 64) {
+        crit_on();  // (the one wave working: first at its SIMD)
         uint32_t *firstl = L.xe;  // (dead after peeling) lowest lane of the chunk touching a vertex
         uint32_t *ccnt = L.deg;   // core edges to come per vertex (the peel's degrees)
         auto pick = [](bool f0, bool f1, bool f2, uint32_t c0, uint32_t c1, uint32_t c2, uint32_t v0, uint32_t v1,
@@ -894,6 +917,7 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
         for (uint32_t v = tid; v < nv; v += 64) seen[v] = 0;
         __builtin_amdgcn_wave_barrier();
         pc.lap(GP_GREEDY);
+        crit_off();
     }
     // BFS augmenting paths, one wave: the queue is consumed in chunks of up
     // to 21 edges, lane 3e+i taking vertex i of the chunk's edge e, which is
@@ -905,6 +929,7 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
     // entries carrying their edge's vertices, read by the appending lane, to
     // save the next chunk a round trip: BFS 7.15e6 -> 8.30e6 cycles, not kept.)
     if (tid < 64) {
+        crit_on();  // (the one wave working: first at its SIMD)
         int16_t *bfs_prev = L.a0, *queue = L.a1;
         uint32_t *first_lane = L.xe;  // (dead after peeling)
         const uint32_t lane = tid;
@@ -1001,6 +1026,7 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
             pc.add(GP_N_BFS_ITERS, niters);
             pc.add(GP_N_FLIP_STEPS, nflip);
         }
+        crit_off();
     }
     __syncthreads();
     pc.lap(GP_BFS);
@@ -1075,6 +1101,7 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
         }
     __syncthreads();
     if (tid == 0 && L.pivot != 0xFFFFFFFFu) {
+        crit_on();
         // follow first dependencies from the first core edge: the walk ends
         // on a cycle, almost surely inside the big component
         int p = (int)L.pivot;
@@ -1086,20 +1113,50 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
         }
         L.pivot = (uint32_t)p;
         fb[p] = 3u;
+        crit_off();
     }
     __syncthreads();
+    pc.lap(GP_TJ_PREP);
     if (L.pivot != 0xFFFFFFFFu) {
+        // a thread's edges and their dependencies stay in registers across the
+        // sweeps, so a sweep is two rounds of independent LDS reads (the
+        // edges' marks, then their dependencies') and fire-and-forget ORs
+        // instead of a chain of dependent reads per edge
+        constexpr uint32_t KPT = (Lds::CMAX + GS_THREADS - 1) / GS_THREADS;
+        int dk[KPT][3];
+#pragma unroll
+        for (uint32_t j = 0; j < KPT; ++j) {
+            const uint32_t k = tid + j * GS_THREADS;
+            const bool core = k < cnt && L.round_of[k] < 0;
+#pragma unroll
+            for (int i = 0; i < 3; ++i) dk[j][i] = core ? (int)L.dep[3 * k + i] : -1;
+        }
         for (;;) {
+            uint32_t fk[KPT], fw[KPT][3];
+#pragma unroll
+            for (uint32_t j = 0; j < KPT; ++j) {
+                const uint32_t k = tid + j * GS_THREADS;
+                fk[j] = k < cnt ? fb[k] : 0u;
+#pragma unroll
+                for (int i = 0; i < 3; ++i) fw[j][i] = dk[j][i] >= 0 ? fb[dk[j][i]] : 0u;
+            }
             int ch = 0;
-            for (uint32_t k = tid; k < cnt; k += GS_THREADS) {
-                if (L.round_of[k] >= 0) continue;
-                const uint32_t fk = fb[k];
+#pragma unroll
+            for (uint32_t j = 0; j < KPT; ++j) {
+                uint32_t nk = fk[j];
+#pragma unroll
                 for (int i = 0; i < 3; ++i) {
-                    const int w = L.dep[3 * k + i];
+                    const int w = dk[j][i];
                     if (w < 0) continue;
-                    const uint32_t fw = fb[w];
-                    if ((fk & 1u) && !(fw & 1u)) { atomicOr(&fb[w], 1u); ch = 1; }                   // F: push
-                    if ((fw & 2u) && !(fk & 2u) && !(fb[k] & 2u)) { atomicOr(&fb[k], 2u); ch = 1; }  // B: pull
+                    if ((fk[j] & 1u) && !(fw[j][i] & 1u)) {  // F: push
+                        atomicOr(&fb[w], 1u);
+                        ch = 1;
+                    }
+                    nk |= fw[j][i] & 2u;  // B: pull
+                }
+                if (nk & ~fk[j] & 2u) {
+                    atomicOr(&fb[tid + j * GS_THREADS], 2u);
+                    ch = 1;
                 }
             }
             pc.add(GP_N_SCC_SWEEPS, 1);
@@ -1110,6 +1167,7 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
         if (ns) atomicAdd(&L.nscc, ns);
         __syncthreads();
     }
+    pc.lap(GP_TJ_SWEEP);
     const bool big = L.nscc >= 64;  // (a small S: plain Tarjan over the whole core)
     if (!big) pc.add(GP_N_SMALL_S, 1);
     // ordered compaction (wave ballots, wave totals by barrier): class 0 =
@@ -1159,7 +1217,9 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
         if (phase == 0) { L.rounds = run0; L.chg = run1; L.nleft = run2; }
     }
     const uint32_t nA = L.rounds, nS = L.chg, nC = L.nleft;
+    pc.lap(GP_TJ_COMPACT);
     if (tid == 0) {
+        crit_on();  // (the one wave working: first at its SIMD)
         int16_t *tidx = L.a0, *tlow = L.a1, *tstk = L.a2, *cstk = L.a3;
         uint8_t *onst = L.b0, *cpos = L.b1;
         int counter = 0, sp = 0, nm = 0, nc = 0;
@@ -1209,6 +1269,7 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
             }
         }
         L.ncomp = (uint32_t)nc;
+        crit_off();
     }
     __syncthreads();
     pc.lap(GP_TARJAN);
@@ -1218,6 +1279,7 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
     uint32_t c = 0;
     while (c < ncomp) {
         if (tid == 0) {
+            crit_on();  // (the one wave working: first at its SIMD)
             // run of singletons
             while (c < ncomp) {
                 const int beg = c ? L.comp_end[c - 1] : 0;
@@ -1240,6 +1302,7 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
                 ++c;
             }
             L.pivot = c;
+            crit_off();
         }
         __syncthreads();
         pc.lap(GP_SINGLE);
@@ -1535,7 +1598,7 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
             uint8_t *used_m = L.b1;
             uint32_t *flags = L.hbin;                         // [w]: wave w has an unused row; [16]: the leader's block end
             uint64_t *slots = pw, *pinfo = pw + NW * SW;      // pinfo[4 cl ..]: pivot panel word, e_c + M[p]
-            uint64_t *Q = pinfo + 4 * 64;                     // Q[(j * W + t) * 2 + q]
+            uint64_t *Q = pinfo + 4 * 64;                     // the pair table of the trailing update
             const uint32_t rr = tid, lane = tid & 63, wv = tid >> 6;
             const bool mine = rr < n;
             bool used = false;
@@ -1577,7 +1640,9 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
                     // published, beside the leader (no barrier between).
                     ++seq;  // (< 0xFFFF: a block takes at least one column)
                     uint32_t ce = cl;
+                    const uint64_t tl0 = pc.now();
                     if (wv == lead) {
+                        crit_on();  // (the one wave working: first at its SIMD)
                         for (; ce < cn; ++ce) {
                             const uint64_t bit = 1ULL << ce;
                             const uint64_t bal = __builtin_amdgcn_ballot_w64(mine && !used && ((r1 | r2) & bit));
@@ -1596,6 +1661,9 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
                             apply(bit, q1, q2, d1, d2, p);
                         }
                         if (lane == 0) __hip_atomic_store(&flags[16], seq << 16 | 0x8000u | ce, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        crit_off();
+                        pc.add_any(GP_GJ_LEAD, pc.now() - tl0);
+                        pc.add_any(GP_GJ_LEADCOLS, ce - cl);
                     } else if (lead < NW) {
                         uint32_t c2 = cl;
                         for (;;) {
@@ -1619,6 +1687,7 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
                                     apply(1ULL << c2, pi[0], pi[1], pi[2], pi[3], 0xFFFFFFFFu);
                                 }
                                 ce = lim;
+                                pc.add_any(GP_GJ_FOLLOW, pc.now() - tl0);
                                 break;
                             }
                             if (GOV_GJ_SLEEP && c2 + FU > lim) __builtin_amdgcn_s_sleep(GOV_GJ_SLEEP);
@@ -1652,6 +1721,7 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
                             }
                         }
                         const uint32_t c = 64 * wc + cl;
+                        pc.add(GP_GJ_SLOTCOLS, 1);
                         if (best == ~0ULL) {  // a free column (uniform): x_c = 0
                             if (tid == 0) piv[c] = -1;
                             ++nfree;
@@ -1667,38 +1737,44 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
                     X(rr, wc, 0) = r1;
                     X(rr, wc, 1) = r2;
                 }
+                const uint64_t tt0 = pc.now();
+                pc.add(GP_GJ_PANELS, 1);
                 if (TW) {
-                    // Q_j: pivot row j's trailing words at the panel's start
-                    // (the rows are updated in place below)
-                    __syncthreads();
-                    for (uint32_t ix = tid; ix < cn * TW; ix += GS_THREADS) {
-                        const uint32_t j = ix / TW, t = ix - j * TW;
-                        const int pr = piv[64 * wc + j];
-                        if (pr >= 0) {
-                            Q[((size_t)j * W + t) * 2] = X((uint32_t)pr, wc + 1 + t, 0);
-                            Q[((size_t)j * W + t) * 2 + 1] = X((uint32_t)pr, wc + 1 + t, 1);
-                        }
-                    }
-                    __syncthreads();
-                    if (mine && (m1 | m2)) {
-                        // row += sum_j M[j] Q_j (the panel's columns 4 at a
-                        // time, every lane the same Q words: broadcast reads)
-                        const uint32_t ncol = 64 - (uint32_t)__builtin_clzll(m1 | m2);
-                        for (uint32_t t = 0; t < TW; ++t) {
-                            uint64_t t1 = X(rr, wc + 1 + t, 0), t2 = X(rr, wc + 1 + t, 1);
-                            constexpr uint32_t BU = GOV_GJ_B2;
-                            for (uint32_t c0 = 0; c0 < ncol; c0 += BU) {
-                                uint64_t a1[BU], a2[BU];
-#pragma unroll
-                                for (uint32_t k = 0; k < BU; ++k) {
-                                    const uint64_t *qj = Q + ((size_t)(c0 + k) * W + t) * 2;
-                                    a1[k] = qj[0];
-                                    a2[k] = qj[1];
+                    // row += sum_j M[j] Q_j, Q_j = pivot row j's trailing words
+                    // at the panel's start, one trailing word at a time by the
+                    // method of four Russians over F3: the panel's columns in
+                    // pairs, T[c][d0 + 3 d1] = d0 Q_2c + d1 Q_2c+1 (9 entries a
+                    // pair, built by the workgroup from the pivot rows, which no
+                    // row has updated in this word yet), then each row adds one
+                    // entry a pair (its two M digits) instead of a conditional
+                    // add a column: a third of the VALU work
+                    for (uint32_t t = 0; t < TW; ++t) {
+                        __syncthreads();  // (the previous word's rows are done with T)
+                        for (uint32_t ix = tid; ix < 32 * 9; ix += GS_THREADS) {
+                            const uint32_t c = ix / 9, d = ix - 9 * c, d0 = d % 3, d1 = d / 3;
+                            uint64_t e1 = 0, e2 = 0;
+                            for (uint32_t h = 0; h < 2; ++h) {
+                                const uint32_t j = 2 * c + h, dj = h ? d1 : d0;
+                                const int pr = (j < cn && dj) ? piv[64 * wc + j] : -1;
+                                if (pr >= 0) {
+                                    const uint64_t q1 = X((uint32_t)pr, wc + 1 + t, 0), q2 = X((uint32_t)pr, wc + 1 + t, 1);
+                                    gf3_add(e1, e2, dj == 1 ? q1 : q2, dj == 1 ? q2 : q1);
                                 }
-#pragma unroll
-                                for (uint32_t k = 0; k < BU; ++k) {
-                                    if ((m1 >> (c0 + k)) & 1u) gf3_add(t1, t2, a1[k], a2[k]);
-                                    if ((m2 >> (c0 + k)) & 1u) gf3_add(t1, t2, a2[k], a1[k]);
+                            }
+                            Q[2 * ix] = e1;
+                            Q[2 * ix + 1] = e2;
+                        }
+                        __syncthreads();
+                        if (mine && (m1 | m2)) {
+                            const uint32_t npair = (65 - (uint32_t)__builtin_clzll(m1 | m2)) >> 1;
+                            uint64_t t1 = X(rr, wc + 1 + t, 0), t2 = X(rr, wc + 1 + t, 1);
+                            for (uint32_t c = 0; c < npair; ++c) {
+                                const uint32_t b1 = (uint32_t)(m1 >> (2 * c)) & 3u, b2 = (uint32_t)(m2 >> (2 * c)) & 3u;
+                                // digits: d = bit of m1 + 2 bit of m2, per column of the pair
+                                const uint32_t idx = (b1 & 1u) + 2 * (b2 & 1u) + 3 * ((b1 >> 1) + 2 * (b2 >> 1));
+                                if (idx) {
+                                    const uint64_t *te = Q + 2 * (9 * c + idx);
+                                    gf3_add(t1, t2, te[0], te[1]);
                                 }
                             }
                             X(rr, wc + 1 + t, 0) = t1;
@@ -1707,6 +1783,7 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
                     }
                 }
                 __syncthreads();
+                pc.add(GP_GJ_TRAIL, pc.now() - tt0);
             }
             if (mine) used_m[rr] = used ? 1 : 0;
             if (tid == 0) L.nfree = nfree;
@@ -1768,9 +1845,6 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
             // member's lvl is final when its last slot is released: the
             // closure costs one returned LDS atomic per dependency.
             uint32_t *roff = L.deg;                                        // reverse CSR offsets
-            // dependents (3 * CMAX int16) in the workgroup's scratch past the
-            // forms (words [28 CMAX, 29.5 CMAX)); pending counts in LDS
-            int16_t *rev = reinterpret_cast<int16_t *>(scr + (size_t)28 * Lds::CMAX);
             uint32_t *pend = L.pend();
             int16_t *queue = L.a3;
             for (uint32_t i = tid; i <= sz; i += GS_THREADS) roff[i] = 0;
@@ -1792,12 +1866,23 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
             }
             __syncthreads();
             wg_excl_scan3(roff, sz + 1, L.xe + Lds::CMAX);
+            // the dependents (int16, roff[sz] of them) in LDS when they fit the
+            // free tails of idep's and indeg's arrays (every block of a random
+            // set but the largest): the closure's chain per dependency is then
+            // an LDS read and a returned LDS atomic, not a global load first;
+            // otherwise in the workgroup's scratch past the forms (words
+            // [28 CMAX, 29.5 CMAX))
+            const uint32_t rev_cap1 = 3 * (Lds::CMAX - sz), nrev = roff[sz];
+            const bool rev_lds = nrev <= rev_cap1 + 2 * (Lds::CMAX - sz);  // (uniform)
+            int16_t *const revA = rev_lds ? L.dep + 3 * sz : reinterpret_cast<int16_t *>(scr + (size_t)28 * Lds::CMAX);
+            int16_t *const revB = reinterpret_cast<int16_t *>(L.claim + sz);
+            auto rev = [&](uint32_t x) -> int16_t & { return (!rev_lds || x < rev_cap1) ? revA[x] : revB[x - rev_cap1]; };
             for (uint32_t d = tid; d < sz; d += GS_THREADS) indeg[d] = roff[d];
             __syncthreads();
             for (uint32_t i = tid; i < sz; i += GS_THREADS)
                 for (int t = 0; t < 3; ++t) {
                     const int d = idep[3 * i + t];
-                    if (d >= 0) rev[atomicAdd(&indeg[d], 1u)] = (int16_t)i;
+                    if (d >= 0) rev(atomicAdd(&indeg[d], 1u)) = (int16_t)i;
                 }
             __syncthreads();
             for (uint32_t d = tid; d < sz; d += GS_THREADS) {
@@ -1813,6 +1898,7 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
             for (;;) {
                 // the ready closure (wave 0)
                 if (tid < 64) {
+                    crit_on();  // (the one wave working: first at its SIMD)
                     uint32_t qt = L.qtail;
                     while (qh < qt) {
                         ++nbatch;
@@ -1842,7 +1928,7 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
                             bool ready = false;
                             uint32_t i = 0;
                             if (act) {
-                                i = (uint32_t)rev[x];
+                                i = (uint32_t)rev(x);
                                 atomicMax(&lvl[i], myl);
                                 ready = atomicSub(&pend[i], 1u) == 1u;  // its last slot
                             }
@@ -1855,6 +1941,7 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
                         __builtin_amdgcn_wave_barrier();
                     }
                     if (lane == 0) L.qtail = qt;
+                    crit_off();
                 }
                 __syncthreads();
                 const uint32_t qt = L.qtail;

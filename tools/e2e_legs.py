@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """The bench's end-to-end legs alone (BSDB_BUILDER_PROFILE=1 prints their
 phases): C4 from host memory through the streaming builder into index.db,
-and C2 from kv.db files.  python tools/e2e_legs.py [--c4] [--kv]"""
+and C2 / C3 from kv.db files.
+python tools/e2e_legs.py [--c4] [--kv] [--parts P] [--kv-n N] [--approx]"""
 import argparse
 import json
 import os
@@ -17,14 +18,18 @@ def main():
     ap.add_argument("--kv", action="store_true")
     ap.add_argument("--n", type=int, default=13_193_787_549)
     ap.add_argument("--reps", type=int, default=1, help="kv leg repetitions in this process")
+    ap.add_argument("--parts", type=int, default=8, help="kv.db partitions (0 = 2 x usable CPUs)")
+    ap.add_argument("--kv-n", type=int, default=100_000_000)
+    ap.add_argument("--approx", action="store_true", help="index.approximate = true (C3)")
     args = ap.parse_args()
     import bench
     from bsdb_amd import Context
     ctx = Context(0)
     out = {}
     for _ in range(args.reps if args.kv else 0):
-        out["e2e_c2_kv_to_disk"] = bench.e2e_c2_kv_to_disk(ctx, 100_000_000, 4)
-        print(json.dumps(out["e2e_c2_kv_to_disk"]), flush=True)
+        parts = args.parts or 2 * bench.usable_cpus()
+        out["e2e_kv_to_disk"] = bench.e2e_kv_to_disk(ctx, args.kv_n, 4, parts, args.approx)
+        print(json.dumps(out["e2e_kv_to_disk"]), flush=True)
     if args.c4:
         out["e2e_c4_host_passes"] = bench.e2e_c4_host_passes(ctx, args.n, 4)
         print(json.dumps(out["e2e_c4_host_passes"]), flush=True)
