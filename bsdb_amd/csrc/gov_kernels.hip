@@ -78,8 +78,10 @@ __host__ __device__ constexpr size_t gj_panel_words(uint32_t n) {
 #ifndef GOV_PICK_REPS
 // FVS: pairs of heavy hinges taken per stuck cascade (with the in x out pick
 // key, C2 at 6 / 8 / 12 / 16 / 20 / 24 / 28: 522 / 536 / 553 / 558 / 566–569 /
-// 565 / 560 M keys/s, profiles/r4/pick_size_ab/, solver_sweep/)
-#define GOV_PICK_REPS 20
+// 565 / 560 M keys/s, profiles/r4/pick_size_ab/, solver_sweep/; round 6, with
+// the four-Russians trailing update: C2 gov 20 / 24 / 28 pairs 122.2 / 121.2 /
+// 123.2 ms, profiles/r6/solver/)
+#define GOV_PICK_REPS 24
 #endif
 constexpr int GS_WMAX = (GS_CMAX + 1 + 63) / 64;  // words per bit-sliced row
 // Oversized buckets (adversarial or skewed key sets: > GS_CMAX keys, 14 sigma
@@ -598,6 +600,15 @@ constexpr size_t solve_scratch_words() {
 }
 static_assert(GS_CMAX != 1664 || 30 * 8 + NB_MAX <= 8 * 2 * GS_WMAX, "FVS null-vector basis fits the dense scratch");
 
+// a workgroup-uniform word read from LDS, as a scalar (the compiler treats
+// LDS reads as per-lane; control flow on them is then exec-mask bookkeeping)
+__device__ __forceinline__ uint32_t uni(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
+
+__device__ __forceinline__ uint64_t readfirstlane64(uint64_t x) {
+    return ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(x >> 32)) << 32) |
+           (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)x);
+}
+
 __device__ __forceinline__ void gf3_add(uint64_t &x1, uint64_t &x2, uint64_t y1, uint64_t y2) {
     const uint64_t a1 = x1, a2 = x2;
     x1 = (a1 & ~y1 & ~y2) | (~a1 & ~a2 & y1) | (a2 & y2);
@@ -716,7 +727,7 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
     }
     __syncthreads();
     pc.lap(GP_EDGES);
-    if (L.flag) {
+    if (uni(L.flag)) {
         pc.add(GP_N_FAIL_DEGEN, 1);
         return false;
     }
@@ -749,7 +760,7 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
             }
         }
         __syncthreads();
-        if (!L.flag) break;
+        if (!uni(L.flag)) break;
         for (uint32_t k = tid; k < cnt; k += GS_THREADS)
             if (L.round_of[k] == r)
                 for (int i = 0; i < 3; ++i) {
@@ -781,7 +792,7 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
             atomicAdd(&L.nscc, cv);
         }
         __syncthreads();
-        const bool over = L.pivot > L.nscc;  // (uniform; both words are next written after the BFS's barrier)
+        const bool over = uni(L.pivot) > uni(L.nscc);  // (uniform; both words are next written after the BFS's barrier)
         if (over) {
             pc.add(GP_N_FAIL_ORIENT, 1);
             return false;
@@ -1030,7 +1041,7 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
     }
     __syncthreads();
     pc.lap(GP_BFS);
-    if (!L.flag) {
+    if (!uni(L.flag)) {
         pc.add(GP_N_FAIL_ORIENT, 1);
         return false;
     }
@@ -1086,13 +1097,17 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
     // (F is finished by then).  SCCs are unique and this is a valid
     // dependency order, and a nonsingular block has one solution, so the
     // values are those of a whole-core Tarjan.
-    uint32_t *fb = L.claim;  // bit 0: in F, bit 1: in B (dead after peeling)
+    // bit 0: in F, bit 1: in B, a word an edge (claim is dead after peeling;
+    // 16 edges packed a word measured slower: the ORs then meet on one word)
+    uint32_t *fbw = L.claim;
+    auto fb = [&](uint32_t k) -> uint32_t { return fbw[k]; };
+    auto fb_or = [&](uint32_t k, uint32_t bits) { atomicOr(&fbw[k], bits); };
     int16_t *roots = reinterpret_cast<int16_t *>(L.xe);  // Tarjan roots: F \ S, then the rest (dead after the BFS)
     if (tid == 0) {
         L.pivot = 0xFFFFFFFFu;
         L.nscc = 0;
     }
-    for (uint32_t k = tid; k < cnt; k += GS_THREADS) fb[k] = 0;
+    for (uint32_t k = tid; k < cnt; k += GS_THREADS) fbw[k] = 0;
     __syncthreads();
     for (uint32_t k = tid; k < cnt; k += GS_THREADS)
         if (L.round_of[k] < 0) {
@@ -1112,7 +1127,7 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
             p = nx;
         }
         L.pivot = (uint32_t)p;
-        fb[p] = 3u;
+        fb_or((uint32_t)p, 3u);
         crit_off();
     }
     __syncthreads();
@@ -1136,9 +1151,9 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
 #pragma unroll
             for (uint32_t j = 0; j < KPT; ++j) {
                 const uint32_t k = tid + j * GS_THREADS;
-                fk[j] = k < cnt ? fb[k] : 0u;
+                fk[j] = k < cnt ? fb(k) : 0u;
 #pragma unroll
-                for (int i = 0; i < 3; ++i) fw[j][i] = dk[j][i] >= 0 ? fb[dk[j][i]] : 0u;
+                for (int i = 0; i < 3; ++i) fw[j][i] = dk[j][i] >= 0 ? fb((uint32_t)dk[j][i]) : 0u;
             }
             int ch = 0;
 #pragma unroll
@@ -1149,13 +1164,13 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
                     const int w = dk[j][i];
                     if (w < 0) continue;
                     if ((fk[j] & 1u) && !(fw[j][i] & 1u)) {  // F: push
-                        atomicOr(&fb[w], 1u);
+                        fb_or((uint32_t)w, 1u);
                         ch = 1;
                     }
                     nk |= fw[j][i] & 2u;  // B: pull
                 }
                 if (nk & ~fk[j] & 2u) {
-                    atomicOr(&fb[tid + j * GS_THREADS], 2u);
+                    fb_or(tid + j * GS_THREADS, 2u);
                     ch = 1;
                 }
             }
@@ -1163,12 +1178,12 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
             if (!__syncthreads_or(ch)) break;
         }
         uint32_t ns = 0;
-        for (uint32_t k = tid; k < cnt; k += GS_THREADS) ns += fb[k] == 3u;
+        for (uint32_t k = tid; k < cnt; k += GS_THREADS) ns += fb(k) == 3u;
         if (ns) atomicAdd(&L.nscc, ns);
         __syncthreads();
     }
     pc.lap(GP_TJ_SWEEP);
-    const bool big = L.nscc >= 64;  // (a small S: plain Tarjan over the whole core)
+    const bool big = uni(L.nscc) >= 64;  // (a small S: plain Tarjan over the whole core)
     if (!big) pc.add(GP_N_SMALL_S, 1);
     // ordered compaction (wave ballots, wave totals by barrier): class 0 =
     // F \ S roots, 1 = S (straight into members[], after the F \ S
@@ -1182,7 +1197,7 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
             const uint32_t k = k0 + tid;
             uint32_t cl = 3;
             if (k < cnt && L.round_of[k] < 0) {
-                const uint32_t f = big ? fb[k] : 0u;
+                const uint32_t f = big ? fb(k) : 0u;
                 cl = f == 1u ? 0u : f == 3u ? 1u : 2u;
             }
             const uint64_t b0 = __builtin_amdgcn_ballot_w64(cl == 0), b1 = __builtin_amdgcn_ballot_w64(cl == 1),
@@ -1216,7 +1231,7 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
         base2 = run0;             // roots: F \ S, then the rest
         if (phase == 0) { L.rounds = run0; L.chg = run1; L.nleft = run2; }
     }
-    const uint32_t nA = L.rounds, nS = L.chg, nC = L.nleft;
+    const uint32_t nA = uni(L.rounds), nS = uni(L.chg), nC = uni(L.nleft);
     pc.lap(GP_TJ_COMPACT);
     if (tid == 0) {
         crit_on();  // (the one wave working: first at its SIMD)
@@ -1275,7 +1290,7 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
     pc.lap(GP_TARJAN);
 
     // ---- 3b. blocks in emission order: singletons on lane 0, blocks with the WG
-    const uint32_t ncomp = L.ncomp;
+    const uint32_t ncomp = uni(L.ncomp);
     uint32_t c = 0;
     while (c < ncomp) {
         if (tid == 0) {
@@ -1306,11 +1321,11 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
         }
         __syncthreads();
         pc.lap(GP_SINGLE);
-        c = L.pivot;
+        c = uni(L.pivot);
         if (c >= ncomp) break;
         // dense block c
-        const uint32_t beg = c ? (uint32_t)L.comp_end[c - 1] : 0;
-        const uint32_t sz = (uint32_t)L.comp_end[c] - beg;
+        const uint32_t beg = c ? uni((uint32_t)L.comp_end[c - 1]) : 0;
+        const uint32_t sz = uni((uint32_t)L.comp_end[c]) - beg;
         // the block's columns in increasing edge order (the order that
         // defines the solution of a singular block, see gauss_jordan): S
         // comes out of the ordered compaction sorted, Tarjan's blocks in stack
@@ -1403,7 +1418,7 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
             }
             __syncthreads();
             for (uint32_t cc = 0; cc < n; ++cc) {
-                const uint32_t p = bid[cc % 3];
+                const uint32_t p = uni(bid[cc % 3]);
                 if (p == 0xFFFFFFFFu) {  // a free column (uniform): x_cc = 0
                     const uint32_t cn = cc + 1, wn = cn >> 6;
                     const uint64_t nbit = 1ULL << (cn & 63);
@@ -1634,6 +1649,10 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
                             lead = w;
                             break;
                         }
+                    // (values read from LDS are per-lane to the compiler; these
+                    // are the same in every lane, and the loops below are then
+                    // scalar loops: no exec-mask bookkeeping per column)
+                    lead = (uint32_t)__builtin_amdgcn_readfirstlane((int)lead);
                     // The leader's progress word: (block sequence << 16) |
                     // columns recorded | 0x8000 once the block has ended.  The
                     // other waves take each recorded column as soon as it is
@@ -1667,7 +1686,8 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
                     } else if (lead < NW) {
                         uint32_t c2 = cl;
                         for (;;) {
-                            const uint32_t v = __hip_atomic_load(&flags[16], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                            const uint32_t v = (uint32_t)__builtin_amdgcn_readfirstlane(
+                                (int)__hip_atomic_load(&flags[16], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
                             const bool mine_seq = (v >> 16) == seq;
                             const uint32_t lim = mine_seq ? (v & 0x7FFFu) : cl;
                             constexpr uint32_t FU = GOV_GJ_FOLLOW;
@@ -1694,7 +1714,7 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
                         }
                     }
                     // (every wave has ce; uniform)
-                    cl = ce;
+                    cl = (uint32_t)__builtin_amdgcn_readfirstlane((int)ce);
                     if (cl < cn) {
                         // column cl: no candidate in the leader -- every
                         // wave's lowest candidate (or a free column)
@@ -1720,6 +1740,8 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
                                 bw = w;
                             }
                         }
+                        best = readfirstlane64(best);
+                        bw = (uint32_t)__builtin_amdgcn_readfirstlane((int)bw);
                         const uint32_t c = 64 * wc + cl;
                         pc.add(GP_GJ_SLOTCOLS, 1);
                         if (best == ~0ULL) {  // a free column (uniform): x_c = 0
@@ -1766,16 +1788,24 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
                         }
                         __syncthreads();
                         if (mine && (m1 | m2)) {
+                            // four pairs a step, their entries loaded together and
+                            // added unconditionally (entry 0 of a pair is zero)
                             const uint32_t npair = (65 - (uint32_t)__builtin_clzll(m1 | m2)) >> 1;
                             uint64_t t1 = X(rr, wc + 1 + t, 0), t2 = X(rr, wc + 1 + t, 1);
-                            for (uint32_t c = 0; c < npair; ++c) {
-                                const uint32_t b1 = (uint32_t)(m1 >> (2 * c)) & 3u, b2 = (uint32_t)(m2 >> (2 * c)) & 3u;
-                                // digits: d = bit of m1 + 2 bit of m2, per column of the pair
-                                const uint32_t idx = (b1 & 1u) + 2 * (b2 & 1u) + 3 * ((b1 >> 1) + 2 * (b2 >> 1));
-                                if (idx) {
+                            for (uint32_t c0 = 0; c0 < npair; c0 += 4) {
+                                uint64_t e1[4], e2[4];
+#pragma unroll
+                                for (uint32_t u = 0; u < 4; ++u) {
+                                    const uint32_t c = c0 + u;  // (c < 32: pairs past npair read their zero entry)
+                                    const uint32_t b1 = (uint32_t)(m1 >> (2 * c)) & 3u, b2 = (uint32_t)(m2 >> (2 * c)) & 3u;
+                                    // digits: d = bit of m1 + 2 bit of m2, per column of the pair
+                                    const uint32_t idx = (b1 & 1u) + 2 * (b2 & 1u) + 3 * ((b1 >> 1) + 2 * (b2 >> 1));
                                     const uint64_t *te = Q + 2 * (9 * c + idx);
-                                    gf3_add(t1, t2, te[0], te[1]);
+                                    e1[u] = te[0];
+                                    e2[u] = te[1];
                                 }
+#pragma unroll
+                                for (uint32_t u = 0; u < 4; ++u) gf3_add(t1, t2, e1[u], e2[u]);
                             }
                             X(rr, wc + 1 + t, 0) = t1;
                             X(rr, wc + 1 + t, 1) = t2;
@@ -1872,7 +1902,7 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
             // an LDS read and a returned LDS atomic, not a global load first;
             // otherwise in the workgroup's scratch past the forms (words
             // [28 CMAX, 29.5 CMAX))
-            const uint32_t rev_cap1 = 3 * (Lds::CMAX - sz), nrev = roff[sz];
+            const uint32_t rev_cap1 = 3 * (Lds::CMAX - sz), nrev = uni(roff[sz]);
             const bool rev_lds = nrev <= rev_cap1 + 2 * (Lds::CMAX - sz);  // (uniform)
             int16_t *const revA = rev_lds ? L.dep + 3 * sz : reinterpret_cast<int16_t *>(scr + (size_t)28 * Lds::CMAX);
             int16_t *const revB = reinterpret_cast<int16_t *>(L.claim + sz);
@@ -1899,7 +1929,7 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
                 // the ready closure (wave 0)
                 if (tid < 64) {
                     crit_on();  // (the one wave working: first at its SIMD)
-                    uint32_t qt = L.qtail;
+                    uint32_t qt = uni(L.qtail);
                     while (qh < qt) {
                         ++nbatch;
                         const uint32_t nb = min(64u, qt - qh);
@@ -1944,7 +1974,7 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
                     crit_off();
                 }
                 __syncthreads();
-                const uint32_t qt = L.qtail;
+                const uint32_t qt = uni(L.qtail);
                 if (qt >= sz) break;  // every member placed (each enters the queue once)
                 // a pick adds up to 2 heavy hinges: the heavy set stays
                 // <= fvs_max, so forms and heavy rows (constant column at nH)
@@ -2035,8 +2065,8 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
                             const uint32_t pos = my_sb + __builtin_amdgcn_mbcnt_hi((uint32_t)(sm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)sm, 0u));
                             make_heavy(i, nh + pos, qt + pos);
                         }
-                        run_eq = eb;
-                        got = sb;
+                        run_eq = uni(eb);
+                        got = uni(sb);
                     }
                     nh += got;
                     if (tid == 0) L.qtail = qt + got;
@@ -2084,7 +2114,7 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
                     }
                 }
                 __syncthreads();
-                if (T >= 63 || pick_exact) nh = L.nleft;  // (the exact rounds ran)
+                if (T >= 63 || pick_exact) nh = uni(L.nleft);  // (the exact rounds ran)
                 if (pc.on()) pick_cyc += clock64() - tpk;
             }
             // st and the levels; the highest level
@@ -2107,8 +2137,8 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
                 pc.add(GP_SEL_PICK_CYCLES, pick_cyc);
             }
             __syncthreads();
-            const uint32_t nH = L.nleft, r = L.rounds;
-            const bool fall_back = L.chg != 0;
+            const uint32_t nH = uni(L.nleft), r = uni(L.rounds);
+            const bool fall_back = uni(L.chg) != 0;
             pc.lap(GP_FVS_SEL);
             pc.add(GP_N_FVS_BLOCKS, 1);
             pc.add(GP_N_FORM_LEVELS, r);
@@ -2194,11 +2224,13 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
                 // FW-word form spilled part of them to scratch at the
                 // kernel's 128-VGPR limit: a scratch round trip per member)
                 // (wave 0 alone with a wave fence per level instead of the
-                // workgroup barrier: forms 4.13e6 -> 4.59e6 cycles, not kept)
+                // workgroup barrier: forms 4.13e6 -> 4.59e6 cycles, not kept;
+                // the next level's members read from LDS during this level's
+                // loads: forms 4.11e6 -> 4.39e6, more spills, not kept)
                 auto form_levels = [&](auto hw) {
                     constexpr uint32_t H = decltype(hw)::value;
                     for (uint32_t R = 0; R < r; ++R) {
-                        const uint32_t o0 = roff[R], nR = roff[R + 1] - o0;
+                        const uint32_t o0 = uni(roff[R]), nR = uni(roff[R + 1]) - o0;
                         if (nR == 0) continue;  // (uniform)
                         for (uint32_t t = tid; t < nR; t += GS_THREADS) {
                             const uint32_t i = (uint32_t)rlist[o0 + t];
@@ -2309,7 +2341,7 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
                     pc.add(GP_N_FAIL_INCONS, 1);
                     return false;
                 }
-                const uint32_t nfree = L.nfree;
+                const uint32_t nfree = uni(L.nfree);
                 // evaluate: x_i = forms . (x_heavy, 1)
                 uint64_t *X1 = L.prow, *X2 = L.prow + 8;
                 for (uint32_t w = tid; w < 16; w += GS_THREADS) L.prow[w] = 0;
@@ -2398,7 +2430,7 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
                             if (u) atomicMax(&L.npos, i + 1);
                         }
                         __syncthreads();
-                        const uint32_t pnew = L.npos - 1;  // (T z is independent of the basis: npos > 0)
+                        const uint32_t pnew = uni(L.npos) - 1;  // (T z is independent of the basis: npos > 0)
                         const uint32_t sc = NBV(nb, pnew);  // 1 or 2 = its own inverse
                         for (uint32_t l = tid; l < nb; l += GS_THREADS) coef[l] = NBV(l, pnew);
                         __syncthreads();
@@ -2464,7 +2496,7 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
         if (sz > 440) pc.add(GP_N_BIG_ROWS, sz);
         ++c;
     }
-    if (!L.flag) return false;
+    if (!uni(L.flag)) return false;
 
     // ---- 4. peeled edges, last round first
     for (int rr = rounds - 1; rr >= 0; --rr) {
@@ -2646,14 +2678,15 @@ __global__ __launch_bounds__(GS_THREADS, GS_THREADS * GS_PER_CU / 256) void k_go
             sh_win = lb != cur;  // (a speculative attempt)
         }
         __syncthreads();
-        const uint32_t lb = sh_lb, sd = sh_s;
+        const uint32_t lb = uni(sh_lb), sd = uni(sh_s);
         if (lb == 0xFFFFFFFFu) break;
         if (a.spec & 0x100u) {
             if (sh_win) __builtin_amdgcn_s_setprio(0);
             else __builtin_amdgcn_s_setprio(2);
         }
         const uint64_t b = a.b0 + lb;
-        const uint64_t lo = a.E[b] & OFFSET_MASK, hi = a.E[b + 1] & OFFSET_MASK;
+        // (the bucket's bounds as scalars: every phase's loops are bounded by them)
+        const uint64_t lo = readfirstlane64(a.E[b] & OFFSET_MASK), hi = readfirstlane64(a.E[b + 1] & OFFSET_MASK);
         const uint32_t cnt = (uint32_t)(hi - lo);
         const uint32_t nv = (uint32_t)(vertex_offset(hi) - vertex_offset(lo));
         if (cnt == 0) {  // nothing to solve: seed 0, no values
