@@ -75,6 +75,9 @@ constexpr int GS_TINY = 12;      // brute-force buckets (only in sets of < ~1500
 __host__ __device__ constexpr size_t gj_panel_words(uint32_t n) {
     return (size_t)(GOV_THREADS / 64) * 5 + (size_t)4 * 64 + (size_t)2 * 32 * 9;  // slots, pinfo, the pair table
 }
+#ifndef GOV_GREEDY_CHUNK
+#define GOV_GREEDY_CHUNK 64  // core edges the greedy orientation takes a step (wave 0)
+#endif
 #ifndef GOV_PICK_REPS
 // FVS: pairs of heavy hinges taken per stuck cascade (with the in x out pick
 // key, C2 at 6 / 8 / 12 / 16 / 20 / 24 / 28: 522 / 536 / 553 / 558 / 566–569 /
@@ -707,7 +710,6 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
     }
     for (uint32_t v = tid; v < nv; v += GS_THREADS) {
         L.deg[v] = 0;
-        L.xe[v] = 0;
         L.vowner[v] = -1;
         L.xval[v] = 0;
     }
@@ -720,7 +722,6 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
         for (int i = 0; i < 3; ++i) {
             L.e[3 * k + i] = (uint16_t)e[i];
             atomicAdd(&L.deg[e[i]], 1u);
-            atomicXor(&L.xe[e[i]], k);
         }
         L.hinge[k] = -1;
         L.round_of[k] = -1;
@@ -741,33 +742,68 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
         return true;
     }
 
-    // ---- 1. peeling in rounds
+    // ---- 1. peeling in rounds, from the edge side: an unpeeled edge with a
+    // vertex of degree 1 is peeled in this round, its hinge the smallest such
+    // vertex -- the edge every degree-1 vertex claims (its only remaining
+    // one), the smallest claimant winning.  Two barriers a round (claims by
+    // vertex took four), and the LDS solver's edges stay in registers.
     int r = 0;
-    for (;; ++r) {
-        for (uint32_t k = tid; k < cnt; k += GS_THREADS) L.claim[k] = 0xFFFFFFFFu;
-        if (tid == 0) L.flag = 0;
-        __syncthreads();
-        for (uint32_t v = tid; v < nv; v += GS_THREADS)
-            if (L.deg[v] == 1) atomicMin(&L.claim[L.xe[v]], v);
-        __syncthreads();
-        for (uint32_t k = tid; k < cnt; k += GS_THREADS) {
-            const uint32_t c = L.claim[k];
-            if (c != 0xFFFFFFFFu) {
-                L.hinge[k] = (int16_t)c;
-                L.vowner[c] = (int16_t)k;
-                L.round_of[k] = (int16_t)r;
-                L.flag = 1;
+    {
+        constexpr uint32_t KPT = (Lds::CMAX + GS_THREADS - 1) / GS_THREADS;
+        constexpr bool REG = KPT <= 4;  // (the global-slab instance reads its edges each round)
+        constexpr uint32_t KR = REG ? KPT : 1;
+        uint32_t pe[KR][3];
+        uint32_t live = 0;  // (REG) bit j: edge tid + j * GS_THREADS not peeled
+        if constexpr (REG) {
+#pragma unroll
+            for (uint32_t j = 0; j < KR; ++j) {
+                const uint32_t k = tid + j * GS_THREADS;
+                pe[j][0] = pe[j][1] = pe[j][2] = 0;
+                if (k < cnt) {
+                    live |= 1u << j;
+                    pe[j][0] = L.e[3 * k];
+                    pe[j][1] = L.e[3 * k + 1];
+                    pe[j][2] = L.e[3 * k + 2];
+                }
             }
         }
-        __syncthreads();
-        if (!uni(L.flag)) break;
-        for (uint32_t k = tid; k < cnt; k += GS_THREADS)
-            if (L.round_of[k] == r)
-                for (int i = 0; i < 3; ++i) {
-                    atomicSub(&L.deg[L.e[3 * k + i]], 1u);
-                    atomicXor(&L.xe[L.e[3 * k + i]], k);
-                }
-        __syncthreads();
+        auto try_peel = [&](uint32_t k, uint32_t v0, uint32_t v1, uint32_t v2) -> bool {
+            const uint32_t d0 = L.deg[v0], d1 = L.deg[v1], d2 = L.deg[v2];
+            uint32_t h = 0xFFFFFFFFu;
+            if (d0 == 1u) h = v0;
+            if (d1 == 1u) h = min(h, v1);
+            if (d2 == 1u) h = min(h, v2);
+            if (h == 0xFFFFFFFFu) return false;
+            L.hinge[k] = (int16_t)h;
+            L.vowner[h] = (int16_t)k;
+            L.round_of[k] = (int16_t)r;
+            return true;
+        };
+        for (;; ++r) {
+            uint32_t newp = 0;
+            if constexpr (REG) {
+#pragma unroll
+                for (uint32_t j = 0; j < KR; ++j)
+                    if (((live >> j) & 1u) && try_peel(tid + j * GS_THREADS, pe[j][0], pe[j][1], pe[j][2]))
+                        newp |= 1u << j;
+                live &= ~newp;
+            } else {
+                for (uint32_t k = tid; k < cnt; k += GS_THREADS)
+                    if (L.round_of[k] < 0 && try_peel(k, L.e[3 * k], L.e[3 * k + 1], L.e[3 * k + 2])) newp = 1;
+            }
+            if (!__syncthreads_or(newp != 0)) break;
+            if constexpr (REG) {
+#pragma unroll
+                for (uint32_t j = 0; j < KR; ++j)
+                    if ((newp >> j) & 1u)
+                        for (int i = 0; i < 3; ++i) atomicSub(&L.deg[pe[j][i]], 1u);
+            } else {
+                for (uint32_t k = tid; k < cnt; k += GS_THREADS)
+                    if (L.round_of[k] == r)
+                        for (int i = 0; i < 3; ++i) atomicSub(&L.deg[L.e[3 * k + i]], 1u);
+            }
+            __syncthreads();
+        }
     }
     const int rounds = r;
     pc.lap(GP_PEEL);
@@ -852,12 +888,17 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
         };
         bool nact;
         uint32_t n0, n1, n2;
-        chunk_edges(tid, nact, n0, n1, n2);
-        for (uint32_t k0 = 0; k0 < cnt; k0 += 64) {
+        // GOV_GREEDY_CHUNK edges a step (lanes above it idle): fewer lanes
+        // whose vertices an earlier lane of the step touches, each of which
+        // costs a serial step below
+        constexpr uint32_t GCH = GOV_GREEDY_CHUNK;
+        static_assert(GCH >= 1 && GCH <= 64, "greedy chunk");
+        chunk_edges(tid < GCH ? tid : cnt, nact, n0, n1, n2);
+        for (uint32_t k0 = 0; k0 < cnt; k0 += GCH) {
             const uint32_t k = k0 + tid;
             const bool act = nact;
             uint32_t v0 = n0, v1 = n1, v2 = n2, c0 = 0, c1 = 0, c2 = 0;
-            chunk_edges(k + 64, nact, n0, n1, n2);
+            chunk_edges(tid < GCH ? k + GCH : cnt, nact, n0, n1, n2);
             bool f0 = false, f1 = false, f2 = false;
             const uint32_t me = lane_tag | tid;
             lane_tag -= 64;
@@ -987,6 +1028,8 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
                     atomicMin(&first_lane[v], me);
                 }
                 __builtin_amdgcn_wave_barrier();
+                // (the root's iteration without the queue read and the
+                // atomics, duplicates compared in registers: BFS +2 %, not kept)
                 const bool valid = act && first_lane[v] == me && sn != epoch;
                 const uint64_t fb = __builtin_amdgcn_ballot_w64(valid && o < 0);
                 const uint32_t F = fb ? (uint32_t)__builtin_ctzll(fb) : 64u;
@@ -1246,41 +1289,63 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
             if (ri == nA + nC) break;
             const uint32_t r0 = (uint32_t)roots[ri];
             if (tidx[r0] >= 0) continue;
-            int csp = 0;
-            cstk[csp] = (int16_t)r0;
-            cpos[csp] = 0;
-            ++csp;
-            tidx[r0] = tlow[r0] = (int16_t)counter++;
-            tstk[sp++] = (int16_t)r0;
-            onst[r0] = 1;
-            while (csp) {
-                const int k = cstk[csp - 1];
-                if (cpos[csp - 1] < 3) {
-                    const int w = L.dep[3 * k + cpos[csp - 1]];
-                    ++cpos[csp - 1];
+            // the top frame lives in registers (its edge, next dependency
+            // slot, low link, index and dependencies); the frames below it in
+            // cstk / cpos / tlow.  The same walk, in the same order, as one
+            // with every frame in LDS, with a third of the dependent LDS round
+            // trips per step.
+            int csp = 0, k = (int)r0, pos = 0, tk = counter++, lowk = tk;
+            int d0 = L.dep[3 * k], d1 = L.dep[3 * k + 1], d2 = L.dep[3 * k + 2];
+            tidx[k] = (int16_t)tk;
+            tstk[sp++] = (int16_t)k;
+            onst[k] = 1;
+            for (;;) {
+                if (pos < 3) {
+                    const int w = pos == 0 ? d0 : pos == 1 ? d1 : d2;
+                    ++pos;
                     if (w < 0) continue;
-                    if (tidx[w] < 0) {
-                        tidx[w] = tlow[w] = (int16_t)counter++;
-                        tstk[sp++] = (int16_t)w;
-                        onst[w] = 1;
-                        cstk[csp] = (int16_t)w;
-                        cpos[csp] = 0;
+                    const int tw = tidx[w];
+                    const bool on = onst[w] != 0;
+                    if (tw < 0) {  // descend: the current frame goes to the stack
+                        cstk[csp] = (int16_t)k;
+                        cpos[csp] = (uint8_t)pos;
+                        tlow[k] = (int16_t)lowk;
                         ++csp;
-                    } else if (onst[w] && tidx[w] < tlow[k]) {
-                        tlow[k] = tidx[w];
+                        k = w;
+                        pos = 0;
+                        tk = lowk = counter++;
+                        d0 = L.dep[3 * k];
+                        d1 = L.dep[3 * k + 1];
+                        d2 = L.dep[3 * k + 2];
+                        tidx[k] = (int16_t)tk;
+                        tstk[sp++] = (int16_t)k;
+                        onst[k] = 1;
+                    } else if (on && tw < lowk) {
+                        lowk = tw;
                     }
                     continue;
                 }
-                --csp;
-                if (csp && tlow[k] < tlow[cstk[csp - 1]]) tlow[cstk[csp - 1]] = tlow[k];
-                if (tlow[k] != tidx[k]) continue;
-                for (;;) {
-                    const int w = tstk[--sp];
-                    onst[w] = 0;
-                    L.members[nm++] = (int16_t)w;
-                    if (w == k) break;
+                if (lowk == tk) {  // k roots a component
+                    for (;;) {
+                        const int w = tstk[--sp];
+                        onst[w] = 0;
+                        L.members[nm++] = (int16_t)w;
+                        if (w == k) break;
+                    }
+                    L.comp_end[nc++] = (int16_t)nm;
                 }
-                L.comp_end[nc++] = (int16_t)nm;
+                if (csp == 0) break;
+                // back to the parent frame, its low link taking the child's
+                const int lowc = lowk;
+                --csp;
+                k = cstk[csp];
+                pos = cpos[csp];
+                lowk = tlow[k];
+                tk = tidx[k];
+                d0 = L.dep[3 * k];
+                d1 = L.dep[3 * k + 1];
+                d2 = L.dep[3 * k + 2];
+                if (lowc < lowk) lowk = lowc;
             }
         }
         L.ncomp = (uint32_t)nc;
