@@ -340,7 +340,7 @@ def usable_cpus() -> int:
     return max(1, n)
 
 
-def e2e_kv_to_disk(ctx, n: int, width: int, partitions: int = 8, approximate: bool = False):
+def e2e_kv_to_disk(ctx, n: int, width: int, partitions: int = 8, approximate: bool = False, threads: int = 0):
     """BASELINE C2 / C3 from the DATA FILES: n records of 13-byte keys and
     32-byte values in SimpleCompactKVWriter's layout (48-byte records,
     kv.db.<p>, written before the clock) -> bsdb_kv_build_index (host threads
@@ -377,7 +377,7 @@ def e2e_kv_to_disk(ctx, n: int, width: int, partitions: int = 8, approximate: bo
         torch.cuda.empty_cache()
         ip, ap = os.path.join(tmp, "index.db"), os.path.join(tmp, "index_a.db")
         t0 = _t.perf_counter()
-        mph = ctx.kv_build_index(base, partitions, width, ip, ap, approximate=approximate)
+        mph = ctx.kv_build_index(base, partitions, width, ip, ap, approximate=approximate, threads=threads)
         mph.dump(os.path.join(tmp, "hash.dump"))
         dt = _t.perf_counter() - t0
         size, asize = os.path.getsize(ip), os.path.getsize(ap)

@@ -1691,6 +1691,9 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
             for (uint32_t wc = 0; 64 * wc < n; ++wc) {
                 const uint32_t TW = W - wc - 1, cn = min(64u, n - 64 * wc);
                 uint64_t r1 = mine ? X(rr, wc, 0) : 0, r2 = mine ? X(rr, wc, 1) : 0, m1 = 0, m2 = 0;
+                // (the multipliers' high half untouched below column 32 and the
+                // rows' low half from column 32 on without a free column,
+                // skipped by uniform branches: leader +12 % cycles, not kept)
                 auto apply = [&](uint64_t bit, uint64_t q1, uint64_t q2, uint64_t d1, uint64_t d2, uint32_t p) {
                     if (rr == p) {
                         used = true;
@@ -1740,6 +1743,7 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
                                 pinfo[4 * ce + 2] = d1;
                                 pinfo[4 * ce + 3] = d2;
                                 piv[64 * wc + ce] = (int16_t)p;
+                                // (publishing every 2 or 4 columns: no change, not kept)
                                 __hip_atomic_store(&flags[16], seq << 16 | (ce + 1), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
                             }
                             apply(bit, q1, q2, d1, d2, p);
@@ -2017,6 +2021,8 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
                         // heavy set do not depend on the queue order).  (Up
                         // to 4 per lane per step, issued together: slower,
                         // 7.3e6 -> 8.4e6 selection cycles.)
+                        // (the next dependent read beside a step's atomics:
+                        // no change, C2 gov 114.5 vs 114.5 ms, not kept)
                         for (uint32_t x = x0;; ++x) {
                             const bool act = x < x1;
                             if (__builtin_amdgcn_ballot_w64(act) == 0) break;
@@ -2292,35 +2298,32 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
                 // workgroup barrier: forms 4.13e6 -> 4.59e6 cycles, not kept;
                 // the next level's members read from LDS during this level's
                 // loads: forms 4.11e6 -> 4.39e6, more spills, not kept)
+                // A word of a form per thread (H threads a member, adjacent
+                // lanes on adjacent words: the dependencies' forms read as
+                // consecutive 16-byte pairs); a level's VALU spreads over H
+                // times the lanes of the member-per-thread form, whose one
+                // wave carried a typical level's ~20 members alone.
                 auto form_levels = [&](auto hw) {
                     constexpr uint32_t H = decltype(hw)::value;
                     for (uint32_t R = 0; R < r; ++R) {
                         const uint32_t o0 = uni(roff[R]), nR = uni(roff[R + 1]) - o0;
                         if (nR == 0) continue;  // (uniform)
-                        for (uint32_t t = tid; t < nR; t += GS_THREADS) {
-                            const uint32_t i = (uint32_t)rlist[o0 + t];
+                        for (uint32_t t = tid; t < nR * H; t += GS_THREADS) {
+                            const uint32_t mi = t / H, w = t - mi * H;
+                            const uint32_t i = (uint32_t)rlist[o0 + mi];
                             const int d0 = idep[3 * i], d1 = idep[3 * i + 1], d2 = idep[3 * i + 2];
                             const uint32_t info = (uint32_t)rinfo[i];
-                            uint64_t a1[H], a2[H];
-#pragma unroll
-                            for (uint32_t w = 0; w < H; ++w) {
-                                a1[w] = a2[w] = 0;
-                                if (d0 >= 0) gf3_add(a1[w], a2[w], V(d0, w, 0), V(d0, w, 1));
-                                if (d1 >= 0) gf3_add(a1[w], a2[w], V(d1, w, 0), V(d1, w, 1));
-                                if (d2 >= 0) gf3_add(a1[w], a2[w], V(d2, w, 0), V(d2, w, 1));
-                            }
+                            uint64_t a1 = 0, a2 = 0;
+                            if (d0 >= 0) gf3_add(a1, a2, V(d0, w, 0), V(d0, w, 1));
+                            if (d1 >= 0) gf3_add(a1, a2, V(d1, w, 0), V(d1, w, 1));
+                            if (d2 >= 0) gf3_add(a1, a2, V(d2, w, 0), V(d2, w, 1));
                             // x = cf * (h - sum): -sum has the planes swapped;
                             // add h - cst in the constant column of (a2, a1)
                             const uint32_t kk = info & 3u;
-#pragma unroll
-                            for (uint32_t w = 0; w < H; ++w)
-                                if (w == cw) gf3_add(a2[w], a1[w], kk == 1 ? cbit : 0, kk == 2 ? cbit : 0);
-#pragma unroll
-                            for (uint32_t w = 0; w < H; ++w) {
-                                // times cf = 2 swaps the planes back
-                                V(i, w, 0) = (info & 4u) ? a1[w] : a2[w];
-                                V(i, w, 1) = (info & 4u) ? a2[w] : a1[w];
-                            }
+                            if (w == cw) gf3_add(a2, a1, kk == 1 ? cbit : 0, kk == 2 ? cbit : 0);
+                            // times cf = 2 swaps the planes back
+                            V(i, w, 0) = (info & 4u) ? a1 : a2;
+                            V(i, w, 1) = (info & 4u) ? a2 : a1;
                         }
                         __syncthreads();
                     }

@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--parts", type=int, default=8, help="kv.db partitions (0 = 2 x usable CPUs)")
     ap.add_argument("--kv-n", type=int, default=100_000_000)
     ap.add_argument("--approx", action="store_true", help="index.approximate = true (C3)")
+    ap.add_argument("--threads", type=int, default=0, help="kv scan threads (0 = the library's default)")
     args = ap.parse_args()
     import bench
     from bsdb_amd import Context
@@ -28,7 +29,7 @@ def main():
     out = {}
     for _ in range(args.reps if args.kv else 0):
         parts = args.parts or 2 * bench.usable_cpus()
-        out["e2e_kv_to_disk"] = bench.e2e_kv_to_disk(ctx, args.kv_n, 4, parts, args.approx)
+        out["e2e_kv_to_disk"] = bench.e2e_kv_to_disk(ctx, args.kv_n, 4, parts, args.approx, args.threads)
         print(json.dumps(out["e2e_kv_to_disk"]), flush=True)
     if args.c4:
         out["e2e_c4_host_passes"] = bench.e2e_c4_host_passes(ctx, args.n, 4)
