@@ -2228,34 +2228,6 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
                             V(i, w, 1) = 0;
                         }
                 __syncthreads();
-                // sum over the non-hinge vertices of member k: in-block ones as
-                // forms, the rest as known values (into the constant column)
-                // (register arrays indexed by unrolled constants only: a
-                // runtime index would put them in scratch)
-                auto accumulate = [&](uint32_t k, uint64_t (&a1)[FW], uint64_t (&a2)[FW], uint32_t &cst) {
-#pragma unroll
-                    for (uint32_t w = 0; w < FW; ++w) a1[w] = a2[w] = 0;
-                    cst = 0;
-                    for (int t = 0; t < 3; ++t) {
-                        const uint32_t v = L.e[3 * k + t];
-                        if (v == (uint32_t)L.hinge[k]) continue;
-                        const int o = L.vowner[v];
-                        if (o >= 0 && L.col_of[o] >= 0) {
-                            const uint32_t j = (uint32_t)L.col_of[o];
-#pragma unroll
-                            for (uint32_t w = 0; w < FW; ++w)
-                                if (w < HW) gf3_add(a1[w], a2[w], V(j, w, 0), V(j, w, 1));
-                        } else {
-                            cst += L.xval[v];
-                        }
-                    }
-                };
-                // word w's share of k * e_col (k in {0, 1, 2}) into planes
-                auto add_unit = [&](uint64_t (&a1)[FW], uint64_t (&a2)[FW], uint32_t col, uint32_t kk) {
-#pragma unroll
-                    for (uint32_t w = 0; w < FW; ++w)
-                        if (w == (col >> 6)) gf3_add(a1[w], a2[w], kk == 1 ? 1ULL << (col & 63) : 0, kk == 2 ? 1ULL << (col & 63) : 0);
-                };
                 auto hinge_pos = [&](uint32_t k, uint32_t &h, uint32_t &cf) {
                     h = 0;
                     while (L.e[3 * k + h] != (uint32_t)L.hinge[k]) ++h;
@@ -2350,36 +2322,44 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
                                    hs_lds && (size_t)2 * HW * nH + pscr <= Lds::HS_WORDS;
                 uint64_t *const hsb = L.hs();
                 auto HSL = [&](uint32_t rr, uint32_t w, uint32_t q) -> uint64_t & { return hsb[(2 * w + q) * nH + rr]; };
-                for (uint32_t i = tid; i < sz; i += GS_THREADS) {
+                // a word of a heavy row per thread (as the forms)
+                for (uint32_t t = tid; t < sz * HW; t += GS_THREADS) {
+                    const uint32_t i = t / HW, w = t - i * HW;
                     if (st[i] != 2) continue;
                     const uint32_t k = (uint32_t)L.members[beg + i], j = (uint32_t)hid[i];
-                    uint64_t a1[FW], a2[FW];
-                    uint32_t cst, h, cf;
-                    accumulate(k, a1, a2, cst);
+                    uint64_t a1 = 0, a2 = 0;
+                    uint32_t cst = 0, h, cf;
+                    // the member's other vertices: in-block ones as forms, the
+                    // rest as known values
+                    for (int t3 = 0; t3 < 3; ++t3) {
+                        const uint32_t v = L.e[3 * k + t3];
+                        if (v == (uint32_t)L.hinge[k]) continue;
+                        const int o = L.vowner[v];
+                        if (o >= 0 && L.col_of[o] >= 0) {
+                            const uint32_t d = (uint32_t)L.col_of[o];
+                            gf3_add(a1, a2, V(d, w, 0), V(d, w, 1));
+                        } else {
+                            cst += L.xval[v];
+                        }
+                    }
                     hinge_pos(k, h, cf);
-                    add_unit(a1, a2, j, cf);
-                    // the forms' constant column moves to the right-hand side:
-                    // rhs = h - cst - const
-                    uint32_t cform = 0;
-#pragma unroll
-                    for (uint32_t w = 0; w < FW; ++w)
-                        if (w == cw) {
-                            cform = (a1[w] & cbit) ? 1 : (a2[w] & cbit) ? 2 : 0;
-                            a1[w] &= ~cbit;
-                            a2[w] &= ~cbit;
-                        }
-                    add_unit(a1, a2, nH, (h + 3 * 64 - cst - cform) % 3);
-#pragma unroll
-                    for (uint32_t w = 0; w < FW; ++w)
-                        if (w < HW) {
-                            if (hs_lds) {
-                                HSL(j, w, 0) = a1[w];
-                                HSL(j, w, 1) = a2[w];
-                            } else {
-                                X(j, w, 0) = a1[w];
-                                X(j, w, 1) = a2[w];
-                            }
-                        }
+                    if (w == (j >> 6)) gf3_add(a1, a2, cf == 1 ? 1ULL << (j & 63) : 0, cf == 2 ? 1ULL << (j & 63) : 0);
+                    if (w == cw) {
+                        // the forms' constant column moves to the right-hand
+                        // side: rhs = h - cst - const
+                        const uint32_t cform = (a1 & cbit) ? 1 : (a2 & cbit) ? 2 : 0;
+                        a1 &= ~cbit;
+                        a2 &= ~cbit;
+                        const uint32_t rhs = (h + 3 * 64 - cst - cform) % 3;
+                        gf3_add(a1, a2, rhs == 1 ? cbit : 0, rhs == 2 ? cbit : 0);
+                    }
+                    if (hs_lds) {
+                        HSL(j, w, 0) = a1;
+                        HSL(j, w, 1) = a2;
+                    } else {
+                        X(j, w, 0) = a1;
+                        X(j, w, 1) = a2;
+                    }
                 }
                 __syncthreads();
                 // (rows in X: words < 12 CMAX, below the forms)
@@ -2628,20 +2608,37 @@ __device__ __forceinline__ void store_bucket(Lds &L, const SolveArgs &a, uint64_
     const uint32_t nv = (uint32_t)(vertex_offset(hi) - vo);
     const ulonglong2 *sig = reinterpret_cast<const ulonglong2 *>(a.sig) + (lo - a.e0);
     // values: hinge -> xval or 3, other vertices 0; words shared with the
-    // neighbouring buckets are OR-ed
+    // neighbouring buckets are OR-ed.  A vertex per lane: a wave's two 32-lane
+    // halves are two aligned value words, packed from the lanes' two bit
+    // planes (ballots) by lanes 0 and 32
     const uint64_t w0 = vo >> 5, w1 = (vo + nv + 31) >> 5;
-    for (uint64_t w = w0 + threadIdx.x; w < w1; w += GS_THREADS) {
-        uint64_t word = 0;
-        for (uint32_t t = 0; t < 32; ++t) {
-            const uint64_t pos = w * 32 + t;
-            if (pos < vo || pos >= vo + nv) continue;
+    static_assert(GS_THREADS % 64 == 0, "whole waves");
+    auto spread = [](uint32_t x32) {  // bit t -> bit 2t
+        uint64_t x = x32;
+        x = (x | (x << 16)) & 0x0000FFFF0000FFFFull;
+        x = (x | (x << 8)) & 0x00FF00FF00FF00FFull;
+        x = (x | (x << 4)) & 0x0F0F0F0F0F0F0F0Full;
+        x = (x | (x << 2)) & 0x3333333333333333ull;
+        return (x | (x << 1)) & 0x5555555555555555ull;
+    };
+    for (uint64_t p0 = w0 * 32; p0 < w1 * 32; p0 += GS_THREADS) {  // (uniform)
+        const uint64_t pos = p0 + threadIdx.x;
+        uint32_t val = 0;
+        if (pos >= vo && pos < vo + nv) {
             const uint32_t v = (uint32_t)(pos - vo);
-            const uint32_t val = L.vowner[v] >= 0 ? (L.xval[v] ? L.xval[v] : 3u) : 0u;
-            word |= (uint64_t)val << (2 * t);
+            val = L.vowner[v] >= 0 ? (L.xval[v] ? L.xval[v] : 3u) : 0u;
         }
-        const bool inner = w * 32 >= vo && (w + 1) * 32 <= vo + nv;
-        if (inner) a.values[w] = word;
-        else if (word) atomicOr((unsigned long long *)(a.values + w), (unsigned long long)word);
+        const uint64_t pl = __builtin_amdgcn_ballot_w64((val & 1u) != 0), ph = __builtin_amdgcn_ballot_w64((val & 2u) != 0);
+        if ((threadIdx.x & 31) == 0) {
+            const uint64_t w = pos >> 5;
+            const uint32_t sh = threadIdx.x & 32;
+            const uint64_t word = spread((uint32_t)(pl >> sh)) | (spread((uint32_t)(ph >> sh)) << 1);
+            const bool inner = w * 32 >= vo && (w + 1) * 32 <= vo + nv;
+            if (w < w1) {
+                if (inner) a.values[w] = word;
+                else if (word) atomicOr((unsigned long long *)(a.values + w), (unsigned long long)word);
+            }
+        }
     }
     if (threadIdx.x == 0) a.E[b] |= (uint64_t)j << 56;
     if (a.width || a.rank_out || a.index_out) {
