@@ -613,9 +613,12 @@ __device__ __forceinline__ uint64_t readfirstlane64(uint64_t x) {
 }
 
 __device__ __forceinline__ void gf3_add(uint64_t &x1, uint64_t &x2, uint64_t y1, uint64_t y2) {
-    const uint64_t a1 = x1, a2 = x2;
-    x1 = (a1 & ~y1 & ~y2) | (~a1 & ~a2 & y1) | (a2 & y2);
-    x2 = (a2 & ~y1 & ~y2) | (~a1 & ~a2 & y2) | (a1 & y1);
+    // one-hot planes (x1 = [x == 1], x2 = [x == 2]); or/xor form, 7 VALU per
+    // 32-bit half (the and/or/not form took 9-12)
+    const uint64_t t = (x1 | y2) ^ (x2 | y1);
+    const uint64_t s1 = (x2 | y2) ^ t, s2 = (x1 | y1) ^ t;
+    x1 = s1;
+    x2 = s2;
 }
 
 // The single-wave phases (greedy and BFS orientation, the Tarjan walk, the
