@@ -75,6 +75,9 @@ constexpr int GS_TINY = 12;      // brute-force buckets (only in sets of < ~1500
 __host__ __device__ constexpr size_t gj_panel_words(uint32_t n) {
     return (size_t)(GOV_THREADS / 64) * 5 + (size_t)4 * 64 + (size_t)2 * 32 * 9;  // slots, pinfo, the pair table
 }
+#ifndef GOV_GREEDY_ROUNDS
+#define GOV_GREEDY_ROUNDS 1  // greedy: a chunk's overlapping lanes decided in rounds (0: one at a time)
+#endif
 #ifndef GOV_GREEDY_CHUNK
 #define GOV_GREEDY_CHUNK 64  // core edges the greedy orientation takes a step (wave 0)
 #endif
@@ -930,6 +933,42 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
                 atomicSub(&ccnt[v2], 1u);
             }
             uint64_t todo = __builtin_amdgcn_ballot_w64(ovl);
+#if GOV_GREEDY_ROUNDS
+            // the overlapping lanes in rounds: a lane no earlier lane still
+            // to decide shares a vertex with sees, after the previous rounds,
+            // every earlier effect on its vertices, so it decides now (the
+            // lanes of a round touch disjoint vertices); the rest wait
+            while (todo) {  // (wave-uniform)
+                const bool pend = ((todo >> tid) & 1ULL) != 0;
+                const uint32_t me2 = lane_tag | tid;
+                lane_tag -= 64;
+                if (pend) {
+                    atomicMin(&firstl[v0], me2);
+                    atomicMin(&firstl[v1], me2);
+                    atomicMin(&firstl[v2], me2);
+                }
+                __builtin_amdgcn_wave_barrier();
+                const bool wait = pend && (firstl[v0] < me2 || firstl[v1] < me2 || firstl[v2] < me2);
+                if (pend && !wait) {
+                    f0 = L.vowner[v0] < 0;
+                    f1 = L.vowner[v1] < 0;
+                    f2 = L.vowner[v2] < 0;
+                    c0 = ccnt[v0];
+                    c1 = ccnt[v1];
+                    c2 = ccnt[v2];
+                    chosen = pick(f0, f1, f2, c0, c1, c2, v0, v1, v2);
+                    if (chosen >= 0) {
+                        L.vowner[chosen] = (int16_t)k;
+                        L.hinge[k] = (int16_t)chosen;
+                    }
+                    atomicSub(&ccnt[v0], 1u);
+                    atomicSub(&ccnt[v1], 1u);
+                    atomicSub(&ccnt[v2], 1u);
+                }
+                todo = __builtin_amdgcn_ballot_w64(wait);
+                __builtin_amdgcn_wave_barrier();
+            }
+#else
             if (todo) {  // (wave-uniform)
                 __builtin_amdgcn_wave_barrier();
                 if (ovl) {  // the independent lanes' choices and decrements (all earlier, see above)
@@ -966,6 +1005,7 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
                     atomicSub(&ccnt[v2], 1u);
                 }
             }
+#endif
             __builtin_amdgcn_wave_barrier();
         }
         // the counts' words become the BFS's stamps
@@ -1062,13 +1102,15 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
             if (lane == 0) {
                 int k = found_e, v = found_v;
                 for (;;) {
-                    const int old = L.hinge[k];
+                    // (both reads of a step issued before its writes: one
+                    // LDS round trip a step)
+                    const int old = L.hinge[k], up = bfs_prev[k];
                     L.hinge[k] = (int16_t)v;
                     L.vowner[v] = (int16_t)k;
                     ++nflip;
                     if (k == (int)k0) break;
                     v = old;
-                    k = bfs_prev[k];
+                    k = up;
                 }
             }
             if (pc.on()) flip_cyc += clock64() - tf;
@@ -2026,6 +2068,10 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
                         // 7.3e6 -> 8.4e6 selection cycles.)
                         // (the next dependent read beside a step's atomics:
                         // no change, C2 gov 114.5 vs 114.5 ms, not kept)
+                        // (flattened: the batch's dependents spread over the
+                        // lanes by a ballot prefix sum, 64 a step: selection
+                        // 3.52e6 -> 3.61e6 cycles, not kept -- a batch's
+                        // members have few dependents each)
                         for (uint32_t x = x0;; ++x) {
                             const bool act = x < x1;
                             if (__builtin_amdgcn_ballot_w64(act) == 0) break;
