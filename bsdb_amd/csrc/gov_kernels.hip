@@ -1040,7 +1040,12 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
         for (;;) {
             while (!pendm && base < cnt) {
                 const uint32_t k = base + lane;
-                pendm = __builtin_amdgcn_ballot_w64(k < cnt && L.round_of[k] < 0 && L.hinge[k] < 0);
+                bool un = false;
+                if (k < cnt) {  // (both words read in one round trip)
+                    const int ro = L.round_of[k], hi = L.hinge[k];
+                    un = (ro < 0) & (hi < 0);
+                }
+                pendm = __builtin_amdgcn_ballot_w64(un);
                 base += 64;
             }
             if (!pendm || !ok) break;
@@ -1789,11 +1794,18 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
                                 pinfo[4 * ce + 3] = d2;
                                 piv[64 * wc + ce] = (int16_t)p;
                                 // (publishing every 2 or 4 columns: no change, not kept)
-                                __hip_atomic_store(&flags[16], seq << 16 | (ce + 1), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                                // LDS operations of a wave are performed in
+                                // the order it issues them, so the progress
+                                // word lands after the pivot's words without
+                                // a release wait for them; the signal fence
+                                // keeps the compiler from reordering the stores
+                                __atomic_signal_fence(__ATOMIC_SEQ_CST);
+                                __hip_atomic_store(&flags[16], seq << 16 | (ce + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                             }
                             apply(bit, q1, q2, d1, d2, p);
                         }
-                        if (lane == 0) __hip_atomic_store(&flags[16], seq << 16 | 0x8000u | ce, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        __atomic_signal_fence(__ATOMIC_SEQ_CST);
+                        if (lane == 0) __hip_atomic_store(&flags[16], seq << 16 | 0x8000u | ce, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                         crit_off();
                         pc.add_any(GP_GJ_LEAD, pc.now() - tl0);
                         pc.add_any(GP_GJ_LEADCOLS, ce - cl);
