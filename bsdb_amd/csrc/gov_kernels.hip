@@ -75,6 +75,9 @@ constexpr int GS_TINY = 12;      // brute-force buckets (only in sets of < ~1500
 __host__ __device__ constexpr size_t gj_panel_words(uint32_t n) {
     return (size_t)(GOV_THREADS / 64) * 5 + (size_t)4 * 64 + (size_t)2 * 32 * 9;  // slots, pinfo, the pair table
 }
+#ifndef GOV_BFS_BRANCHFREE
+#define GOV_BFS_BRANCHFREE 1  // BFS rounds without exec-mask branches (dead-word stores)
+#endif
 #ifndef GOV_GREEDY_ROUNDS
 #define GOV_GREEDY_ROUNDS 1  // greedy: a chunk's overlapping lanes decided in rounds (0: one at a time)
 #endif
@@ -1064,10 +1067,21 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
                 const uint32_t ch = min(21u, qt - qh);
                 const bool act = lane < 3 * ch;
                 const uint32_t ei = lane / 3, vi = lane - 3 * ei;
-                int k = 0, o = -1;
-                uint32_t v = 0, sn = 0;
                 const uint32_t me = lane_tag | lane;
                 lane_tag -= 64;
+#if GOV_BFS_BRANCHFREE
+                // every lane reads (a lane past the chunk reads its last
+                // edge) and the lanes past it aim their atomic and stores at
+                // a dead word of their own: no exec-mask branches in a round
+                uint32_t *const dead = L.hbin;  // (the FVS pick's bins: dead until the selection, which clears them)
+                const int k = queue[qh + min(ei, ch - 1)];
+                const uint32_t v = L.e[3 * k + vi];
+                const uint32_t sn = seen[v];
+                const int o = L.vowner[v];
+                atomicMin(act ? &first_lane[v] : &dead[lane], me);
+#else
+                int k = 0, o = -1;
+                uint32_t v = 0, sn = 0;
                 if (act) {
                     k = queue[qh + ei];
                     v = L.e[3 * k + vi];
@@ -1075,6 +1089,7 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
                     o = L.vowner[v];
                     atomicMin(&first_lane[v], me);
                 }
+#endif
                 __builtin_amdgcn_wave_barrier();
                 // (the root's iteration without the queue read and the
                 // atomics, duplicates compared in registers: BFS +2 %, not kept)
@@ -1083,12 +1098,22 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
                 const uint32_t F = fb ? (uint32_t)__builtin_ctzll(fb) : 64u;
                 const bool take = valid && lane < F;  // (o >= 0 below F)
                 const uint64_t tb = __builtin_amdgcn_ballot_w64(take);
+#if GOV_BFS_BRANCHFREE
+                {
+                    const uint32_t pos = qt + __builtin_amdgcn_mbcnt_hi((uint32_t)(tb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)tb, 0u));
+                    int16_t *const dead16 = reinterpret_cast<int16_t *>(dead);
+                    *(valid && lane <= F ? &seen[v] : &dead[lane]) = epoch;
+                    *(take ? &bfs_prev[o] : &dead16[lane]) = (int16_t)k;
+                    *(take ? &queue[pos] : &dead16[64 + lane]) = (int16_t)o;
+                }
+#else
                 if (valid && lane <= F) seen[v] = epoch;
                 if (take) {
                     const uint32_t pos = qt + __builtin_amdgcn_mbcnt_hi((uint32_t)(tb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)tb, 0u));
                     bfs_prev[o] = (int16_t)k;
                     queue[pos] = (int16_t)o;
                 }
+#endif
                 qt += (uint32_t)__builtin_popcountll(tb);
                 qh += ch;
                 npops += ch;
