@@ -75,6 +75,15 @@ constexpr int GS_TINY = 12;      // brute-force buckets (only in sets of < ~1500
 __host__ __device__ constexpr size_t gj_panel_words(uint32_t n) {
     return (size_t)(GOV_THREADS / 64) * 5 + (size_t)4 * 64 + (size_t)2 * 32 * 9;  // slots, pinfo, the pair table
 }
+#ifndef GOV_GREEDY_BRANCHFREE
+#define GOV_GREEDY_BRANCHFREE 1  // greedy steps without exec-mask branches (dead-word stores)
+#endif
+#ifndef GOV_SWEEP_INNER
+#define GOV_SWEEP_INNER 1  // SCC reach sweeps: rounds of reads and marks per barrier (2: half the barriers, sweeps -13 %, the solve unchanged; not kept)
+#endif
+#ifndef GOV_CLOSURE_BRANCHFREE
+#define GOV_CLOSURE_BRANCHFREE 1  // FVS closure batches without exec-mask branches (dead-word stores)
+#endif
 #ifndef GOV_BFS_BRANCHFREE
 #define GOV_BFS_BRANCHFREE 1  // BFS rounds without exec-mask branches (dead-word stores)
 #endif
@@ -886,6 +895,21 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
         };
         // a chunk's edges and vertices are read one chunk ahead (neither
         // changes here), so a chunk starts at its ownership reads
+#if GOV_GREEDY_BRANCHFREE
+        // (every lane reads -- a lane past the edges reads edge 0 -- and the
+        // lanes with nothing to do aim their atomics and stores at a dead
+        // word of their own: no exec-mask branches in a step)
+        uint32_t *const dead = L.hbin;  // (dead until the FVS selection, which clears them)
+        int16_t *const dead16 = reinterpret_cast<int16_t *>(dead);
+        auto chunk_edges = [&](uint32_t k, bool &a, uint32_t &u0, uint32_t &u1, uint32_t &u2) {
+            const uint32_t kc = k < cnt ? k : 0u;
+            const int ro = L.round_of[kc];
+            u0 = L.e[3 * kc];
+            u1 = L.e[3 * kc + 1];
+            u2 = L.e[3 * kc + 2];
+            a = k < cnt && ro < 0;
+        };
+#else
         auto chunk_edges = [&](uint32_t k, bool &a, uint32_t &u0, uint32_t &u1, uint32_t &u2) {
             a = k < cnt && L.round_of[k] < 0;
             u0 = u1 = u2 = 0;
@@ -895,6 +919,7 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
                 u2 = L.e[3 * k + 2];
             }
         };
+#endif
         bool nact;
         uint32_t n0, n1, n2;
         // GOV_GREEDY_CHUNK edges a step (lanes above it idle): fewer lanes
@@ -911,6 +936,66 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
             bool f0 = false, f1 = false, f2 = false;
             const uint32_t me = lane_tag | tid;
             lane_tag -= 64;
+#if GOV_GREEDY_BRANCHFREE
+            // decide: the lane's choice (or none) and its decrements, stores
+            // aimed at the dead words unless `on`
+            auto decide = [&](bool on, int &ch) {
+                f0 = L.vowner[v0] < 0;
+                f1 = L.vowner[v1] < 0;
+                f2 = L.vowner[v2] < 0;
+                c0 = ccnt[v0];
+                c1 = ccnt[v1];
+                c2 = ccnt[v2];
+                const int c = pick(f0, f1, f2, c0, c1, c2, v0, v1, v2);
+                const bool st = on && c >= 0;
+                *(st ? &L.vowner[c < 0 ? 0 : c] : &dead16[tid]) = (int16_t)k;
+                *(st ? &L.hinge[k] : &dead16[64 + tid]) = (int16_t)c;
+                atomicSub(on ? &ccnt[v0] : &dead[tid], 1u);
+                atomicSub(on ? &ccnt[v1] : &dead[tid], 1u);
+                atomicSub(on ? &ccnt[v2] : &dead[tid], 1u);
+                if (on) ch = c;
+            };
+            // (the first step's reads come before any of its stores: the
+            // ownership and counts every lane sees are the chunk's start)
+            f0 = L.vowner[v0] < 0;
+            f1 = L.vowner[v1] < 0;
+            f2 = L.vowner[v2] < 0;
+            c0 = ccnt[v0];
+            c1 = ccnt[v1];
+            c2 = ccnt[v2];
+            atomicMin(act ? &firstl[v0] : &dead[tid], me);
+            atomicMin(act ? &firstl[v1] : &dead[tid], me);
+            atomicMin(act ? &firstl[v2] : &dead[tid], me);
+            __builtin_amdgcn_wave_barrier();
+            const bool ovl = act && (firstl[v0] < me || firstl[v1] < me || firstl[v2] < me);
+            int chosen = -1;
+            {
+                const bool on = act && !ovl;
+                const int c = pick(f0, f1, f2, c0, c1, c2, v0, v1, v2);
+                const bool st = on && c >= 0;
+                *(st ? &L.vowner[c < 0 ? 0 : c] : &dead16[tid]) = (int16_t)k;
+                *(st ? &L.hinge[k] : &dead16[64 + tid]) = (int16_t)c;
+                atomicSub(on ? &ccnt[v0] : &dead[tid], 1u);
+                atomicSub(on ? &ccnt[v1] : &dead[tid], 1u);
+                atomicSub(on ? &ccnt[v2] : &dead[tid], 1u);
+                if (on) chosen = c;
+            }
+            uint64_t todo = __builtin_amdgcn_ballot_w64(ovl);
+            while (todo) {  // (wave-uniform) the overlapping lanes in rounds, as below
+                const bool pend = ((todo >> tid) & 1ULL) != 0;
+                const uint32_t me2 = lane_tag | tid;
+                lane_tag -= 64;
+                atomicMin(pend ? &firstl[v0] : &dead[tid], me2);
+                atomicMin(pend ? &firstl[v1] : &dead[tid], me2);
+                atomicMin(pend ? &firstl[v2] : &dead[tid], me2);
+                __builtin_amdgcn_wave_barrier();
+                const bool wait = pend && (firstl[v0] < me2 || firstl[v1] < me2 || firstl[v2] < me2);
+                decide(pend && !wait, chosen);
+                todo = __builtin_amdgcn_ballot_w64(wait);
+                __builtin_amdgcn_wave_barrier();
+            }
+            (void)chosen;
+#else
             if (act) {
                 f0 = L.vowner[v0] < 0;
                 f1 = L.vowner[v1] < 0;
@@ -1008,6 +1093,7 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
                     atomicSub(&ccnt[v2], 1u);
                 }
             }
+#endif
 #endif
             __builtin_amdgcn_wave_barrier();
         }
@@ -1264,7 +1350,14 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
 #pragma unroll
             for (int i = 0; i < 3; ++i) dk[j][i] = core ? (int)L.dep[3 * k + i] : -1;
         }
+        // GOV_SWEEP_INNER rounds a barrier: a round's reads see this
+        // thread's earlier marks and whatever other threads' marks have
+        // landed, so a barrier covers up to that many levels; the marks only
+        // grow, so the fixpoint (F, B) is the same, and a barrier interval
+        // in which no thread marks anything ends the sweeps
         for (;;) {
+          int ch = 0;
+          for (uint32_t inner = 0; inner < GOV_SWEEP_INNER; ++inner) {
             uint32_t fk[KPT], fw[KPT][3];
 #pragma unroll
             for (uint32_t j = 0; j < KPT; ++j) {
@@ -1273,7 +1366,6 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
 #pragma unroll
                 for (int i = 0; i < 3; ++i) fw[j][i] = dk[j][i] >= 0 ? fb((uint32_t)dk[j][i]) : 0u;
             }
-            int ch = 0;
 #pragma unroll
             for (uint32_t j = 0; j < KPT; ++j) {
                 uint32_t nk = fk[j];
@@ -1292,6 +1384,7 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
                     ch = 1;
                 }
             }
+          }
             pc.add(GP_N_SCC_SWEEPS, 1);
             if (!__syncthreads_or(ch)) break;
         }
@@ -2085,6 +2178,27 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
                         ++nbatch;
                         const uint32_t nb = min(64u, qt - qh);
                         uint32_t x0 = 0, x1 = 0, myl = 0;
+#if GOV_CLOSURE_BRANCHFREE
+                        // (every lane reads -- a lane past the batch reads its
+                        // last member -- and the lanes with nothing to do aim
+                        // their atomics and stores at a dead word of their own)
+                        uint32_t *const dead = L.hbin;  // (the pick's bins: cleared by each pick before use)
+                        int16_t *const dead16 = reinterpret_cast<int16_t *>(dead);
+                        {
+                            const bool inb = lane < nb;
+                            const uint32_t p = (uint32_t)queue[qh + min(lane, nb - 1)];
+                            const int d0 = idep[3 * p], d1 = idep[3 * p + 1], d2 = idep[3 * p + 2];
+                            x0 = roff[p];
+                            x1 = inb ? roff[p + 1] : x0;
+                            const uint32_t pp = pend[p], lp = lvl[p];
+                            atomicSub(inb && d0 >= 0 ? &indeg[d0] : &dead[lane], 1u);
+                            atomicSub(inb && d1 >= 0 ? &indeg[d1] : &dead[lane], 1u);
+                            atomicSub(inb && d2 >= 0 ? &indeg[d2] : &dead[lane], 1u);
+                            // (a heavy member's lvl may have been raised
+                            // while it waited in the queue: its level is 0)
+                            myl = pp >= 0x100u ? 1u : lp + 1;
+                        }
+#else
                         if (lane < nb) {
                             const uint32_t p = (uint32_t)queue[qh + lane];
                             for (int t = 0; t < 3; ++t) {
@@ -2097,6 +2211,7 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
                             // while it waited in the queue: its level is 0)
                             myl = pend[p] >= 0x100u ? 1u : lvl[p] + 1;
                         }
+#endif
                         // the batch's dependents, one per lane per step; the
                         // members they make ready are appended in lane order
                         // by ballot (the ready closure, the levels and so the
@@ -2109,6 +2224,19 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
                         // lanes by a ballot prefix sum, 64 a step: selection
                         // 3.52e6 -> 3.61e6 cycles, not kept -- a batch's
                         // members have few dependents each)
+#if GOV_CLOSURE_BRANCHFREE
+                        for (uint32_t x = x0;; ++x) {
+                            const bool act = x < x1;
+                            if (__builtin_amdgcn_ballot_w64(act) == 0) break;
+                            const uint32_t i = (uint32_t)rev(act ? x : 0u);
+                            atomicMax(act ? &lvl[i] : &dead[lane], myl);
+                            const bool ready = atomicSub(act ? &pend[i] : &dead[lane], 1u) == 1u && act;  // its last slot
+                            const uint64_t rm = __builtin_amdgcn_ballot_w64(ready);
+                            const uint32_t pos = qt + __builtin_amdgcn_mbcnt_hi((uint32_t)(rm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)rm, 0u));
+                            *(ready ? &queue[pos] : &dead16[64 + lane]) = (int16_t)i;
+                            qt += (uint32_t)__builtin_popcountll(rm);
+                        }
+#else
                         for (uint32_t x = x0;; ++x) {
                             const bool act = x < x1;
                             if (__builtin_amdgcn_ballot_w64(act) == 0) break;
@@ -2124,6 +2252,7 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
                                 queue[qt + __builtin_amdgcn_mbcnt_hi((uint32_t)(rm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)rm, 0u))] = (int16_t)i;
                             qt += (uint32_t)__builtin_popcountll(rm);
                         }
+#endif
                         qh += nb;
                         __builtin_amdgcn_wave_barrier();
                     }
