@@ -78,6 +78,9 @@ __host__ __device__ constexpr size_t gj_panel_words(uint32_t n) {
 #ifndef GOV_GREEDY_BRANCHFREE
 #define GOV_GREEDY_BRANCHFREE 1  // greedy steps without exec-mask branches (dead-word stores)
 #endif
+#ifndef GOV_BACK_NOBARRIER
+#define GOV_BACK_NOBARRIER 0  // peeled edges solved as their vertices become final, no barrier per round (back -23 %, the solve +0.3 %: more spills; not kept)
+#endif
 #ifndef GOV_SWEEP_INNER
 #define GOV_SWEEP_INNER 1  // SCC reach sweeps: rounds of reads and marks per barrier (2: half the barriers, sweeps -13 %, the solve unchanged; not kept)
 #endif
@@ -2762,6 +2765,52 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
     if (!uni(L.flag)) return false;
 
     // ---- 4. peeled edges, last round first
+#if GOV_BACK_NOBARRIER
+    // An edge's value needs only its other vertices' final values (hinges of
+    // edges peeled in later rounds, core hinges, or free vertices = 0), so
+    // no barrier per round: a peeled edge's hinge is marked pending, and each
+    // wave retries its lanes' pending edges until they are solved, reading
+    // the other waves' results as they land (LDS, no caching).  The later
+    // rounds' edges are always ready, so every retry makes progress; the
+    // values are those of the rounds in order.
+    {
+        constexpr uint8_t PEND = 0x80u;
+        for (uint32_t k = tid; k < cnt; k += GS_THREADS)
+            if (L.round_of[k] >= 0) L.xval[L.hinge[k]] = PEND;
+        __syncthreads();
+        volatile uint8_t *xv = L.xval;
+        constexpr uint32_t KPT = (Lds::CMAX + GS_THREADS - 1) / GS_THREADS;
+        uint32_t todo = 0;  // bit j: edge tid + j * GS_THREADS still to solve
+        for (uint32_t j = 0; j < KPT && tid + j * GS_THREADS < cnt; ++j)
+            if (L.round_of[tid + j * GS_THREADS] >= 0) todo |= 1u << j;
+        static_assert(KPT <= 32, "edges a thread");
+        while (__builtin_amdgcn_ballot_w64(todo != 0)) {  // (the wave's own loop)
+            for (uint32_t j = 0; j < KPT; ++j) {
+                if (!((todo >> j) & 1u)) continue;
+                const uint32_t k = tid + j * GS_THREADS;
+                const uint32_t hg = (uint32_t)L.hinge[k];
+                uint32_t s = 0, coef = 0, h = 3;
+                bool ready = true;
+                for (int i = 0; i < 3; ++i) {
+                    const uint32_t v = L.e[3 * k + i];
+                    if (v == hg) {
+                        ++coef;
+                        if (h == 3) h = (uint32_t)i;
+                    } else {
+                        const uint32_t x = xv[v];
+                        ready = ready && !(x & PEND);
+                        s += x;
+                    }
+                }
+                if (!ready) continue;
+                const uint32_t rhs = (h + 6 - s) % 3;
+                xv[hg] = (uint8_t)(coef == 1 ? rhs : (2 * rhs) % 3);
+                todo &= ~(1u << j);
+            }
+        }
+        __syncthreads();
+    }
+#else
     for (int rr = rounds - 1; rr >= 0; --rr) {
         for (uint32_t k = tid; k < cnt; k += GS_THREADS) {
             if (L.round_of[k] != rr) continue;
@@ -2777,6 +2826,8 @@ __device__ __forceinline__ bool try_seed(Lds &L, const ulonglong2 *sig, uint32_t
         }
         __syncthreads();
     }
+#endif
+    (void)rounds;
     pc.lap(GP_BACK);
     return true;
 }
