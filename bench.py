@@ -20,6 +20,7 @@ import argparse
 import json
 import os
 import sys
+import threading
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -517,6 +518,8 @@ def main():
     ap.add_argument("--e4-keys", type=int, default=0,
                     help="N>1: keys of the E4 full-build leg over the ranks (0 = C4's per-GPU share x N)")
     ap.add_argument("--e4-reps", type=int, default=1, help="N>1: timed reps of the E4 leg (after one warm rep)")
+    ap.add_argument("--e4-timeout", type=float, default=900.0,
+                    help="N>1: seconds the E4 leg may take before every rank abandons it (the line is still printed)")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="collective backend (nccl = RCCL over xGMI; gloo only to rehearse N ranks on one GPU)")
     args = ap.parse_args()
@@ -732,25 +735,8 @@ def main():
         if not args.no_cpu:
             full["cpu_c1"] = full_build_cpu(1_000_000, 4, args.cpu_threads)
         log("full-build figures done")
-    if world > 1 and not args.no_full_build:
-        # the product's full build at N ranks (E4) beside the histogram stage;
-        # every rank joins, rank 0 reports (after the headline's keys are freed)
-        del keys
-        torch.cuda.empty_cache()
-        ctx.release_workspace()
-        n_e4 = args.e4_keys if args.e4_keys > 0 else -(-README_N * world // 8)
-        full = {}
-        try:
-            full["e4_ranks_full_build"] = e4_ranks_full_build(ctx, world, rank, args.backend, 4, args.e4_reps, n_e4)
-        except Exception as e:  # recorded, not faked; the headline line is printed regardless
-            full["e4_ranks_full_build"] = {"error": repr(e)[:300]}
-        log("E4 full build over the ranks done")
-    if rank == 0:
-        cpu = None
-        if not args.no_cpu and world == 1:  # the CPU baseline is an N = 1 figure
-            cpu = cpu_baseline(m, args.cpu_seconds, args.cpu_threads)
-            log("cpu baseline done")
-        line = {
+    def make_line(cpu, full):
+        return {
             "metric": "index-build keys/s (device-resident), 13B x 13-byte keys; % HBM roofline",
             "value": value,
             "unit": "keys/s",
@@ -788,7 +774,48 @@ def main():
             "full_build": full,
             "check": {"E[m]==n": ok},
         }
-        print(json.dumps(line), flush=True)
+
+    if world > 1 and not args.no_full_build:
+        # the product's full build at N ranks (E4) beside the histogram stage;
+        # every rank joins, rank 0 reports (after the headline's keys are freed)
+        del keys
+        torch.cuda.empty_cache()
+        ctx.release_workspace()
+        n_e4 = args.e4_keys if args.e4_keys > 0 else -(-README_N * world // 8)
+        full = {}
+        # A rank that fails inside the leg leaves the others waiting in a
+        # collective: a watchdog on every rank abandons the leg after
+        # --e4-timeout seconds, rank 0 printing the line (the histogram
+        # stage's figures, the leg recorded as timed out) before every rank
+        # exits, so a failed leg never costs the headline's line.
+        e4_done = threading.Event()
+        emitted = threading.Lock()
+
+        def e4_watchdog():
+            if e4_done.wait(args.e4_timeout):
+                return
+            if rank == 0 and emitted.acquire(blocking=False):
+                full["e4_ranks_full_build"] = {"error": f"abandoned after {args.e4_timeout:.0f} s: a rank did not finish the leg"}
+                print(json.dumps(make_line(None, full)), flush=True)
+            os._exit(0)
+
+        threading.Thread(target=e4_watchdog, daemon=True).start()
+        try:
+            full["e4_ranks_full_build"] = e4_ranks_full_build(ctx, world, rank, args.backend, 4, args.e4_reps, n_e4)
+        except Exception as e:  # recorded, not faked; the headline line is printed regardless
+            full["e4_ranks_full_build"] = {"error": repr(e)[:300]}
+        e4_done.set()
+        log("E4 full build over the ranks done")
+        if rank == 0 and not emitted.acquire(blocking=False):
+            return  # (the watchdog printed the line as the leg ended)
+        if rank == 0:
+            emitted.release()
+    if rank == 0:
+        cpu = None
+        if not args.no_cpu and world == 1:  # the CPU baseline is an N = 1 figure
+            cpu = cpu_baseline(m, args.cpu_seconds, args.cpu_threads)
+            log("cpu baseline done")
+        print(json.dumps(make_line(cpu, full)), flush=True)
     if "keys" in locals():
         del keys
     ctx.close()
